@@ -1,0 +1,246 @@
+"""Benchmark: galah finch precluster path on MI355X.
+
+Metric (BASELINE.json): precluster genome-pairs/sec at 10k genomes (s=1000)
++ sketch Gbases/s.  Workload = config C3: 10,000 synthetic
+3 Mbp genomes in clusters of 10 (member substitution rate ~ U(0, 0.07)),
+k=21, s=1000, min_ani = 0.95 (f32, as parse_percentage(95) yields).
+
+One step = the whole precluster hot path over inputs already resident in
+HBM (2-bit packed genomes):
+  K1 sketch this rank's genome shard  ->  RCCL all_gather of the sketches
+  (N > 1)  ->  K2 all-pairs over this rank's share of the upper-triangle
+  tiles  ->  D2H of the passing (i, j, common, total) tuples.
+value = N(N-1)/2 genome pairs / step time (max over ranks).  Total work is
+fixed as the GPU count grows, so scaling is "strong".
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+import galah_amd as ga  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+LDS_PEAK_GBS = 256 * 128 * 2.4  # 256 CU x 128 B/clk (ds_read_b32 rate) x 2.4 GHz, GB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--genomes", type=int, default=10000)
+    ap.add_argument("--genome-len", type=int, default=3000000)
+    ap.add_argument("--cluster", type=int, default=10)
+    ap.add_argument("--max-sub", type=float, default=0.07)
+    ap.add_argument("--min-ani", type=float, default=95.0, help="--precluster-ani (percent)")
+    ap.add_argument("--sketch", type=int, default=1000)
+    ap.add_argument("--k", type=int, default=21)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(words_dev, runs, glen, sk_all, lens_all, k, s, min_ani, n_total, budget_s):
+    """The CPU oracle (oracle/, a C restatement of finch as galah calls it)
+    timed on this host on a bounded sample, extrapolated to the workload:
+    sketching parallel over genomes on T threads (finch sketch_files is a
+    rayon par_iter over files), the pair loop serial as src/finch.rs:53."""
+    import concurrent.futures as cf
+
+    import oracle
+    T = max(1, min(16, os.cpu_count() or 1))
+    # -- sketch sample: T genomes, one per thread
+    n_s = min(T, len(runs))
+    words = words_dev[: (n_s * glen) // 16].cpu().numpy().view(np.uint32)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    seqs = []
+    for g in range(n_s):
+        w = words[g * glen // 16:(g + 1) * glen // 16]
+        codes = (w[:, None] >> (np.uint32(30) - 2 * np.arange(16, dtype=np.uint32))[None, :]) & np.uint32(3)
+        seqs.append(acgt[codes.reshape(-1)].tobytes())
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(T) as ex:
+        outs = list(ex.map(lambda q: oracle.sketch_sequence(q, k=k, s=s), seqs))
+    t_sk = time.perf_counter() - t0
+    for g in range(n_s):  # the sample doubles as a parity spot check
+        assert (outs[g] == sk_all[g][:lens_all[g]]).all()
+    sketch_bases_per_s = n_s * glen / t_sk
+    # -- pair sample: the serial loop over the first m genomes' sketches
+    m = 200
+    while True:
+        t0 = time.perf_counter()
+        oracle.pairs(sk_all[:m], lens_all[:m].astype(np.int32), min_ani, k=k, cap=m * m)
+        t_p = time.perf_counter() - t0
+        if t_p > budget_s / 4 or m >= min(2000, n_total):
+            break
+        m = min(min(2000, n_total), int(m * max(1.5, (budget_s / 4 / max(t_p, 1e-3)) ** 0.5)))
+    pair_rate = m * (m - 1) / 2 / t_p
+    npairs = n_total * (n_total - 1) / 2
+    t_total = n_total * glen / sketch_bases_per_s + npairs / pair_rate
+    return {
+        "value": npairs / t_total, "unit": "genome-pairs/s", "cores": T, "kind": "port",
+        "sample": ("oracle/ C restatement of finch on %d host threads: sketched %d x %d bp synthetic genomes "
+                   "(%.1f Mbases/s), serial pair loop (1 core, src/finch.rs:53) over %d genomes' sketches "
+                   "(%.0f pairs/s); extrapolated to %d genomes = %.0f s"
+                   % (T, n_s, glen, sketch_bases_per_s / 1e6, m, pair_rate, n_total, t_total)),
+        "sketch_mbases_per_s": sketch_bases_per_s / 1e6,
+        "pair_rate_1core": pair_rate,
+    }
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    N, glen, s = a.genomes, a.genome_len, a.sketch
+    assert N % world == 0, "genome count must divide by the GPU count"
+    n_loc = N // world
+    g0 = rank * n_loc
+    min_ani = ga.parse_percentage(a.min_ani)
+    ctx = ga.Context(k=a.k, sketch_size=s, seed=0, device=local)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+
+    # inputs resident in HBM: this rank's genome shard, 2-bit packed
+    d_words = torch.empty(n_loc * glen // 16, dtype=torch.int32, device="cuda")
+    runs = ctx.synth_device(n_loc, glen, a.cluster, a.max_sub, a.seed, d_words, stream=sh, first_genome=g0)
+    d_sk_loc = torch.empty((n_loc, s), dtype=torch.int64, device="cuda")
+    d_len_loc = torch.empty(n_loc, dtype=torch.int32, device="cuda")
+    if world > 1:
+        d_sk = torch.empty((N, s), dtype=torch.int64, device="cuda")
+        d_len = torch.empty(N, dtype=torch.int32, device="cuda")
+    else:
+        d_sk, d_len = d_sk_loc, d_len_loc
+    tb, te = ga.pair_partition(N, world, rank)
+    cap = max(1 << 22, N * 64)
+    d_out = torch.empty(cap * 4, dtype=torch.int32, device="cuda")
+    d_cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    torch.cuda.synchronize()
+
+    ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for k in ("sketch", "gather", "pairs")}
+
+    def step():
+        ev["sketch"][0].record(stream)
+        ctx.sketch_device(d_words, runs, n_loc, d_sk_loc, d_len_loc, stream=sh)
+        ev["sketch"][1].record(stream)
+        ev["gather"][0].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(d_sk, d_sk_loc)
+            dist.all_gather_into_tensor(d_len, d_len_loc)
+        ev["gather"][1].record(stream)
+        d_cnt.zero_()
+        ev["pairs"][0].record(stream)
+        ctx.pairs_device(d_sk, d_len, N, tb, te, min_ani, d_out, cap, d_cnt, stream=sh)
+        ev["pairs"][1].record(stream)
+        cnt = int(d_cnt.item())
+        if cnt > cap:
+            raise RuntimeError("pair buffer too small: %d > %d" % (cnt, cap))
+        host = d_out[: cnt * 4].cpu()  # sparse results to host
+        return cnt, host
+
+    for _ in range(a.warmup):
+        step()
+    phase = {k: 0.0 for k in ev}
+    ctx.timing_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    found = 0
+    for _ in range(a.steps):
+        found, _host = step()
+        torch.cuda.synchronize()
+        for k, (e0, e1) in ev.items():
+            phase[k] += e0.elapsed_time(e1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kst = {name: ctx.timing_read(kid) for name, kid in
+           (("sketch", ga.KERNEL_SKETCH), ("finalize", ga.KERNEL_FINALIZE), ("pairs", ga.KERNEL_PAIRS))}
+    ctx.timing_enable(False)
+    t = torch.tensor([elapsed, phase["sketch"], phase["pairs"], phase["gather"], float(found)],
+                     dtype=torch.float64, device="cuda")
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+    else:
+        tmax = tsum = t
+    elapsed_max = float(tmax[0])
+    ms_step = elapsed_max / a.steps * 1e3
+    npairs = N * (N - 1) // 2
+    value = npairs / (elapsed_max / a.steps)
+    total_bases = N * glen
+
+    # roofline of the dominant kernel, from this rank's per-launch events
+    sk_ms = kst["sketch"]["ms"] / max(1, kst["sketch"]["launches"])
+    pr_ms = kst["pairs"]["ms"] / max(1, kst["pairs"]["launches"])
+    kmers_per_launch = kst["sketch"]["work"] / max(1, kst["sketch"]["launches"])
+    pairs_per_launch = kst["pairs"]["work"] / max(1, kst["pairs"]["launches"])
+    k1 = {"kernel": "sketch_candidates_kernel<21>", "bound": "hbm", "unit": "GB/s",
+          "achieved": kmers_per_launch * 0.25 / (sk_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+          "avg_ms": sk_ms, "work_per_launch": kmers_per_launch,
+          "note": "algorithmic bytes = 0.25 B per k-mer position (2-bit input read once)"}
+    k2 = {"kernel": "pairs_merge_kernel", "bound": "lds", "unit": "GB/s",
+          "achieved": pairs_per_launch * 16.0 * s / (pr_ms * 1e-3) / 1e9, "peak": LDS_PEAK_GBS,
+          "avg_ms": pr_ms, "work_per_launch": pairs_per_launch,
+          "note": "algorithmic bytes = 8 B x (|A|+|B|) = 16 KB per pair at s=1000"}
+    dom = k1 if sk_ms * kst["sketch"]["launches"] >= pr_ms * kst["pairs"]["launches"] else k2
+    roof = {"bound": dom["bound"], "achieved": round(dom["achieved"], 3), "peak": dom["peak"],
+            "unit": dom["unit"], "frac": round(dom["achieved"] / dom["peak"], 5), "traffic": None,
+            "kernel": dom["kernel"], "avg_launch_ms": round(dom["avg_ms"], 4), "note": dom["note"],
+            "other_kernels": [{kk: (round(v, 5) if isinstance(v, float) else v) for kk, v in x.items()}
+                              for x in (k1, k2) if x is not dom]}
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        sk_h = d_sk.cpu().numpy().view(np.uint64)
+        ln_h = d_len.cpu().numpy().view(np.uint32)
+        cpu = cpu_baseline(d_words, runs, glen, sk_h, ln_h, a.k, s, min_ani, N, a.cpu_budget_s)
+
+    if rank == 0:
+        line = {
+            "metric": "precluster genome-pairs/sec at 10k genomes (s=1000) + sketch Gbases/s",
+            "value": round(value, 1), "unit": "genome-pairs/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic clustered genomes generated on device (no network)",
+            "config": {"workload": "C3: %d synthetic genomes x %d bp, clusters of %d, sub rate U(0,%.2f), "
+                                   "k=%d, s=%d, min_ani=%s" % (N, glen, a.cluster, a.max_sub, a.k, s, min_ani),
+                       "genomes": N, "genome_len": glen, "sketch_size": s, "k": a.k,
+                       "min_ani": float(min_ani), "parallelism": "dp%d" % world},
+            "sketch_gbases_per_s": round(total_bases / (float(tmax[1]) / a.steps * 1e-3) / 1e9, 3),
+            "pairs_kernel_pairs_per_s": round(npairs / (float(tmax[2]) / a.steps * 1e-3), 1),
+            "phase_ms": {"sketch": round(float(tmax[1]) / a.steps, 3), "allgather": round(float(tmax[3]) / a.steps, 3),
+                         "pairs": round(float(tmax[2]) / a.steps, 3)},
+            "pairs_found": int(tsum[4]) if world > 1 else found,
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,461 @@
+"""galah_amd -- MI355X-native finch MinHash precluster path for galah.
+
+Python host mirror of the reference interface for this path, over the C ABI
+of libgalahgpu.so (include/galahgpu.h):
+
+  reference (AroneyS/galah @ 2024-12-18)              here
+  src/lib.rs:23-27     trait PreclusterDistanceFinder  PreclusterDistanceFinder
+  src/finch.rs:4-24    struct FinchPreclusterer        FinchPreclusterer
+  src/finch.rs:26-75   finch::distances                distances()
+  src/sorted_pair_genome_distance_cache.rs:4-59        SortedPairGenomeDistanceCache
+  src/cluster_argument_parsing.rs:1160-1182            parse_percentage()
+
+There is no CPU fallback: importing works without a GPU (so the ABI can be
+inspected), but every compute call needs a gfx950 device and raises
+GalahGpuError otherwise.  The library must have been built in-tree
+(`make -C galah_amd/csrc` or __graft_entry__.build()); a missing library is
+an ImportError, never a silent substitute.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+__all__ = [
+    "GalahGpuError", "Context", "Packed", "pack_files", "pack_records",
+    "ani_f32", "ani_f64", "parse_percentage", "pair_tiles", "pair_partition",
+    "SortedPairGenomeDistanceCache", "PreclusterDistanceFinder",
+    "FinchPreclusterer", "distances", "PAIR_DTYPE", "LIB_PATH", "EXPORTED_SYMBOLS",
+]
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libgalahgpu.so")
+
+PAIR_DTYPE = np.dtype([("i", np.uint32), ("j", np.uint32), ("common", np.uint32), ("total", np.uint32)])
+
+# every function include/galahgpu.h declares
+EXPORTED_SYMBOLS = (
+    "gg_abi_version", "gg_status_string", "gg_last_error", "gg_thread_last_error",
+    "gg_create", "gg_destroy", "gg_device",
+    "gg_pack_files", "gg_pack_records", "gg_packed_free",
+    "gg_sketch", "gg_sketch_device",
+    "gg_pair_tiles", "gg_pair_partition", "gg_pairs", "gg_pairs_device",
+    "gg_precluster_files", "gg_ani_f64", "gg_ani_f32", "gg_parse_percentage",
+    "gg_free", "gg_synth_clustered_device", "gg_timing_enable", "gg_timing_read",
+)
+
+GG_OK = 0
+GG_ERR_NO_DEVICE = 4
+
+
+class GalahGpuError(RuntimeError):
+    def __init__(self, status, message):
+        super().__init__("%s (status %d)" % (message, status))
+        self.status = status
+
+
+class _Run(ctypes.Structure):
+    _fields_ = [("genome", ctypes.c_uint32), ("len", ctypes.c_uint32), ("base", ctypes.c_uint64)]
+
+
+class _Packed(ctypes.Structure):
+    _fields_ = [("words", ctypes.POINTER(ctypes.c_uint32)), ("n_words", ctypes.c_uint64),
+                ("n_bases", ctypes.c_uint64), ("runs", ctypes.POINTER(_Run)), ("n_runs", ctypes.c_uint64),
+                ("n_genomes", ctypes.c_uint32), ("genome_kmers", ctypes.POINTER(ctypes.c_uint64))]
+
+
+RUN_DTYPE = np.dtype([("genome", np.uint32), ("len", np.uint32), ("base", np.uint64)])
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError("libgalahgpu.so is not built (%s); run `make -C galah_amd/csrc` "
+                      "or __graft_entry__.build()" % LIB_PATH)
+
+_L = ctypes.CDLL(LIB_PATH)
+_vp = ctypes.c_void_p
+_u32, _u64, _i32 = ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+
+
+def _sig(name, res, args):
+    f = getattr(_L, name)
+    f.restype = res
+    f.argtypes = args
+
+
+_sig("gg_abi_version", _u32, [])
+_sig("gg_status_string", ctypes.c_char_p, [_i32])
+_sig("gg_last_error", ctypes.c_char_p, [_vp])
+_sig("gg_thread_last_error", ctypes.c_char_p, [])
+_sig("gg_create", _vp, [_i32, _u32, _u64, _i32, ctypes.POINTER(_i32)])
+_sig("gg_destroy", None, [_vp])
+_sig("gg_device", _i32, [_vp])
+_sig("gg_pack_files", _i32, [ctypes.POINTER(ctypes.c_char_p), _u32, _i32, _i32, ctypes.POINTER(ctypes.POINTER(_Packed))])
+_sig("gg_pack_records", _i32, [ctypes.POINTER(_vp), _vp, _vp, _u64, _u32, _i32, ctypes.POINTER(ctypes.POINTER(_Packed))])
+_sig("gg_packed_free", None, [ctypes.POINTER(_Packed)])
+_sig("gg_sketch", _i32, [_vp, ctypes.POINTER(_Packed), _vp, _vp])
+_sig("gg_sketch_device", _i32, [_vp, _vp, _u64, _vp, _u64, _u32, _vp, _vp, _vp])
+_sig("gg_pair_tiles", _u64, [_u32])
+_sig("gg_pair_partition", None, [_u32, _u32, _u32, ctypes.POINTER(_u64), ctypes.POINTER(_u64)])
+_sig("gg_pairs", _i32, [_vp, _vp, _vp, _u32, ctypes.c_float, ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
+_sig("gg_pairs_device", _i32, [_vp, _vp, _vp, _u32, _u64, _u64, ctypes.c_float, _vp, _u64, _vp, _vp])
+_sig("gg_precluster_files", _i32, [_vp, ctypes.POINTER(ctypes.c_char_p), _u32, ctypes.c_float,
+                                   ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
+_sig("gg_ani_f64", ctypes.c_double, [_u32, _u32, _i32])
+_sig("gg_ani_f32", ctypes.c_float, [_u32, _u32, _i32])
+_sig("gg_parse_percentage", _i32, [ctypes.c_float, ctypes.POINTER(ctypes.c_float)])
+_sig("gg_free", None, [_vp])
+_sig("gg_synth_clustered_device", _i32, [_vp, _u32, _u32, _u32, _u32, ctypes.c_float, _u64, _vp, _vp, _vp])
+
+
+class _KStats(ctypes.Structure):
+    _fields_ = [("ms", ctypes.c_double), ("launches", ctypes.c_uint64), ("work", ctypes.c_uint64)]
+
+
+_sig("gg_timing_enable", _i32, [_vp, _i32])
+_sig("gg_timing_read", _i32, [_vp, _i32, ctypes.POINTER(_KStats)])
+KERNEL_SKETCH, KERNEL_FINALIZE, KERNEL_PAIRS = 0, 1, 2
+
+
+def lib():
+    """The loaded ctypes handle of libgalahgpu.so."""
+    return _L
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_vp)
+
+
+def _thread_err(st):
+    return GalahGpuError(st, _L.gg_thread_last_error().decode(errors="replace"))
+
+
+def abi_version():
+    return _L.gg_abi_version()
+
+
+def ani_f64(common, total, k=21):
+    """src/finch.rs:56-64: 1 - finch mash_distance (f64)."""
+    return _L.gg_ani_f64(common, total, k)
+
+
+def ani_f32(common, total, k=21):
+    """The stored value, Some(ani as f32) (src/finch.rs:70)."""
+    return np.float32(_L.gg_ani_f32(common, total, k))
+
+
+def parse_percentage(value):
+    """CAP:1160-1182 for --precluster-ani: [1,100] -> /100 in f32,
+    [0,1) kept, anything else is an error."""
+    out = ctypes.c_float()
+    st = _L.gg_parse_percentage(ctypes.c_float(value), ctypes.byref(out))
+    if st != GG_OK:
+        raise ValueError(_L.gg_thread_last_error().decode())
+    return np.float32(out.value)
+
+
+def pair_tiles(n):
+    return _L.gg_pair_tiles(n)
+
+
+def pair_partition(n, parts, part):
+    b, e = _u64(), _u64()
+    _L.gg_pair_partition(n, parts, part, ctypes.byref(b), ctypes.byref(e))
+    return b.value, e.value
+
+
+class Packed:
+    """2-bit packed genomes (gg_packed), owned by the library."""
+
+    def __init__(self, ptr):
+        self._p = ptr
+        p = ptr.contents
+        self.n_words = p.n_words
+        self.n_bases = p.n_bases
+        self.n_runs = p.n_runs
+        self.n_genomes = p.n_genomes
+        self.words = np.ctypeslib.as_array(p.words, shape=(max(p.n_words, 1),))[:p.n_words]
+        runs_buf = (ctypes.c_char * (max(p.n_runs, 1) * RUN_DTYPE.itemsize)).from_address(
+            ctypes.addressof(p.runs.contents))
+        self.runs = np.frombuffer(runs_buf, dtype=RUN_DTYPE)[:p.n_runs]
+        self.genome_kmers = np.ctypeslib.as_array(p.genome_kmers, shape=(max(p.n_genomes, 1),))[:p.n_genomes]
+
+    def free(self):
+        if self._p:
+            _L.gg_packed_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        self.free()
+
+
+def pack_files(paths, k=21, threads=0):
+    arr = (ctypes.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+    out = ctypes.POINTER(_Packed)()
+    st = _L.gg_pack_files(arr, len(paths), k, threads, ctypes.byref(out))
+    if st != GG_OK:
+        raise _thread_err(st)
+    return Packed(out)
+
+
+def pack_records(genomes, k=21):
+    """genomes: list (per genome) of lists of record byte strings."""
+    recs, gid = [], []
+    for g, rs in enumerate(genomes):
+        for r in rs:
+            recs.append(bytes(r))
+            gid.append(g)
+    bufs = [ctypes.create_string_buffer(r, len(r) + 1) for r in recs]
+    seqs = (_vp * max(len(recs), 1))(*[ctypes.cast(b, _vp) for b in bufs])
+    lens = np.array([len(r) for r in recs] or [0], dtype=np.uint64)
+    gids = np.array(gid or [0], dtype=np.uint32)
+    out = ctypes.POINTER(_Packed)()
+    st = _L.gg_pack_records(seqs, _ptr(lens), _ptr(gids), len(recs), len(genomes), k, ctypes.byref(out))
+    if st != GG_OK:
+        raise _thread_err(st)
+    return Packed(out)
+
+
+def _take_pairs(ptr, n):
+    if n == 0:
+        _L.gg_free(ptr)
+        return np.zeros(0, dtype=PAIR_DTYPE)
+    buf = (ctypes.c_char * (n * PAIR_DTYPE.itemsize)).from_address(ptr.value)
+    out = np.frombuffer(buf, dtype=PAIR_DTYPE).copy()
+    _L.gg_free(ptr)
+    return out
+
+
+def _dev_ptr(t):
+    """Device pointer of a torch tensor or an int."""
+    return t if isinstance(t, int) else t.data_ptr()
+
+
+class Context:
+    """A gg_ctx: one HIP device, fixed k / sketch size / seed."""
+
+    def __init__(self, k=21, sketch_size=1000, seed=0, device=-1):
+        st = _i32()
+        self._c = _L.gg_create(k, sketch_size, seed, device, ctypes.byref(st))
+        if not self._c:
+            raise _thread_err(st.value)
+        self.k, self.s, self.seed = k, sketch_size, seed
+
+    def close(self):
+        if getattr(self, "_c", None):
+            _L.gg_destroy(self._c)
+            self._c = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _err(self, st):
+        return GalahGpuError(st, _L.gg_last_error(self._c).decode(errors="replace"))
+
+    @property
+    def device(self):
+        return _L.gg_device(self._c)
+
+    def timing_enable(self, on=True):
+        st = _L.gg_timing_enable(self._c, 1 if on else 0)
+        if st != GG_OK:
+            raise self._err(st)
+
+    def timing_read(self, kernel):
+        """-> dict(ms, launches, work) summed since timing_enable."""
+        k = _KStats()
+        st = _L.gg_timing_read(self._c, kernel, ctypes.byref(k))
+        if st != GG_OK:
+            raise self._err(st)
+        return {"ms": k.ms, "launches": k.launches, "work": k.work}
+
+    # -- host-buffer API -------------------------------------------------
+    def sketch(self, packed):
+        """-> (sketches [n_genomes, s] u64 padded with 0, lens [n] u32)."""
+        ng = packed.n_genomes
+        out = np.zeros((max(ng, 1), self.s), dtype=np.uint64)
+        lens = np.zeros(max(ng, 1), dtype=np.uint32)
+        st = _L.gg_sketch(self._c, packed._p, _ptr(out), _ptr(lens))
+        if st != GG_OK:
+            raise self._err(st)
+        return out[:ng], lens[:ng]
+
+    def pairs(self, sketches, lens, min_ani):
+        sk = np.ascontiguousarray(sketches, dtype=np.uint64)
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = ln.shape[0]
+        if n and sk.shape != (n, self.s):
+            raise ValueError("sketches must be [n, sketch_size]")
+        outp, cnt = _vp(), _u64()
+        st = _L.gg_pairs(self._c, _ptr(sk), _ptr(ln), n, ctypes.c_float(min_ani), ctypes.byref(outp),
+                         ctypes.byref(cnt))
+        if st != GG_OK:
+            raise self._err(st)
+        return _take_pairs(outp, cnt.value)
+
+    def precluster_files(self, paths, min_ani):
+        """-> (pairs structured array sorted by (i, j), ani f32 array)."""
+        arr = (ctypes.c_char_p * max(len(paths), 1))(*[os.fsencode(p) for p in paths])
+        pp, ap, cnt = _vp(), _vp(), _u64()
+        st = _L.gg_precluster_files(self._c, arr, len(paths), ctypes.c_float(min_ani), ctypes.byref(pp),
+                                    ctypes.byref(ap), ctypes.byref(cnt))
+        if st != GG_OK:
+            raise self._err(st)
+        n = cnt.value
+        if n:
+            ani = np.ctypeslib.as_array(ctypes.cast(ap, ctypes.POINTER(ctypes.c_float)), shape=(n,)).copy()
+        else:
+            ani = np.zeros(0, np.float32)
+        _L.gg_free(ap)
+        return _take_pairs(pp, n), ani
+
+    # -- device-resident API (torch tensors on this context's device) ---------
+    def sketch_device(self, d_words, runs, n_genomes, d_out, d_lens, stream=None):
+        runs = np.ascontiguousarray(runs, dtype=RUN_DTYPE)
+        st = _L.gg_sketch_device(self._c, _dev_ptr(d_words), d_words.numel(), _ptr(runs), len(runs),
+                                 n_genomes, _dev_ptr(d_out), _dev_ptr(d_lens),
+                                 None if stream is None else stream)
+        if st != GG_OK:
+            raise self._err(st)
+
+    def pairs_device(self, d_sketches, d_lens, n, tile_begin, tile_end, min_ani, d_out, out_cap, d_count,
+                     stream=None):
+        st = _L.gg_pairs_device(self._c, _dev_ptr(d_sketches), _dev_ptr(d_lens), n, tile_begin, tile_end,
+                                ctypes.c_float(min_ani), _dev_ptr(d_out), out_cap, _dev_ptr(d_count),
+                                None if stream is None else stream)
+        if st != GG_OK:
+            raise self._err(st)
+
+    def synth_device(self, n_genomes, genome_len, cluster_size, max_sub_rate, seed, d_words, stream=None,
+                     first_genome=0):
+        runs = np.zeros(n_genomes, dtype=RUN_DTYPE)
+        st = _L.gg_synth_clustered_device(self._c, first_genome, n_genomes, genome_len, cluster_size,
+                                          ctypes.c_float(max_sub_rate), seed, _dev_ptr(d_words), _ptr(runs),
+                                          None if stream is None else stream)
+        if st != GG_OK:
+            raise self._err(st)
+        return runs
+
+
+# ---------------------------------------------------------------------------
+# Reference-interface mirror
+# ---------------------------------------------------------------------------
+def _rust_f32_debug(x):
+    """Rust `{:?}` of an f32: shortest round-trip decimal, always with a '.'."""
+    s = np.format_float_positional(np.float32(x), unique=True, trim="-")
+    if "." not in s and "inf" not in s and "nan" not in s:
+        s += ".0"
+    return s
+
+
+class SortedPairGenomeDistanceCache:
+    """src/sorted_pair_genome_distance_cache.rs:4-59: a map keyed by (min, max)."""
+
+    def __init__(self):
+        self.internal = {}
+
+    @staticmethod
+    def _key(ids):
+        a, b = ids
+        return (a, b) if a < b else (b, a)
+
+    def insert(self, genome_ids, distance):
+        self.internal[self._key(genome_ids)] = distance
+
+    def get(self, genome_ids):
+        """Option<&Option<f32>>: KeyError-free; returns the stored value or the
+        sentinel `MISSING` when absent."""
+        return self.internal.get(self._key(genome_ids), MISSING)
+
+    def contains_key(self, genome_ids):
+        return self._key(genome_ids) in self.internal
+
+    def transform_ids(self, input_ids):
+        """:47-58 -- subset with ids re-numbered by position in input_ids."""
+        out = SortedPairGenomeDistanceCache()
+        for i, g1 in enumerate(input_ids):
+            for j in range(i + 1, len(input_ids)):
+                v = self.get((g1, input_ids[j]))
+                if v is not MISSING:
+                    out.insert((i, j), v)
+        return out
+
+    def __len__(self):
+        return len(self.internal)
+
+    def __eq__(self, other):
+        if not isinstance(other, SortedPairGenomeDistanceCache):
+            return NotImplemented
+        if self.internal.keys() != other.internal.keys():
+            return False
+        for k, v in self.internal.items():
+            w = other.internal[k]
+            if (v is None) != (w is None):
+                return False
+            if v is not None and np.float32(v) != np.float32(w):
+                return False
+        return True
+
+    def __repr__(self):
+        items = ", ".join(
+            "(%d, %d): %s" % (k[0], k[1], "None" if v is None else "Some(%s)" % _rust_f32_debug(v))
+            for k, v in sorted(self.internal.items()))
+        return "SortedPairGenomeDistanceCache { internal: {%s} }" % items
+
+
+MISSING = object()
+
+
+class PreclusterDistanceFinder:
+    """src/lib.rs:23-27."""
+
+    def distances(self, genome_fasta_paths):
+        raise NotImplementedError
+
+    def method_name(self):
+        raise NotImplementedError
+
+
+_CTX_CACHE = {}
+
+
+def _context(k, s, seed=0):
+    key = (k, s, seed)
+    c = _CTX_CACHE.get(key)
+    if c is None:
+        c = Context(k, s, seed)
+        _CTX_CACHE[key] = c
+    return c
+
+
+def distances(genome_fasta_paths, min_ani, num_kmers, kmer_length):
+    """src/finch.rs:26-75 -> SortedPairGenomeDistanceCache, computed on the GPU."""
+    try:
+        ctx = _context(int(kmer_length), int(num_kmers))
+        pairs, ani = ctx.precluster_files(list(genome_fasta_paths), float(np.float32(min_ani)))
+    except GalahGpuError as e:
+        # src/finch.rs:50
+        raise RuntimeError("Failed to sketch genomes with finch: %s" % e) from e
+    cache = SortedPairGenomeDistanceCache()
+    for p, a in zip(pairs, ani):
+        cache.insert((int(p["i"]), int(p["j"])), np.float32(a))
+    return cache
+
+
+class FinchPreclusterer(PreclusterDistanceFinder):
+    """src/finch.rs:4-24: min_ani is a fraction (f32), num_kmers = s, kmer_length = k."""
+
+    def __init__(self, min_ani, num_kmers=1000, kmer_length=21):
+        self.min_ani = np.float32(min_ani)
+        self.num_kmers = int(num_kmers)
+        self.kmer_length = int(kmer_length)
+
+    def distances(self, genome_fasta_paths):
+        return distances(genome_fasta_paths, self.min_ani, self.num_kmers, self.kmer_length)
+
+    def method_name(self):
+        return "finch"

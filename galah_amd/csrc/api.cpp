@@ -1,0 +1,798 @@
+// Host runtime of libgalahgpu.so: context, device memory, the retry loop of
+// the bottom-s selection, the cmin threshold table, tile partitioning and
+// the C ABI declared in include/galahgpu.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "gg_internal.hpp"
+
+struct gg_ctx {
+  int k = 21;
+  uint32_t s = 1000;
+  uint64_t seed = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // grow-only device scratch, keyed by purpose
+  std::map<std::string, std::pair<void*, size_t>> scratch;
+  // cached cmin table
+  float cmin_key = -1.0f;
+  std::vector<uint32_t> cmin_host;
+  // per-kernel timing (gg_timing_enable)
+  struct Timed {
+    int kernel;
+    hipEvent_t a, b;
+    uint64_t work;
+  };
+  bool timing = false;
+  std::vector<Timed> timed;
+  std::vector<hipEvent_t> spare_events;
+};
+
+namespace gg {
+
+thread_local std::string g_thread_err;
+
+void set_thread_error(const std::string& msg) { g_thread_err = msg; }
+
+namespace {
+
+gg_status fail(gg_ctx* c, gg_status st, const std::string& msg) {
+  if (c) c->err = msg;
+  set_thread_error(msg);
+  return st;
+}
+
+gg_status hip_fail(gg_ctx* c, hipError_t e, const char* what) {
+  return fail(c, e == hipErrorOutOfMemory ? GG_ERR_OUT_OF_MEMORY : GG_ERR_HIP,
+              std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define GG_HIP(ctx, expr)                                   \
+  do {                                                      \
+    hipError_t _e = (expr);                                 \
+    if (_e != hipSuccess) return hip_fail((ctx), _e, #expr); \
+  } while (0)
+
+// Grow-only scratch buffer owned by the context.
+hipError_t scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
+  auto& e = c->scratch[key];
+  if (e.second < bytes) {
+    if (e.first) {
+      hipError_t err = hipFree(e.first);
+      if (err != hipSuccess) return err;
+      e.first = nullptr;
+      e.second = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 256);
+    hipError_t err = hipMalloc(&e.first, want);
+    if (err != hipSuccess) return err;
+    e.second = want;
+  }
+  *out = e.first;
+  return hipSuccess;
+}
+
+hipEvent_t take_event(gg_ctx* c) {
+  if (!c->spare_events.empty()) {
+    hipEvent_t e = c->spare_events.back();
+    c->spare_events.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Runs `launch` (which enqueues one kernel on st); when timing is enabled
+// brackets it with events recorded on the same stream.
+template <typename F>
+hipError_t timed_launch(gg_ctx* c, int kernel, uint64_t work, hipStream_t st, F&& launch) {
+  if (!c->timing) return launch();
+  hipEvent_t a = take_event(c), b = take_event(c);
+  if (!a || !b) return hipErrorOutOfMemory;
+  hipError_t e = hipEventRecord(a, st);
+  if (e != hipSuccess) return e;
+  e = launch();
+  if (e != hipSuccess) return e;
+  e = hipEventRecord(b, st);
+  if (e != hipSuccess) return e;
+  c->timed.push_back(gg_ctx::Timed{kernel, a, b, work});
+  return hipSuccess;
+}
+
+// Number of pairs (i < j < n) in tiles [tb, te).
+uint64_t pairs_in_tiles(uint32_t n, uint64_t tb, uint64_t te) {
+  const uint64_t nb = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
+  uint64_t t = 0, acc = 0;
+  for (uint64_t I = 0; I < nb && t < te; ++I) {
+    const uint64_t ri = std::min<uint64_t>(GG_PAIR_TILE, n - I * GG_PAIR_TILE);
+    const uint64_t row_tiles = nb - I;
+    if (t + row_tiles <= tb) {
+      t += row_tiles;
+      continue;
+    }
+    for (uint64_t J = I; J < nb && t < te; ++J, ++t) {
+      if (t < tb) continue;
+      const uint64_t cj = std::min<uint64_t>(GG_PAIR_TILE, n - J * GG_PAIR_TILE);
+      acc += (I == J) ? ri * (ri - 1) / 2 : ri * cj;
+    }
+  }
+  return acc;
+}
+
+template <typename T>
+hipError_t scratch_t(gg_ctx* c, const char* key, size_t count, T** out) {
+  void* p = nullptr;
+  hipError_t e = scratch(c, key, count * sizeof(T), &p);
+  *out = (T*)p;
+  return e;
+}
+
+inline double rust_min(double a, double b) {
+  if (std::isnan(a)) return b;
+  if (std::isnan(b)) return a;
+  return a < b ? a : b;
+}
+inline double rust_max(double a, double b) {
+  if (std::isnan(a)) return b;
+  if (std::isnan(b)) return a;
+  return a > b ? a : b;
+}
+
+// Bottom-s selection geometry (see sketch.hip header).
+struct SketchGeom {
+  uint32_t limit;      // max distinct candidates per genome
+  uint32_t sort_pow2;  // LDS sort size (>= limit)
+  uint32_t cap_log2;   // per-genome set capacity = 2 * sort_pow2
+  double over;         // expected candidates = over * s
+};
+
+SketchGeom sketch_geom(uint32_t s) {
+  SketchGeom g;
+  g.limit = std::min<uint32_t>(kSortCap, std::max<uint32_t>(4 * s, 64));
+  g.sort_pow2 = 1;
+  while (g.sort_pow2 < g.limit) g.sort_pow2 <<= 1;
+  g.cap_log2 = 1;
+  while ((1u << g.cap_log2) < 2 * g.sort_pow2) ++g.cap_log2;
+  g.over = std::min(2.0, 0.8 * (double)g.limit / (double)s);
+  return g;
+}
+
+uint64_t initial_tau(uint64_t nk, uint32_t s, double over) {
+  const long double want = (long double)over * (long double)s;
+  if (nk == 0 || want >= (long double)nk) return kEmpty;
+  const long double t = want / (long double)nk * 18446744073709551616.0L;
+  if (t >= 18446744073709551615.0L) return kEmpty;
+  return (uint64_t)t;
+}
+
+struct TauSearch {
+  uint64_t tau;
+  uint64_t lo = 0;  // largest tau known to give fewer than s distinct
+  uint64_t hi = 0;  // smallest tau known to overflow
+  bool lo_known = false;
+  bool hi_known = false;
+  int steps = 0;
+};
+
+// Moves tau after a failed pass.  Exactness does not depend on where tau
+// ends up, only on every distinct hash <= tau being collected.  Returns
+// false when the search cannot continue (cannot happen for limit > s + 1:
+// the distinct count below tau grows by one value at a time).
+bool advance_tau(TauSearch& t, uint32_t status) {
+  if (++t.steps > 130) return false;
+  if (status == kSketchRetryLarger) {
+    t.lo = t.tau;
+    t.lo_known = true;
+    if (t.hi_known) t.tau = t.lo + (t.hi - t.lo) / 2;
+    else t.tau = (t.tau > kEmpty / 4) ? kEmpty : t.tau * 4 + 3;
+  } else {
+    t.hi = t.tau;
+    t.hi_known = true;
+    t.tau = t.lo + (t.hi - t.lo) / 2;
+  }
+  if (t.lo_known && t.hi_known && t.hi - t.lo <= 1) return false;
+  return true;
+}
+
+gg_status validate_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t n_genomes,
+                        uint64_t n_words) {
+  uint32_t prev = 0;
+  for (uint64_t r = 0; r < n_runs; ++r) {
+    const gg_run& x = runs[r];
+    if (x.genome >= n_genomes || x.genome < prev)
+      return fail(c, GG_ERR_INVALID_ARG, "runs must be grouped by non-decreasing genome < n_genomes");
+    if (x.len < (uint32_t)c->k)
+      return fail(c, GG_ERR_INVALID_ARG, "run shorter than k");
+    if (x.base + x.len > n_words * 16ull)
+      return fail(c, GG_ERR_INVALID_ARG, "run extends past the packed words");
+    prev = x.genome;
+  }
+  return GG_OK;
+}
+
+// Core of K1 over device-resident packed words; runs are host metadata.
+gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, const gg_run* runs,
+                      uint64_t n_runs, uint32_t n_genomes, uint64_t* d_out, uint32_t* d_lens,
+                      hipStream_t st) {
+  gg_status vs = validate_runs(c, runs, n_runs, n_genomes, n_words);
+  if (vs != GG_OK) return vs;
+  if (n_genomes == 0) return GG_OK;
+  const SketchGeom geom = sketch_geom(c->s);
+  const uint64_t cap = 1ull << geom.cap_log2;
+  // genomes per batch: tables limited to ~4 GiB
+  const uint32_t max_batch = (uint32_t)std::max<uint64_t>(
+      1, std::min<uint64_t>(n_genomes, (4ull << 30) / (cap * sizeof(uint64_t))));
+
+  // per-genome run ranges
+  std::vector<uint64_t> gr(n_genomes + 1, n_runs);
+  {
+    uint64_t r = 0;
+    for (uint32_t g = 0; g < n_genomes; ++g) {
+      while (r < n_runs && runs[r].genome < g) ++r;
+      gr[g] = r;
+    }
+    gr[n_genomes] = n_runs;
+  }
+
+  int n_cu = 256;
+  (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
+  const int grid = std::max(1, n_cu) * 8;
+
+  uint64_t* d_table;
+  uint32_t *d_count, *d_flags, *d_status, *d_slot_list, *d_slot_genome;
+  uint64_t* d_tau;
+  GG_HIP(c, scratch_t(c, "table", (size_t)max_batch * cap, &d_table));
+  GG_HIP(c, scratch_t(c, "count", max_batch, &d_count));
+  GG_HIP(c, scratch_t(c, "flags", max_batch, &d_flags));
+  GG_HIP(c, scratch_t(c, "status", max_batch, &d_status));
+  GG_HIP(c, scratch_t(c, "slot_list", max_batch, &d_slot_list));
+  GG_HIP(c, scratch_t(c, "slot_genome", max_batch, &d_slot_genome));
+  GG_HIP(c, scratch_t(c, "tau", max_batch, &d_tau));
+
+  for (uint32_t g0 = 0; g0 < n_genomes; g0 += max_batch) {
+    const uint32_t g1 = std::min(n_genomes, g0 + max_batch);
+    const uint32_t nb = g1 - g0;
+    std::vector<TauSearch> ts(nb);
+    std::vector<uint64_t> h_tau(nb);
+    std::vector<uint32_t> h_slot_genome(nb), h_slot_list(nb);
+    for (uint32_t i = 0; i < nb; ++i) {
+      uint64_t nk = 0;
+      for (uint64_t r = gr[g0 + i]; r < gr[g0 + i + 1]; ++r) nk += runs[r].len - c->k + 1;
+      ts[i].tau = initial_tau(nk, c->s, geom.over);
+      h_tau[i] = ts[i].tau;
+      h_slot_genome[i] = g0 + i;
+      h_slot_list[i] = i;
+    }
+    GG_HIP(c, hipMemcpyAsync(d_slot_genome, h_slot_genome.data(), nb * sizeof(uint32_t),
+                             hipMemcpyHostToDevice, st));
+
+    // active genome slots for this pass
+    std::vector<uint32_t> active = h_slot_list;
+    for (int pass = 0; !active.empty(); ++pass) {
+      if (pass > 200) return fail(c, GG_ERR_INTERNAL, "bottom-s threshold search did not converge");
+      // run table for the active genomes
+      std::vector<uint64_t> rb, rk;
+      std::vector<uint32_t> rs;
+      uint64_t kacc = 0;
+      for (uint32_t slot : active) {
+        const uint32_t g = g0 + slot;
+        for (uint64_t r = gr[g]; r < gr[g + 1]; ++r) {
+          rb.push_back(runs[r].base);
+          rk.push_back(kacc);
+          rs.push_back(slot);
+          kacc += runs[r].len - c->k + 1;
+        }
+      }
+      rk.push_back(kacc);
+      const uint32_t nr = (uint32_t)rs.size();
+      uint64_t *d_rb, *d_rk;
+      uint32_t* d_rs;
+      GG_HIP(c, scratch_t(c, "run_base", std::max<size_t>(nr, 1), &d_rb));
+      GG_HIP(c, scratch_t(c, "run_kstart", nr + 1, &d_rk));
+      GG_HIP(c, scratch_t(c, "run_slot", std::max<size_t>(nr, 1), &d_rs));
+      if (nr) {
+        GG_HIP(c, hipMemcpyAsync(d_rb, rb.data(), nr * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+        GG_HIP(c, hipMemcpyAsync(d_rs, rs.data(), nr * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+      }
+      GG_HIP(c, hipMemcpyAsync(d_rk, rk.data(), (nr + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+      GG_HIP(c, hipMemcpyAsync(d_tau, h_tau.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+      GG_HIP(c, hipMemcpyAsync(d_slot_list, active.data(), active.size() * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, st));
+      if (pass == 0) {
+        GG_HIP(c, hipMemsetAsync(d_table, 0xFF, (size_t)nb * cap * sizeof(uint64_t), st));
+        GG_HIP(c, hipMemsetAsync(d_count, 0, nb * sizeof(uint32_t), st));
+        GG_HIP(c, hipMemsetAsync(d_flags, 0, nb * sizeof(uint32_t), st));
+      } else {
+        for (uint32_t slot : active) {
+          GG_HIP(c, hipMemsetAsync(d_table + (uint64_t)slot * cap, 0xFF, cap * sizeof(uint64_t), st));
+          GG_HIP(c, hipMemsetAsync(d_count + slot, 0, sizeof(uint32_t), st));
+          GG_HIP(c, hipMemsetAsync(d_flags + slot, 0, sizeof(uint32_t), st));
+        }
+      }
+      SketchLaunch a;
+      a.words = d_words;
+      a.run_base = d_rb;
+      a.run_kstart = d_rk;
+      a.run_slot = d_rs;
+      a.n_runs = nr;
+      a.n_kmers = kacc;
+      a.tau = d_tau;
+      a.table = d_table;
+      a.cap_log2 = geom.cap_log2;
+      a.count = d_count;
+      a.limit = geom.limit;
+      a.flags = d_flags;
+      a.seed = c->seed;
+      const uint64_t segs = (kacc + 31) / 32;
+      const int g = (int)std::min<uint64_t>((uint64_t)grid, std::max<uint64_t>(1, (segs + 255) / 256));
+      GG_HIP(c, timed_launch(c, GG_KERNEL_SKETCH, kacc, st,
+                             [&] { return launch_sketch_candidates(c->k, a, g, st); }));
+      GG_HIP(c, timed_launch(c, GG_KERNEL_FINALIZE, active.size(), st, [&] {
+        return launch_sketch_finalize(d_slot_list, (uint32_t)active.size(), d_slot_genome, d_tau,
+                                      d_table, geom.cap_log2, d_count, d_flags, c->s,
+                                      geom.sort_pow2, d_out, d_lens, d_status, st);
+      }));
+      std::vector<uint32_t> status(nb);
+      GG_HIP(c, hipMemcpyAsync(status.data(), d_status, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      GG_HIP(c, hipStreamSynchronize(st));
+      std::vector<uint32_t> next;
+      for (uint32_t slot : active) {
+        if (status[slot] == kSketchOk) continue;
+        if (!advance_tau(ts[slot], status[slot]))
+          return fail(c, GG_ERR_INTERNAL, "bottom-s threshold search failed");
+        h_tau[slot] = ts[slot].tau;
+        next.push_back(slot);
+      }
+      active.swap(next);
+    }
+  }
+  return GG_OK;
+}
+
+gg_status ensure_cmin(gg_ctx* c, float min_ani, uint32_t** d_cmin, hipStream_t st) {
+  const uint32_t tmax = 2 * c->s;
+  GG_HIP(c, scratch_t(c, "cmin", tmax + 1, d_cmin));
+  if (c->cmin_key != min_ani || c->cmin_host.size() != tmax + 1) {
+    c->cmin_host = build_cmin(c->s, c->k, min_ani);
+    c->cmin_key = min_ani;
+  }
+  GG_HIP(c, hipMemcpyAsync(*d_cmin, c->cmin_host.data(), (tmax + 1) * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, st));
+  return GG_OK;
+}
+
+gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
+                     uint64_t tb, uint64_t te, float min_ani, gg_pair* d_out, uint64_t cap,
+                     uint64_t* d_count, hipStream_t st) {
+  uint32_t* d_cmin;
+  gg_status cs = ensure_cmin(c, min_ani, &d_cmin, st);
+  if (cs != GG_OK) return cs;
+  PairsLaunch a;
+  a.sketches = d_sk;
+  a.lens = d_lens;
+  a.n = n;
+  a.stride = c->s;
+  a.n_row_tiles = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
+  a.tile_begin = tb;
+  a.tile_end = std::min<uint64_t>(te, gg_pair_tiles(n));
+  a.cmin = d_cmin;
+  a.tmax = 2 * c->s;
+  a.out = d_out;
+  a.out_cap = cap;
+  a.count = (unsigned long long*)d_count;
+  const uint64_t work = c->timing ? pairs_in_tiles(n, a.tile_begin, a.tile_end) : 0;
+  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs(a, st); }));
+  return GG_OK;
+}
+
+// Device sketches -> sorted host pairs.
+gg_status pairs_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
+                        float min_ani, std::vector<gg_pair>& res, hipStream_t st) {
+  uint64_t* d_count;
+  GG_HIP(c, scratch_t(c, "pair_count", 1, &d_count));
+  uint64_t cap = std::max<uint64_t>(1 << 20, (uint64_t)n * 16);
+  const uint64_t all = (uint64_t)n * (n > 0 ? n - 1 : 0) / 2;
+  cap = std::min<uint64_t>(cap, std::max<uint64_t>(all, 1));
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    gg_pair* d_out;
+    GG_HIP(c, scratch_t(c, "pair_out", cap, &d_out));
+    GG_HIP(c, hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
+    gg_status ps = pairs_core(c, d_sk, d_lens, n, 0, gg_pair_tiles(n), min_ani, d_out, cap, d_count, st);
+    if (ps != GG_OK) return ps;
+    uint64_t cnt = 0;
+    GG_HIP(c, hipMemcpyAsync(&cnt, d_count, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(c, hipStreamSynchronize(st));
+    if (cnt <= cap) {
+      res.resize(cnt);
+      if (cnt) {
+        GG_HIP(c, hipMemcpyAsync(res.data(), d_out, cnt * sizeof(gg_pair), hipMemcpyDeviceToHost, st));
+        GG_HIP(c, hipStreamSynchronize(st));
+      }
+      std::sort(res.begin(), res.end(), [](const gg_pair& x, const gg_pair& y) {
+        return x.i != y.i ? x.i < y.i : x.j < y.j;
+      });
+      return GG_OK;
+    }
+    cap = cnt;
+  }
+  return fail(c, GG_ERR_INTERNAL, "pair output sizing failed");
+}
+
+template <typename T>
+T* copy_out(const std::vector<T>& v) {
+  T* p = (T*)malloc(std::max<size_t>(v.size(), 1) * sizeof(T));
+  if (p && !v.empty()) memcpy(p, v.data(), v.size() * sizeof(T));
+  return p;
+}
+
+}  // namespace
+
+double ani_f64(uint32_t common, uint32_t total, int k) {
+  // finch distance(): J = common/total; mash = -ln(2J/(1+J))/k clamped to
+  // [0,1] with f64::min / f64::max; galah: ani = 1 - mash (src/finch.rs:56)
+  const double jaccard = (double)common / (double)total;
+  double d = -1.0 * std::log((2.0 * jaccard) / (1.0 + jaccard)) / (double)k;
+  d = rust_max(rust_min(d, 1.0), 0.0);
+  return 1.0 - d;
+}
+
+std::vector<uint32_t> build_cmin(uint32_t s, int k, float min_ani) {
+  const uint32_t tmax = 2 * s;
+  const double thr = (double)min_ani;  // src/finch.rs:69: min_ani as f64
+  std::vector<uint32_t> cmin(tmax + 1, 0xFFFFFFFFu);
+  for (uint32_t t = 0; t <= tmax; ++t) {
+    const uint32_t cmax = std::min(t, s);
+    if (!(ani_f64(cmax, t, k) >= thr)) continue;  // nothing passes at this total
+    uint32_t lo = 0, hi = cmax;  // smallest c with ani(c,t) >= thr lies in [lo, hi]
+    if (ani_f64(0, t, k) >= thr) {
+      cmin[t] = 0;
+      continue;
+    }
+    while (hi - lo > 1) {
+      const uint32_t mid = lo + (hi - lo) / 2;
+      if (ani_f64(mid, t, k) >= thr) hi = mid;
+      else lo = mid;
+    }
+    cmin[t] = hi;
+  }
+  return cmin;
+}
+
+}  // namespace gg
+
+using namespace gg;
+
+// ----------------------------------------------------------------------------
+extern "C" {
+
+uint32_t gg_abi_version(void) { return GG_ABI_VERSION; }
+
+const char* gg_status_string(gg_status s) {
+  switch (s) {
+    case GG_OK: return "ok";
+    case GG_ERR_INVALID_ARG: return "invalid argument";
+    case GG_ERR_IO: return "I/O error";
+    case GG_ERR_FORMAT: return "format error";
+    case GG_ERR_NO_DEVICE: return "no usable gfx950 device";
+    case GG_ERR_HIP: return "HIP error";
+    case GG_ERR_OUT_OF_MEMORY: return "out of memory";
+    case GG_ERR_INTERNAL: return "internal error";
+    case GG_ERR_OUTPUT_FULL: return "output buffer full";
+  }
+  return "unknown status";
+}
+
+const char* gg_last_error(const gg_ctx* ctx) { return ctx ? ctx->err.c_str() : g_thread_err.c_str(); }
+const char* gg_thread_last_error(void) { return g_thread_err.c_str(); }
+
+gg_ctx* gg_create(int kmer_length, uint32_t sketch_size, uint64_t hash_seed, int device,
+                  gg_status* status) {
+  gg_status dummy;
+  if (!status) status = &dummy;
+  if (kmer_length < 1 || kmer_length > 32 || sketch_size < 1 || sketch_size > 12000) {
+    *status = fail(nullptr, GG_ERR_INVALID_ARG, "kmer_length must be 1..32 and sketch_size 1..12000");
+    return nullptr;
+  }
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    *status = fail(nullptr, GG_ERR_NO_DEVICE, "no HIP device visible (libgalahgpu has no CPU path)");
+    return nullptr;
+  }
+  int dev = device;
+  if (dev < 0 && hipGetDevice(&dev) != hipSuccess) dev = 0;
+  if (dev >= n) {
+    *status = fail(nullptr, GG_ERR_NO_DEVICE, "device ordinal out of range");
+    return nullptr;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+      strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    *status = fail(nullptr, GG_ERR_NO_DEVICE,
+                   std::string("device is not gfx950 (MI355X): ") + prop.gcnArchName);
+    return nullptr;
+  }
+  gg_ctx* c = new (std::nothrow) gg_ctx();
+  if (!c) {
+    *status = fail(nullptr, GG_ERR_OUT_OF_MEMORY, "out of host memory");
+    return nullptr;
+  }
+  c->k = kmer_length;
+  c->s = sketch_size;
+  c->seed = hash_seed;
+  c->device = dev;
+  hipError_t e = hipSetDevice(dev);
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  (void)e;
+  if (!c->stream) {
+    *status = fail(nullptr, GG_ERR_HIP, "stream creation failed");
+    delete c;
+    return nullptr;
+  }
+  *status = GG_OK;
+  return c;
+}
+
+void gg_destroy(gg_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->scratch)
+    if (kv.second.first) (void)hipFree(kv.second.first);
+  for (auto& t : ctx->timed) {
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
+  }
+  for (hipEvent_t e : ctx->spare_events) (void)hipEventDestroy(e);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int gg_device(const gg_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+gg_status gg_sketch_device(gg_ctx* ctx, const uint32_t* d_words, uint64_t n_words,
+                           const gg_run* runs, uint64_t n_runs, uint32_t n_genomes,
+                           uint64_t* d_out, uint32_t* d_lens, void* stream) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if ((n_runs && (!runs || !d_words)) || (n_genomes && (!d_out || !d_lens)))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_sketch_device: null buffer");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+  return sketch_core(ctx, d_words, n_words, runs, n_runs, n_genomes, d_out, d_lens, st);
+}
+
+gg_status gg_sketch(gg_ctx* ctx, const gg_packed* packed, uint64_t* out_hashes,
+                    uint32_t* out_lens) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (!packed || (packed->n_genomes && (!out_hashes || !out_lens)))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_sketch: null buffer");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
+  hipStream_t st = ctx->stream;
+  const uint32_t ng = packed->n_genomes;
+  if (ng == 0) return GG_OK;
+  uint32_t* d_words;
+  uint64_t* d_out;
+  uint32_t* d_lens;
+  GG_HIP(ctx, scratch_t(ctx, "in_words", std::max<uint64_t>(packed->n_words, 1), &d_words));
+  GG_HIP(ctx, scratch_t(ctx, "sk_out", (size_t)ng * ctx->s, &d_out));
+  GG_HIP(ctx, scratch_t(ctx, "sk_lens", ng, &d_lens));
+  if (packed->n_words)
+    GG_HIP(ctx, hipMemcpyAsync(d_words, packed->words, packed->n_words * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, st));
+  GG_HIP(ctx, hipMemsetAsync(d_out, 0, (size_t)ng * ctx->s * sizeof(uint64_t), st));
+  gg_status s = sketch_core(ctx, d_words, packed->n_words, packed->runs, packed->n_runs, ng, d_out,
+                            d_lens, st);
+  if (s != GG_OK) return s;
+  GG_HIP(ctx, hipMemcpyAsync(out_hashes, d_out, (size_t)ng * ctx->s * sizeof(uint64_t),
+                             hipMemcpyDeviceToHost, st));
+  GG_HIP(ctx, hipMemcpyAsync(out_lens, d_lens, ng * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  GG_HIP(ctx, hipStreamSynchronize(st));
+  return GG_OK;
+}
+
+uint64_t gg_pair_tiles(uint32_t n) {
+  const uint64_t nb = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
+  return nb * (nb + 1) / 2;
+}
+
+// First tile whose first pair index is >= target (pairs counted in tile
+// enumeration order); nt when none.
+static uint64_t tile_at_pair(uint32_t n, long double target) {
+  const uint64_t nb = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
+  uint64_t t = 0;
+  long double acc = 0;
+  for (uint64_t I = 0; I < nb; ++I) {
+    const uint64_t ri = std::min<uint64_t>(GG_PAIR_TILE, n - I * GG_PAIR_TILE);
+    for (uint64_t J = I; J < nb; ++J, ++t) {
+      if (acc >= target) return t;
+      const uint64_t cj = std::min<uint64_t>(GG_PAIR_TILE, n - J * GG_PAIR_TILE);
+      acc += (I == J) ? (long double)(ri * (ri - 1) / 2) : (long double)(ri * cj);
+    }
+  }
+  return t;
+}
+
+void gg_pair_partition(uint32_t n, uint32_t parts, uint32_t part, uint64_t* begin, uint64_t* end) {
+  if (!begin || !end) return;
+  const uint64_t nt = gg_pair_tiles(n);
+  if (parts == 0 || part >= parts) {
+    *begin = *end = nt;
+    return;
+  }
+  const long double all = (long double)n * (long double)(n ? n - 1 : 0) / 2.0L;
+  *begin = (part == 0) ? 0 : tile_at_pair(n, all * part / parts);
+  *end = (part + 1 == parts) ? nt : tile_at_pair(n, all * (part + 1) / parts);
+  if (*end < *begin) *end = *begin;
+}
+
+gg_status gg_pairs_device(gg_ctx* ctx, const uint64_t* d_sketches, const uint32_t* d_lens,
+                          uint32_t n, uint64_t tile_begin, uint64_t tile_end, float min_ani,
+                          gg_pair* d_out, uint64_t out_cap, uint64_t* d_count, void* stream) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (n && (!d_sketches || !d_lens || !d_count || (out_cap && !d_out)))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_pairs_device: null buffer");
+  if (std::isnan(min_ani)) return fail(ctx, GG_ERR_INVALID_ARG, "min_ani is NaN");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+  return pairs_core(ctx, d_sketches, d_lens, n, tile_begin, tile_end, min_ani, d_out, out_cap,
+                    d_count, st);
+}
+
+gg_status gg_pairs(gg_ctx* ctx, const uint64_t* sketches, const uint32_t* lens, uint32_t n,
+                   float min_ani, gg_pair** out, uint64_t* n_out) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (!out || !n_out || (n && (!sketches || !lens)))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_pairs: null buffer");
+  if (std::isnan(min_ani)) return fail(ctx, GG_ERR_INVALID_ARG, "min_ani is NaN");
+  *out = nullptr;
+  *n_out = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (lens[i] > ctx->s) return fail(ctx, GG_ERR_INVALID_ARG, "sketch longer than sketch_size");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
+  hipStream_t st = ctx->stream;
+  std::vector<gg_pair> res;
+  if (n >= 2) {
+    uint64_t* d_sk;
+    uint32_t* d_lens;
+    GG_HIP(ctx, scratch_t(ctx, "pin_sk", (size_t)n * ctx->s, &d_sk));
+    GG_HIP(ctx, scratch_t(ctx, "pin_lens", n, &d_lens));
+    GG_HIP(ctx, hipMemcpyAsync(d_sk, sketches, (size_t)n * ctx->s * sizeof(uint64_t),
+                               hipMemcpyHostToDevice, st));
+    GG_HIP(ctx, hipMemcpyAsync(d_lens, lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    gg_status s = pairs_to_host(ctx, d_sk, d_lens, n, min_ani, res, st);
+    if (s != GG_OK) return s;
+  }
+  *out = copy_out(res);
+  if (!*out) return fail(ctx, GG_ERR_OUT_OF_MEMORY, "out of host memory");
+  *n_out = res.size();
+  return GG_OK;
+}
+
+gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
+                              float min_ani, gg_pair** pairs, float** ani, uint64_t* n_out) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (!pairs || !ani || !n_out || (n_paths && !paths))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_precluster_files: null argument");
+  if (std::isnan(min_ani)) return fail(ctx, GG_ERR_INVALID_ARG, "min_ani is NaN");
+  *pairs = nullptr;
+  *ani = nullptr;
+  *n_out = 0;
+  gg_packed* pk = nullptr;
+  gg_status s = gg_pack_files(paths, n_paths, ctx->k, 0, &pk);
+  if (s != GG_OK) return fail(ctx, s, g_thread_err);
+  struct Free {
+    gg_packed* p;
+    ~Free() { gg_packed_free(p); }
+  } guard{pk};
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
+  hipStream_t st = ctx->stream;
+  const uint32_t ng = pk->n_genomes;
+  std::vector<gg_pair> res;
+  if (ng >= 2) {
+    uint32_t* d_words;
+    uint64_t* d_out;
+    uint32_t* d_lens;
+    GG_HIP(ctx, scratch_t(ctx, "in_words", std::max<uint64_t>(pk->n_words, 1), &d_words));
+    GG_HIP(ctx, scratch_t(ctx, "sk_out", (size_t)ng * ctx->s, &d_out));
+    GG_HIP(ctx, scratch_t(ctx, "sk_lens", ng, &d_lens));
+    if (pk->n_words)
+      GG_HIP(ctx, hipMemcpyAsync(d_words, pk->words, pk->n_words * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, st));
+    GG_HIP(ctx, hipMemsetAsync(d_out, 0, (size_t)ng * ctx->s * sizeof(uint64_t), st));
+    s = sketch_core(ctx, d_words, pk->n_words, pk->runs, pk->n_runs, ng, d_out, d_lens, st);
+    if (s != GG_OK) return s;
+    s = pairs_to_host(ctx, d_out, d_lens, ng, min_ani, res, st);
+    if (s != GG_OK) return s;
+  }
+  std::vector<float> a(res.size());
+  for (size_t i = 0; i < res.size(); ++i) a[i] = gg_ani_f32(res[i].common, res[i].total, ctx->k);
+  *pairs = copy_out(res);
+  *ani = copy_out(a);
+  if (!*pairs || !*ani) {
+    free(*pairs);
+    free(*ani);
+    *pairs = nullptr;
+    *ani = nullptr;
+    return fail(ctx, GG_ERR_OUT_OF_MEMORY, "out of host memory");
+  }
+  *n_out = res.size();
+  return GG_OK;
+}
+
+double gg_ani_f64(uint32_t common, uint32_t total, int kmer_length) {
+  return ani_f64(common, total, kmer_length);
+}
+
+float gg_ani_f32(uint32_t common, uint32_t total, int kmer_length) {
+  return (float)ani_f64(common, total, kmer_length);
+}
+
+gg_status gg_parse_percentage(float value, float* fraction) {
+  if (!fraction) return fail(nullptr, GG_ERR_INVALID_ARG, "null output");
+  float p = value;
+  if (p >= 1.0f && p <= 100.0f) {
+    p /= 100.0f;
+  } else if (!(p >= 0.0f && p <= 100.0f)) {
+    char buf[96];
+    snprintf(buf, sizeof buf, "Invalid percentage specified for --precluster-ani: '%g'", (double)value);
+    return fail(nullptr, GG_ERR_INVALID_ARG, buf);
+  }
+  *fraction = p;
+  return GG_OK;
+}
+
+void gg_free(void* p) { free(p); }
+
+gg_status gg_timing_enable(gg_ctx* ctx, int on) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  for (auto& t : ctx->timed) {
+    (void)hipEventSynchronize(t.b);
+    ctx->spare_events.push_back(t.a);
+    ctx->spare_events.push_back(t.b);
+  }
+  ctx->timed.clear();
+  ctx->timing = on != 0;
+  return GG_OK;
+}
+
+gg_status gg_timing_read(gg_ctx* ctx, int kernel, gg_kernel_stats* out) {
+  if (!ctx || !out || kernel < 0 || kernel >= GG_KERNEL_COUNT)
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_timing_read: bad argument");
+  gg_kernel_stats s{0.0, 0, 0};
+  for (auto& t : ctx->timed) {
+    if (t.kernel != kernel) continue;
+    GG_HIP(ctx, hipEventSynchronize(t.b));
+    float ms = 0.f;
+    GG_HIP(ctx, hipEventElapsedTime(&ms, t.a, t.b));
+    s.ms += ms;
+    s.launches += 1;
+    s.work += t.work;
+  }
+  *out = s;
+  return GG_OK;
+}
+
+gg_status gg_synth_clustered_device(gg_ctx* ctx, uint32_t first_genome, uint32_t n_genomes, uint32_t genome_len,
+                                    uint32_t cluster_size, float max_sub_rate, uint64_t seed,
+                                    uint32_t* d_words, gg_run* runs, void* stream) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (!d_words || !runs || genome_len % 16 || genome_len < (uint32_t)ctx->k || cluster_size == 0)
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_synth_clustered_device: bad arguments");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
+  hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+  GG_HIP(ctx, launch_synth(first_genome, n_genomes, genome_len, cluster_size, max_sub_rate, seed, d_words, st));
+  for (uint32_t g = 0; g < n_genomes; ++g) runs[g] = gg_run{g, genome_len, (uint64_t)g * genome_len};
+  return GG_OK;
+}
+
+}  // extern "C"

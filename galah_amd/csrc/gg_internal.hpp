@@ -1,0 +1,88 @@
+// Internal declarations shared by the host runtime (api.cpp, pack.cpp) and
+// the kernels (sketch.hip, pairs.hip, synth.hip) of libgalahgpu.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/galahgpu.h"
+
+namespace gg {
+
+constexpr uint64_t kEmpty = ~0ull;  // empty hash-set slot; also the largest hash
+
+// Per-genome sketch status written by the finalize kernel.
+enum SketchStatus : uint32_t {
+  kSketchOk = 0,
+  kSketchRetryLarger = 1,   // fewer than s distinct hashes <= tau, tau < 2^64-1
+  kSketchRetrySmaller = 2,  // candidate set overflowed its limit
+};
+
+// flags[] bits
+constexpr uint32_t kFlagOverflow = 1u;
+constexpr uint32_t kFlagSawMax = 2u;
+
+// Largest number of candidates the finalize kernel sorts in LDS.
+constexpr uint32_t kSortCap = 16384;
+
+struct SketchLaunch {
+  const uint32_t* words;
+  const uint64_t* run_base;    // [n_runs]
+  const uint64_t* run_kstart;  // [n_runs + 1] exclusive prefix of k-mer counts
+  const uint32_t* run_slot;    // [n_runs] genome slot within the batch
+  uint32_t n_runs;
+  uint64_t n_kmers;
+  const uint64_t* tau;         // [slots]
+  uint64_t* table;             // [slots << cap_log2]
+  uint32_t cap_log2;
+  uint32_t* count;             // [slots]
+  uint32_t limit;
+  uint32_t* flags;             // [slots]
+  uint64_t seed;
+};
+
+// sketch.hip
+hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,
+                                    hipStream_t st);
+hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
+                                  const uint32_t* slot_genome,
+                                  const uint64_t* tau, const uint64_t* table,
+                                  uint32_t cap_log2, const uint32_t* count,
+                                  const uint32_t* flags, uint32_t s,
+                                  uint32_t sort_pow2, uint64_t* out,
+                                  uint32_t* lens, uint32_t* status,
+                                  hipStream_t st);
+
+// pairs.hip
+struct PairsLaunch {
+  const uint64_t* sketches;
+  const uint32_t* lens;
+  uint32_t n;
+  uint32_t stride;      // u64 per sketch row (= sketch size)
+  uint32_t n_row_tiles; // ceil(n / GG_PAIR_TILE)
+  uint64_t tile_begin;
+  uint64_t tile_end;
+  const uint32_t* cmin; // [tmax + 1]; pass iff common >= cmin[total]
+  uint32_t tmax;
+  gg_pair* out;
+  uint64_t out_cap;
+  unsigned long long* count;
+};
+hipError_t launch_pairs(const PairsLaunch& a, hipStream_t st);
+
+// synth.hip
+hipError_t launch_synth(uint32_t first_genome, uint32_t n_genomes, uint32_t genome_len,
+                        uint32_t cluster_size, float max_sub_rate,
+                        uint64_t seed, uint32_t* words, hipStream_t st);
+
+// api.cpp helpers used by pack.cpp
+void set_thread_error(const std::string& msg);
+
+// host arithmetic (api.cpp)
+double ani_f64(uint32_t common, uint32_t total, int k);
+std::vector<uint32_t> build_cmin(uint32_t s, int k, float min_ani);
+
+}  // namespace gg

@@ -1,0 +1,327 @@
+// Host-side ingest: FASTA/FASTQ (plain or gzip) -> 2-bit packed ACGT runs.
+//
+// Replaces the byte-level front half of finch::sketch_files as galah calls
+// it (src/finch.rs:47): needletail 0.5 parse_fastx_file, per-record
+// normalize(false) and the "all k bytes in {A,C,G,T}" window test of
+// canonical_kmers.  After this step a k-mer exists exactly at the positions
+// [base, base + len - k] of each run, which is what kernel K1 enumerates.
+//
+// needletail normalize(false) byte map restated:
+//   A C G T         -> kept                 a c g    -> upper case
+//   t u U           -> T                    ' ' \t \r \n -> dropped (do not
+//   everything else -> 'N' (breaks a k-mer)                 break a k-mer)
+//
+// Each genome starts on a 16-base word boundary so files can be packed on
+// separate threads and concatenated with a memcpy.
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "gg_internal.hpp"
+
+namespace gg {
+namespace {
+
+enum : uint8_t { kBreak = 4, kSkip = 5 };
+
+struct ByteClass {
+  uint8_t t[256];
+  ByteClass() {
+    for (int i = 0; i < 256; ++i) t[i] = kBreak;
+    t['A'] = t['a'] = 0;
+    t['C'] = t['c'] = 1;
+    t['G'] = t['g'] = 2;
+    t['T'] = t['t'] = t['U'] = t['u'] = 3;
+    t[' '] = t['\t'] = t['\r'] = t['\n'] = kSkip;
+  }
+};
+const ByteClass kClass;
+
+// Packs the runs of ONE genome; bases start at word 0 of its own buffer.
+struct GenomePacker {
+  int k;
+  std::vector<uint32_t> words;
+  std::vector<gg_run> runs;  // base relative to this genome's first word
+  uint64_t n_bases = 0;
+  uint32_t cur = 0;
+  uint32_t fill = 0;  // bases in cur
+  uint64_t run_start = 0;
+  bool in_run = false;
+
+  explicit GenomePacker(int k_) : k(k_) {}
+
+  inline void push(uint32_t c) {
+    cur |= c << (30 - 2 * fill);
+    if (++fill == 16) {
+      words.push_back(cur);
+      cur = 0;
+      fill = 0;
+    }
+    ++n_bases;
+  }
+
+  // Drop bases back to `to` (a run shorter than k).
+  void truncate(uint64_t to) {
+    if (to == n_bases) return;
+    const uint64_t w = to >> 4;
+    const uint32_t f = (uint32_t)(to & 15);
+    uint32_t word = (w < words.size()) ? words[w] : cur;
+    words.resize(w);
+    cur = f ? (word & (~0u << (32 - 2 * f))) : 0;
+    fill = f;
+    n_bases = to;
+  }
+
+  inline void end_run() {
+    if (!in_run) return;
+    in_run = false;
+    const uint64_t len = n_bases - run_start;
+    if (len < (uint64_t)k) {
+      truncate(run_start);
+    } else {
+      runs.push_back(gg_run{0u, (uint32_t)len, run_start});
+    }
+  }
+
+  // One record's sequence bytes (may contain line breaks).
+  void add_sequence(const uint8_t* p, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+      const uint8_t c = kClass.t[p[i]];
+      if (c < 4) {
+        if (!in_run) {
+          in_run = true;
+          run_start = n_bases;
+        }
+        push(c);
+      } else if (c == kBreak) {
+        end_run();
+      }
+    }
+  }
+  void end_record() { end_run(); }
+
+  void finish() {
+    end_run();
+    if (fill) {
+      words.push_back(cur);
+      cur = 0;
+      fill = 0;
+    }
+  }
+};
+
+bool read_file(const char* path, std::vector<uint8_t>& buf, std::string& err) {
+  gzFile f = gzopen(path, "rb");
+  if (!f) {
+    err = std::string("could not open ") + path;
+    return false;
+  }
+  gzbuffer(f, 1 << 20);
+  buf.clear();
+  size_t len = 0;
+  size_t cap = 1 << 22;
+  buf.resize(cap);
+  for (;;) {
+    if (len == cap) {
+      cap *= 2;
+      buf.resize(cap);
+    }
+    const size_t want = std::min<size_t>(cap - len, 1u << 30);
+    const int got = gzread(f, buf.data() + len, (unsigned)want);
+    if (got < 0) {
+      int zerr = 0;
+      err = std::string("read error in ") + path + ": " + gzerror(f, &zerr);
+      gzclose(f);
+      return false;
+    }
+    if (got == 0) break;
+    len += (size_t)got;
+  }
+  gzclose(f);
+  buf.resize(len);
+  return true;
+}
+
+// Parses FASTA ('>') or FASTQ ('@') as needletail 0.5 does for well-formed
+// files; anything else is a format error (galah: "Failed to sketch genomes
+// with finch", src/finch.rs:50).
+gg_status pack_buffer(const uint8_t* d, size_t n, const char* name,
+                      GenomePacker& gp, std::string& err) {
+  if (n == 0 || (d[0] != '>' && d[0] != '@')) {
+    err = std::string("not a FASTA/FASTQ file: ") + name;
+    return GG_ERR_FORMAT;
+  }
+  size_t i = 0;
+  while (i < n) {
+    const uint8_t tag = d[i];
+    if (tag != '>' && tag != '@') {
+      err = std::string("malformed record in ") + name;
+      return GG_ERR_FORMAT;
+    }
+    const uint8_t* nl = (const uint8_t*)memchr(d + i, '\n', n - i);
+    i = nl ? (size_t)(nl - d) + 1 : n;  // skip header line
+    if (tag == '>') {
+      size_t start = i;
+      // sequence runs until a line that starts with '>'
+      while (i < n) {
+        if (d[i] == '>') break;
+        const uint8_t* e = (const uint8_t*)memchr(d + i, '\n', n - i);
+        i = e ? (size_t)(e - d) + 1 : n;
+      }
+      gp.add_sequence(d + start, i - start);
+      gp.end_record();
+    } else {
+      const uint8_t* e = (const uint8_t*)memchr(d + i, '\n', n - i);
+      const size_t end = e ? (size_t)(e - d) : n;
+      gp.add_sequence(d + i, end - i);
+      gp.end_record();
+      i = e ? end + 1 : n;
+      for (int skip = 0; skip < 2 && i < n; ++skip) {  // '+' line, quality line
+        const uint8_t* q = (const uint8_t*)memchr(d + i, '\n', n - i);
+        i = q ? (size_t)(q - d) + 1 : n;
+      }
+    }
+  }
+  return GG_OK;
+}
+
+gg_packed* assemble(std::vector<std::unique_ptr<GenomePacker>>& gps) {
+  const uint32_t ng = (uint32_t)gps.size();
+  uint64_t n_words = 0, n_runs = 0;
+  for (auto& g : gps) {
+    n_words += g->words.size();
+    n_runs += g->runs.size();
+  }
+  gg_packed* p = (gg_packed*)calloc(1, sizeof(gg_packed));
+  if (!p) return nullptr;
+  p->words = (uint32_t*)malloc(std::max<uint64_t>(n_words, 1) * sizeof(uint32_t));
+  p->runs = (gg_run*)malloc(std::max<uint64_t>(n_runs, 1) * sizeof(gg_run));
+  p->genome_kmers = (uint64_t*)calloc(std::max<uint32_t>(ng, 1), sizeof(uint64_t));
+  if (!p->words || !p->runs || !p->genome_kmers) {
+    gg_packed_free(p);
+    return nullptr;
+  }
+  uint64_t wo = 0, ro = 0;
+  for (uint32_t g = 0; g < ng; ++g) {
+    GenomePacker& gp = *gps[g];
+    if (!gp.words.empty())
+      memcpy(p->words + wo, gp.words.data(), gp.words.size() * sizeof(uint32_t));
+    uint64_t kmers = 0;
+    for (const gg_run& r : gp.runs) {
+      p->runs[ro++] = gg_run{g, r.len, r.base + wo * 16};
+      kmers += (uint64_t)r.len - (uint64_t)gp.k + 1;
+    }
+    p->genome_kmers[g] = kmers;
+    wo += gp.words.size();
+  }
+  p->n_words = n_words;
+  p->n_bases = n_words * 16;
+  p->n_runs = n_runs;
+  p->n_genomes = ng;
+  return p;
+}
+
+}  // namespace
+}  // namespace gg
+
+using namespace gg;
+
+extern "C" gg_status gg_pack_files(const char* const* paths, uint32_t n_paths,
+                                   int kmer_length, int n_threads,
+                                   gg_packed** out) {
+  if (!out || (n_paths && !paths) || kmer_length < 1 || kmer_length > 32) {
+    set_thread_error("gg_pack_files: invalid argument");
+    return GG_ERR_INVALID_ARG;
+  }
+  *out = nullptr;
+  std::vector<std::unique_ptr<GenomePacker>> gps(n_paths);
+  std::vector<gg_status> st(n_paths, GG_OK);
+  std::vector<std::string> errs(n_paths);
+  if (n_threads <= 0) n_threads = (int)std::max(1u, std::thread::hardware_concurrency());
+  n_threads = (int)std::min<uint32_t>((uint32_t)n_threads, std::max(1u, n_paths));
+  std::atomic<uint32_t> next{0};
+  auto worker = [&]() {
+    std::vector<uint8_t> buf;
+    for (;;) {
+      const uint32_t i = next.fetch_add(1);
+      if (i >= n_paths) break;
+      gps[i].reset(new GenomePacker(kmer_length));
+      if (!paths[i]) {
+        st[i] = GG_ERR_INVALID_ARG;
+        errs[i] = "null path";
+        continue;
+      }
+      if (!read_file(paths[i], buf, errs[i])) {
+        st[i] = GG_ERR_IO;
+        continue;
+      }
+      st[i] = pack_buffer(buf.data(), buf.size(), paths[i], *gps[i], errs[i]);
+      gps[i]->finish();
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < n_threads; ++t) th.emplace_back(worker);
+  worker();
+  for (auto& t : th) t.join();
+  for (uint32_t i = 0; i < n_paths; ++i) {
+    if (st[i] != GG_OK) {
+      set_thread_error(errs[i]);
+      return st[i];
+    }
+  }
+  gg_packed* p = assemble(gps);
+  if (!p) {
+    set_thread_error("gg_pack_files: out of host memory");
+    return GG_ERR_OUT_OF_MEMORY;
+  }
+  *out = p;
+  return GG_OK;
+}
+
+extern "C" gg_status gg_pack_records(const uint8_t* const* seqs,
+                                     const uint64_t* lens,
+                                     const uint32_t* genome_of_record,
+                                     uint64_t n_records, uint32_t n_genomes,
+                                     int kmer_length, gg_packed** out) {
+  if (!out || kmer_length < 1 || kmer_length > 32 ||
+      (n_records && (!seqs || !lens || !genome_of_record))) {
+    set_thread_error("gg_pack_records: invalid argument");
+    return GG_ERR_INVALID_ARG;
+  }
+  *out = nullptr;
+  std::vector<std::unique_ptr<GenomePacker>> gps(n_genomes);
+  for (uint32_t g = 0; g < n_genomes; ++g) gps[g].reset(new GenomePacker(kmer_length));
+  uint32_t prev = 0;
+  for (uint64_t r = 0; r < n_records; ++r) {
+    const uint32_t g = genome_of_record[r];
+    if (g >= n_genomes || g < prev) {
+      set_thread_error("gg_pack_records: records must be grouped by non-decreasing genome < n_genomes");
+      return GG_ERR_INVALID_ARG;
+    }
+    prev = g;
+    gps[g]->add_sequence(seqs[r], (size_t)lens[r]);
+    gps[g]->end_record();
+  }
+  for (auto& g : gps) g->finish();
+  gg_packed* p = assemble(gps);
+  if (!p) {
+    set_thread_error("gg_pack_records: out of host memory");
+    return GG_ERR_OUT_OF_MEMORY;
+  }
+  *out = p;
+  return GG_OK;
+}
+
+extern "C" void gg_packed_free(gg_packed* p) {
+  if (!p) return;
+  free(p->words);
+  free(p->runs);
+  free(p->genome_kmers);
+  free(p);
+}

@@ -1,0 +1,325 @@
+// Kernel K1: canonical k-mer hashing and per-genome bottom-s selection.
+//
+// Restates, bit for bit, what finch's MashSketcher computes for galah
+// (src/finch.rs:33-47: SketchParams::Mash{kmers_to_sketch: s, final_size: s,
+// no_strict: true, kmer_length: k, hash_seed: 0}, no filtering):
+//   for every k-mer window of A/C/G/T inside a record:
+//     canonical = lexicographically smaller of fwd and reverse complement
+//     h = murmurhash3_x64_128(canonical ASCII bytes, seed).0
+//   sketch = the min(s, #distinct) smallest distinct h, ascending.
+//
+// MI355X design
+//   * Input is 2-bit packed (0.25 B/base).  Each lane owns SEG consecutive
+//     k-mer positions and rolls the forward code in both bit orders:
+//       fm = MSB-first code (lexicographic order of the forward k-mer)
+//       fl = LSB-first code (byte p of the hash input = base p)
+//     The reverse complement needs no separate state:
+//       rc MSB-first = ~fl, rc LSB-first = ~fm   (within 2k bits).
+//   * ASCII bytes come from a 256-entry LDS table (4 bases -> 4 bytes).
+//   * Bottom-s selection is a threshold prefilter: a k-mer survives iff
+//     h <= tau[g] where tau[g] ~ C*s/nk_g * 2^64, so only ~C*s of the
+//     ~nk_g hashes per genome reach a per-genome open-addressing set in HBM
+//     (atomicCAS, duplicates collapse).  The finalize kernel sorts the set in
+//     LDS and keeps the first s.  When the set holds fewer than s distinct
+//     values below tau (tau < 2^64-1) or overflows, the host moves tau and
+//     re-runs the affected genomes only; the result is exact in both cases
+//     because every distinct hash <= tau is in the set.
+#include "gg_internal.hpp"
+
+namespace gg {
+namespace {
+
+constexpr int kSeg = 32;        // k-mer positions per lane per segment
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
+  return (x << r) | (x >> (64 - r));
+}
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// murmurhash3_x64_128(bytes, seed).0 where byte p = ASCII of base p of the
+// LSB-first 2-bit code `code` (K <= 32 bases).
+template <int K>
+__device__ __forceinline__ uint64_t hash_code(uint64_t code,
+                                              const uint32_t* __restrict__ lut,
+                                              uint64_t seed) {
+  constexpr int NW = (K + 3) / 4;  // ASCII words of 4 bytes
+  uint32_t w[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) w[q] = 0;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) w[q] = lut[(uint32_t)(code >> (8 * q)) & 0xFFu];
+  if (K % 4) w[NW - 1] &= (1u << (8 * (K % 4))) - 1u;  // bytes past K are not input
+
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  uint64_t h1 = seed, h2 = seed;
+  constexpr int NBLK = K / 16;
+#pragma unroll
+  for (int b = 0; b < NBLK; ++b) {
+    uint64_t k1 = (uint64_t)w[4 * b] | ((uint64_t)w[4 * b + 1] << 32);
+    uint64_t k2 = (uint64_t)w[4 * b + 2] | ((uint64_t)w[4 * b + 3] << 32);
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+  }
+  constexpr int TAIL = K % 16;
+  if (TAIL > 8) {
+    uint64_t k2 = (uint64_t)w[4 * NBLK + 2];
+    if (TAIL > 12) k2 |= (uint64_t)w[4 * NBLK + 3] << 32;
+    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+  }
+  if (TAIL > 0) {
+    uint64_t k1 = (uint64_t)w[4 * NBLK];
+    if (TAIL > 4) k1 |= (uint64_t)w[4 * NBLK + 1] << 32;
+    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  }
+  h1 ^= (uint64_t)K;
+  h2 ^= (uint64_t)K;
+  h1 += h2;
+  h2 += h1;
+  h1 = fmix64(h1);
+  h2 = fmix64(h2);
+  return h1 + h2;
+}
+
+__device__ __forceinline__ void build_lut(uint32_t* lut) {
+  // ASCII 'A','C','G','T' indexed by 2-bit code; lut[x] = 4 bytes for the
+  // 4 codes of x, code j in bits 2j..2j+1 -> byte j.
+  for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t c = (x >> (2 * j)) & 3u;
+      v |= ((0x54474341u >> (8 * c)) & 0xFFu) << (8 * j);
+    }
+    lut[x] = v;
+  }
+}
+
+// Insert h into genome slot's open-addressing set.
+__device__ __forceinline__ void insert_candidate(uint64_t* __restrict__ tab,
+                                                 uint32_t mask,
+                                                 uint32_t* __restrict__ count,
+                                                 uint32_t limit,
+                                                 uint32_t* __restrict__ flags,
+                                                 uint64_t h) {
+  if (h == kEmpty) {  // only reachable when tau == 2^64-1
+    atomicOr(flags, kFlagSawMax);
+    return;
+  }
+  if (__hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kFlagOverflow) return;
+  uint32_t i = (uint32_t)h & mask;
+  for (uint32_t probe = 0; probe <= mask; ++probe) {
+    const unsigned long long old =
+        atomicCAS((unsigned long long*)&tab[i], (unsigned long long)kEmpty,
+                  (unsigned long long)h);
+    if (old == kEmpty) {
+      const uint32_t c = atomicAdd(count, 1u);
+      if (c + 1 >= limit) atomicOr(flags, kFlagOverflow);
+      return;
+    }
+    if (old == h) return;
+    i = (i + 1) & mask;
+  }
+  atomicOr(flags, kFlagOverflow);
+}
+
+// Largest r with run_kstart[r] <= p, searching forward from `from`
+// (positions of one lane increase monotonically).
+__device__ __forceinline__ uint32_t find_run(const uint64_t* __restrict__ ks,
+                                             uint32_t n_runs, uint64_t p,
+                                             uint32_t from) {
+  if (ks[from + 1] > p) return from;
+  // gallop
+  uint32_t lo = from + 1, step = 1;
+  uint32_t hi = lo;
+  while (true) {
+    hi = lo + step;
+    if (hi >= n_runs || ks[hi] > p) break;
+    lo = hi;
+    step <<= 1;
+  }
+  if (hi > n_runs) hi = n_runs;
+  // invariant: ks[lo] <= p, ks[hi] > p (ks[n_runs] = total > p)
+  while (hi - lo > 1) {
+    const uint32_t mid = lo + (hi - lo) / 2;
+    if (ks[mid] <= p) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void sketch_candidates_kernel(SketchLaunch a) {
+  __shared__ uint32_t lut[256];
+  build_lut(lut);
+  __syncthreads();
+
+  constexpr uint64_t MASK = (K == 32) ? ~0ull : ((1ull << (2 * K)) - 1ull);
+  const uint32_t cap_mask = (1u << a.cap_log2) - 1u;
+  const uint64_t nseg = (a.n_kmers + kSeg - 1) / kSeg;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  uint32_t r = 0;
+
+  for (uint64_t seg = (uint64_t)blockIdx.x * kBlock + threadIdx.x; seg < nseg; seg += stride) {
+    uint64_t p = seg * kSeg;
+    const uint64_t pend = min(p + (uint64_t)kSeg, a.n_kmers);
+    r = find_run(a.run_kstart, a.n_runs, p, r);
+    while (p < pend) {
+      const uint64_t rk0 = a.run_kstart[r];
+      const uint64_t stop = min(pend, a.run_kstart[r + 1]);
+      const uint32_t slot = a.run_slot[r];
+      const uint64_t tau = a.tau[slot];
+      uint64_t* tab = a.table + ((uint64_t)slot << a.cap_log2);
+      uint64_t b = a.run_base[r] + (p - rk0);  // first base of k-mer p
+
+      // word cursor
+      uint64_t wi = b >> 4;
+      uint32_t cur = a.words[wi] << (2 * (uint32_t)(b & 15));
+      uint32_t left = 16 - (uint32_t)(b & 15);
+      uint64_t fm = 0, fl = 0;
+#pragma unroll
+      for (int i = 0; i < K - 1; ++i) {
+        if (left == 0) { cur = a.words[++wi]; left = 16; }
+        const uint64_t c = cur >> 30;
+        cur <<= 2; --left;
+        fm = (fm << 2) | c;
+        fl = (fl >> 2) | (c << (2 * K - 2));
+      }
+      for (; p < stop; ++p) {
+        if (left == 0) { cur = a.words[++wi]; left = 16; }
+        const uint64_t c = cur >> 30;
+        cur <<= 2; --left;
+        fm = ((fm << 2) | c) & MASK;
+        fl = (fl >> 2) | (c << (2 * K - 2));
+        const uint64_t rcm = fl ^ MASK;             // reverse complement, MSB-first
+        const uint64_t can = (fm < rcm) ? fl : (fm ^ MASK);  // canonical, LSB-first
+        const uint64_t h = hash_code<K>(can, lut, a.seed);
+        if (h <= tau) insert_candidate(tab, cap_mask, a.count + slot, a.limit, a.flags + slot, h);
+      }
+      if (p < pend) ++r;
+    }
+  }
+}
+
+// One workgroup per genome slot: gather the set, bitonic sort in LDS, keep
+// the first s.  Writes status[] for the host retry loop.
+__global__ __launch_bounds__(kBlock) void sketch_finalize_kernel(
+    const uint32_t* __restrict__ slot_list, const uint32_t* __restrict__ slot_genome,
+    const uint64_t* __restrict__ tau, const uint64_t* __restrict__ table,
+    uint32_t cap_log2, const uint32_t* __restrict__ count,
+    const uint32_t* __restrict__ flags, uint32_t s, uint32_t sort_pow2,
+    uint64_t* __restrict__ out, uint32_t* __restrict__ lens,
+    uint32_t* __restrict__ status) {
+  extern __shared__ uint64_t buf[];
+  __shared__ uint32_t fill;
+  const uint32_t slot = slot_list[blockIdx.x];
+  const uint32_t g = slot_genome[slot];
+  const uint32_t f = flags[slot];
+  const uint32_t cnt = count[slot];
+  uint32_t st = kSketchOk;
+  if (f & kFlagOverflow) st = kSketchRetrySmaller;
+  else if (cnt < s && tau[slot] != kEmpty) st = kSketchRetryLarger;
+  else if (cnt > sort_pow2) st = kSketchRetrySmaller;  // cannot sort in LDS
+  if (st != kSketchOk) {
+    if (threadIdx.x == 0) {
+      status[slot] = st;
+      lens[g] = 0;
+    }
+    return;
+  }
+  if (threadIdx.x == 0) fill = 0;
+  __syncthreads();
+  const uint64_t* tab = table + ((uint64_t)slot << cap_log2);
+  const uint32_t cap = 1u << cap_log2;
+  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+    const uint64_t v = tab[i];
+    if (v != kEmpty) buf[atomicAdd(&fill, 1u)] = v;
+  }
+  __syncthreads();
+  const uint32_t n = fill;  // == cnt
+  uint32_t P = 1;
+  while (P < n) P <<= 1;
+  for (uint32_t i = n + threadIdx.x; i < P; i += blockDim.x) buf[i] = kEmpty;
+  __syncthreads();
+  for (uint32_t size = 2; size <= P; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t t = threadIdx.x; t < P / 2; t += blockDim.x) {
+        const uint32_t lo = 2 * t - (t & (stride - 1));
+        const uint32_t hi = lo + stride;
+        const bool up = ((lo & size) == 0);
+        const uint64_t x = buf[lo], y = buf[hi];
+        if ((x > y) == up) {
+          buf[lo] = y;
+          buf[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  uint32_t m = min(s, n);
+  uint64_t* o = out + (uint64_t)g * s;
+  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) o[i] = buf[i];
+  if ((f & kFlagSawMax) && m < s) {
+    if (threadIdx.x == 0) o[m] = kEmpty;  // 2^64-1 is the largest hash
+    ++m;
+  }
+  if (threadIdx.x == 0) {
+    lens[g] = m;
+    status[slot] = kSketchOk;
+  }
+}
+
+template <int K>
+hipError_t launch_k(const SketchLaunch& a, int grid, hipStream_t st) {
+  hipLaunchKernelGGL(sketch_candidates_kernel<K>, dim3(grid), dim3(kBlock), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,
+                                    hipStream_t st) {
+  if (a.n_kmers == 0) return hipSuccess;
+  switch (k) {
+#define GG_K(N) case N: return launch_k<N>(a, grid, st);
+    GG_K(1) GG_K(2) GG_K(3) GG_K(4) GG_K(5) GG_K(6) GG_K(7) GG_K(8)
+    GG_K(9) GG_K(10) GG_K(11) GG_K(12) GG_K(13) GG_K(14) GG_K(15) GG_K(16)
+    GG_K(17) GG_K(18) GG_K(19) GG_K(20) GG_K(21) GG_K(22) GG_K(23) GG_K(24)
+    GG_K(25) GG_K(26) GG_K(27) GG_K(28) GG_K(29) GG_K(30) GG_K(31) GG_K(32)
+#undef GG_K
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
+                                  const uint32_t* slot_genome,
+                                  const uint64_t* tau, const uint64_t* table,
+                                  uint32_t cap_log2, const uint32_t* count,
+                                  const uint32_t* flags, uint32_t s,
+                                  uint32_t sort_pow2, uint64_t* out,
+                                  uint32_t* lens, uint32_t* status,
+                                  hipStream_t st) {
+  if (n_slots == 0) return hipSuccess;
+  const size_t lds = (size_t)sort_pow2 * sizeof(uint64_t);
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)sketch_finalize_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(sketch_finalize_kernel, dim3(n_slots), dim3(kBlock), lds, st,
+                     slot_list, slot_genome, tau, table, cap_log2, count, flags, s,
+                     sort_pow2, out, lens, status);
+  return hipGetLastError();
+}
+
+}  // namespace gg

@@ -1,0 +1,211 @@
+/*
+ * galahgpu.h -- C ABI of libgalahgpu.so, the MI355X implementation of
+ * galah's finch MinHash precluster path.
+ *
+ * Reference interface this replaces (file:line in AroneyS/galah @ 2024-12-18):
+ *
+ *   src/lib.rs:23-27          trait PreclusterDistanceFinder { distances(); method_name(); }
+ *   src/finch.rs:11-24        impl PreclusterDistanceFinder for FinchPreclusterer
+ *   src/finch.rs:26-75        finch::distances(paths, min_ani, num_kmers, kmer_length)
+ *                             -> SortedPairGenomeDistanceCache
+ *     :33-47                  finch::sketch_files (needletail parse, normalize,
+ *                             canonical k-mers, murmur3, bottom-s)   -> gg_pack_* + gg_sketch*
+ *     :53-73                  serial all-pairs finch::distance::distance,
+ *                             ani >= min_ani as f64, insert Some(ani as f32)
+ *                                                                   -> gg_pairs*
+ *   src/sorted_pair_genome_distance_cache.rs:22-28   key (min,max) normalisation:
+ *                             every gg_pair has i < j.
+ *
+ * Conventions
+ *   - Every entry point returns a status code; nothing throws or aborts
+ *     across the ABI.  gg_last_error(ctx) (or gg_thread_last_error() for the
+ *     ctx-free host functions) describes the last failure.
+ *   - Inputs are borrowed for the duration of the call.  Buffers returned
+ *     through pointer-to-pointer arguments are library-owned and released
+ *     with gg_free / gg_packed_free.
+ *   - A context is bound to one HIP device; calls on one context must be
+ *     serialised by the caller (galah calls distances() once, from one
+ *     thread: src/clusterer.rs:36).
+ *   - There is NO CPU fallback: gg_create fails with GG_ERR_NO_DEVICE when
+ *     no MI355X (gfx950) device is visible.
+ *   - *_device entry points take device pointers on the context's device
+ *     and enqueue on the given hipStream_t (passed as void*); they do not
+ *     synchronise unless stated.
+ */
+#ifndef GALAHGPU_H
+#define GALAHGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GG_ABI_VERSION 1u
+
+typedef enum gg_status {
+  GG_OK = 0,
+  GG_ERR_INVALID_ARG = 1,
+  GG_ERR_IO = 2,          /* file could not be opened / read */
+  GG_ERR_FORMAT = 3,      /* not FASTA/FASTQ */
+  GG_ERR_NO_DEVICE = 4,   /* no usable HIP device */
+  GG_ERR_HIP = 5,         /* HIP runtime error */
+  GG_ERR_OUT_OF_MEMORY = 6,
+  GG_ERR_INTERNAL = 7,
+  GG_ERR_OUTPUT_FULL = 8  /* device pair buffer too small; *count holds the need */
+} gg_status;
+
+typedef struct gg_ctx gg_ctx;
+
+/* One maximal stretch of A/C/G/T (after needletail normalize) inside one
+ * FASTA record, at least k bases long.  Bases [base, base+len) of the
+ * packed stream.  Runs of one genome are contiguous and genomes appear in
+ * input order. */
+typedef struct gg_run {
+  uint32_t genome;
+  uint32_t len;
+  uint64_t base;
+} gg_run;
+
+/* One above-threshold genome pair; i < j (SortedPairGenomeDistanceCache key). */
+typedef struct gg_pair {
+  uint32_t i;
+  uint32_t j;
+  uint32_t common; /* finch raw_distance common  = |A n B|                         */
+  uint32_t total;  /* finch raw_distance total   = i + j - common at first exhaustion */
+} gg_pair;
+
+/* 2-bit packed genomes: A=0 C=1 G=2 T=3, 16 bases per uint32 word, the
+ * first base of a word in bits 31..30. */
+typedef struct gg_packed {
+  uint32_t* words;
+  uint64_t n_words;
+  uint64_t n_bases;
+  gg_run* runs;
+  uint64_t n_runs;
+  uint32_t n_genomes;
+  uint64_t* genome_kmers; /* per genome: number of k-mer positions (sum of len-k+1) */
+} gg_packed;
+
+/* ---- versioning / errors --------------------------------------------- */
+uint32_t gg_abi_version(void);
+const char* gg_status_string(gg_status s);
+const char* gg_last_error(const gg_ctx* ctx);
+const char* gg_thread_last_error(void);
+
+/* ---- context ---------------------------------------------------------- */
+/* kmer_length: 1..32 (galah: 21, CAP:981); sketch_size: 1..12000 (galah:
+ * 1000, CAP:980); hash_seed: murmur3 seed (galah: 0, src/finch.rs:38);
+ * device: HIP ordinal, or -1 for the current device. */
+gg_ctx* gg_create(int kmer_length, uint32_t sketch_size, uint64_t hash_seed,
+                  int device, gg_status* status);
+void gg_destroy(gg_ctx* ctx);
+int gg_device(const gg_ctx* ctx);
+
+/* ---- host-side ingest: FASTA/FASTQ (plain or gz) -> 2-bit runs --------- */
+/* Replaces needletail parse_fastx_file + normalize(false) + the ACGT
+ * window test of canonical_kmers inside finch::sketch_files
+ * (src/finch.rs:47).  n_threads <= 0 means all hardware threads. */
+gg_status gg_pack_files(const char* const* paths, uint32_t n_paths,
+                        int kmer_length, int n_threads, gg_packed** out);
+/* In-memory records: record r (bytes seqs[r][0..lens[r]) , no header, may
+ * contain line breaks) belongs to genome genome_of_record[r]; records must
+ * be grouped by non-decreasing genome index. */
+gg_status gg_pack_records(const uint8_t* const* seqs, const uint64_t* lens,
+                          const uint32_t* genome_of_record, uint64_t n_records,
+                          uint32_t n_genomes, int kmer_length, gg_packed** out);
+void gg_packed_free(gg_packed* p);
+
+/* ---- sketching (kernel K1) -------------------------------------------- */
+/* Bottom-s distinct murmur3 h1 of canonical k-mers per genome, ascending;
+ * bit-exact with finch's MashSketcher + process_post_filter.  out_hashes
+ * is n_genomes * sketch_size (row g padded after out_lens[g]). */
+gg_status gg_sketch(gg_ctx* ctx, const gg_packed* packed,
+                    uint64_t* out_hashes, uint32_t* out_lens);
+/* Device-resident variant: d_words / d_out / d_lens are device pointers;
+ * runs are host metadata (copied by the library).  Synchronises stream
+ * internally (retry planning reads per-genome status). */
+gg_status gg_sketch_device(gg_ctx* ctx, const uint32_t* d_words,
+                           uint64_t n_words, const gg_run* runs,
+                           uint64_t n_runs, uint32_t n_genomes,
+                           uint64_t* d_out, uint32_t* d_lens, void* stream);
+
+/* ---- all-pairs (kernel K2) -------------------------------------------- */
+/* The pair space (i < j < n) is cut into GG_PAIR_TILE x GG_PAIR_TILE tiles
+ * of the upper triangle, enumerated row-major.  Multi-GPU runs partition
+ * the tile range; the union of the per-range outputs is independent of
+ * the partition. */
+#define GG_PAIR_TILE 64u
+uint64_t gg_pair_tiles(uint32_t n);
+/* Tile range [*begin, *end) of part `part` of `parts`, equal pair counts. */
+void gg_pair_partition(uint32_t n, uint32_t parts, uint32_t part,
+                       uint64_t* begin, uint64_t* end);
+
+/* Host buffers in and out.  *out is library-owned (gg_free), sorted by
+ * (i, j).  Pass iff ani(common,total) >= (double)min_ani, ani computed as
+ * src/finch.rs:56-69 does. */
+gg_status gg_pairs(gg_ctx* ctx, const uint64_t* sketches, const uint32_t* lens,
+                   uint32_t n, float min_ani, gg_pair** out, uint64_t* n_out);
+/* Device-resident: sketches [n x sketch_size] u64, lens [n] u32.
+ * Appends passing pairs of tiles [tile_begin, tile_end) to d_out (unsorted),
+ * *d_count (device u64) incremented by the number found; entries past
+ * out_cap are dropped (caller compares *d_count with out_cap). Async. */
+gg_status gg_pairs_device(gg_ctx* ctx, const uint64_t* d_sketches,
+                          const uint32_t* d_lens, uint32_t n,
+                          uint64_t tile_begin, uint64_t tile_end,
+                          float min_ani, gg_pair* d_out, uint64_t out_cap,
+                          uint64_t* d_count, void* stream);
+
+/* ---- the fused FinchPreclusterer::distances body ------------------------ */
+/* paths -> sorted passing pairs plus their f32 ANI (src/finch.rs:70 value). */
+gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths,
+                              uint32_t n_paths, float min_ani, gg_pair** pairs,
+                              float** ani, uint64_t* n_out);
+
+/* ---- host arithmetic shared with the caller ---------------------------- */
+/* src/finch.rs:56-64: 1 - finch mash_distance, f64, Rust NaN semantics */
+double gg_ani_f64(uint32_t common, uint32_t total, int kmer_length);
+/* the value galah stores: Some(ani as f32), src/finch.rs:70 */
+float gg_ani_f32(uint32_t common, uint32_t total, int kmer_length);
+/* CAP:1160-1182 parse_percentage applied to --precluster-ani: values in
+ * [1,100] are divided by 100 in f32, [0,1) kept; else GG_ERR_INVALID_ARG. */
+gg_status gg_parse_percentage(float value, float* fraction);
+
+void gg_free(void* p);
+
+/* ---- per-kernel timing (benchmarks) ------------------------------------ */
+/* When enabled, every kernel launch of the context is bracketed by HIP
+ * events recorded on the stream it is launched on.  gg_timing_read
+ * synchronises on those events and returns the summed duration, the number
+ * of launches and the algorithmic work units (k-mer positions for
+ * GG_KERNEL_SKETCH, genomes for GG_KERNEL_FINALIZE, evaluated pairs for
+ * GG_KERNEL_PAIRS) since the last gg_timing_enable. */
+enum { GG_KERNEL_SKETCH = 0, GG_KERNEL_FINALIZE = 1, GG_KERNEL_PAIRS = 2, GG_KERNEL_COUNT = 3 };
+typedef struct gg_kernel_stats {
+  double ms;
+  uint64_t launches;
+  uint64_t work;
+} gg_kernel_stats;
+gg_status gg_timing_enable(gg_ctx* ctx, int on);
+gg_status gg_timing_read(gg_ctx* ctx, int kernel, gg_kernel_stats* out);
+
+/* ---- benchmark support: synthetic clustered genomes on device ---------- */
+/* Genomes [first_genome, first_genome + n_genomes) of a synthetic set of
+ * genomes of genome_len bases, in clusters of cluster_size consecutive
+ * genomes (global index).  Member m of a cluster is the cluster root with
+ * i.i.d. substitutions at rate r_m ~ U(0, max_sub_rate) (r = 0 for the
+ * root itself).  Counter-based RNG: output depends only on the arguments.
+ * Writes packed words (local genome g at base g*genome_len, genome_len a
+ * multiple of 16) and fills runs[g] = {g, genome_len, g*genome_len} (host
+ * array, local indices). */
+gg_status gg_synth_clustered_device(gg_ctx* ctx, uint32_t first_genome, uint32_t n_genomes,
+                                    uint32_t genome_len, uint32_t cluster_size,
+                                    float max_sub_rate, uint64_t seed,
+                                    uint32_t* d_words, gg_run* runs,
+                                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GALAHGPU_H */

@@ -1,0 +1,56 @@
+import glob
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+GOLD_DATA = os.path.join(GOLD, "data")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device")
+
+
+def golden_names():
+    with np.load(os.path.join(GOLD, "sketches_k21_s1000.npz")) as z:
+        return [str(x) for x in z["names"]]
+
+
+def golden_path(name):
+    return os.path.join(GOLD_DATA, name + ".gz")
+
+
+def load_golden_sketches():
+    with np.load(os.path.join(GOLD, "sketches_k21_s1000.npz")) as z:
+        return [str(x) for x in z["names"]], z["sketches"].copy(), z["lens"].copy()
+
+
+def load_golden_pairs():
+    rows = []
+    with open(os.path.join(GOLD, "pairs_k21_s1000.tsv")) as f:
+        next(f)
+        for line in f:
+            i, j, c, t, a = line.split()
+            rows.append((int(i), int(j), int(c), int(t), np.float32(a)))
+    return rows
+
+
+@pytest.fixture(scope="session")
+def golden():
+    names, sk, lens = load_golden_sketches()
+    return {"names": names, "sketches": sk, "lens": lens, "pairs": load_golden_pairs(),
+            "paths": [golden_path(n) for n in names]}
+
+
+@pytest.fixture(scope="session")
+def gpu_ctx():
+    import galah_amd
+    ctx = galah_amd.Context(k=21, sketch_size=1000, seed=0)
+    yield ctx
+    ctx.close()

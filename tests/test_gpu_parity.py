@@ -1,0 +1,229 @@
+"""Parity of the HIP path (through the C ABI) with the CPU oracle and the
+committed golden fixtures.  Needs an MI355X.
+
+Bar: sketches and (common, total) bit-exact; ANI f32 identical (computed
+from (common, total) by the same f64 expression); pair sets identical.
+"""
+import numpy as np
+import pytest
+
+import galah_amd as ga
+import oracle
+from test_host import EDGE_RECORDS, packed_records, unpack_run
+
+pytestmark = pytest.mark.gpu
+
+
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+def expected_pairs_from_table(golden, min_ani):
+    thr = np.float64(np.float32(min_ani))
+    return [(i, j, c, t) for (i, j, c, t, a) in golden["pairs"] if oracle.ani(c, t) >= thr]
+
+
+def as_tuples(p):
+    return [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in p]
+
+
+def test_golden_sketches_bit_exact(gpu_ctx, golden):
+    pk = ga.pack_files(golden["paths"])
+    sk, lens = gpu_ctx.sketch(pk)
+    assert (lens == golden["lens"]).all()
+    for g in range(len(lens)):
+        n = lens[g]
+        assert (sk[g][:n] == golden["sketches"][g][:n]).all(), golden["names"][g]
+
+
+@pytest.mark.parametrize("min_ani", [0.0, 0.5, 0.9, 0.95, 0.97, 0.98, 0.99, 1.0])
+def test_golden_pairs_exact(gpu_ctx, golden, min_ani):
+    p = gpu_ctx.pairs(golden["sketches"], golden["lens"], np.float32(min_ani))
+    assert as_tuples(p) == expected_pairs_from_table(golden, min_ani)
+
+
+def test_finch_rs_hello_world(golden):
+    # src/finch.rs:85-107 through the reference-interface mirror
+    paths = [golden["paths"][golden["names"].index(n)] for n in ("set1/1mbp.fna", "set1/500kb.fna")]
+    d1 = ga.distances(paths, 0.9, 1000, 21)
+    e1 = ga.SortedPairGenomeDistanceCache()
+    e1.insert((0, 1), np.float32(0.9808188))
+    assert d1 == e1
+    assert repr(d1) == "SortedPairGenomeDistanceCache { internal: {(0, 1): Some(0.9808188)} }"
+    d2 = ga.FinchPreclusterer(0.99, 1000, 21).distances(paths)
+    assert d2 == ga.SortedPairGenomeDistanceCache()
+
+
+def test_precluster_files_matches_oracle(gpu_ctx, golden):
+    min_ani = ga.parse_percentage(90)
+    pairs, ani = gpu_ctx.precluster_files(golden["paths"], min_ani)
+    exp = expected_pairs_from_table(golden, min_ani)
+    assert as_tuples(pairs) == exp and len(exp) == 161
+    for r, a in zip(pairs, ani):
+        assert a == np.float32(oracle.ani(int(r["common"]), int(r["total"])))
+
+
+def test_edge_records_and_retry_paths(gpu_ctx):
+    rng = np.random.default_rng(11)
+    rnd = lambda n: np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)].tobytes()
+    half = rnd(40000)
+    genomes = [[r] for r in EDGE_RECORDS]
+    genomes += [
+        [half, half],            # every k-mer twice: exercises tau retries
+        [half + half],
+        [b"A" * 300000],         # one distinct k-mer
+        [rnd(900)],              # fewer k-mers than s
+        [rnd(1100)],
+        [rnd(30) for _ in range(50)],
+        [],                      # genome without records
+        [rnd(250000)],
+        [(b"ACGTTGCAAT" * 2000)],  # low-complexity
+    ]
+    pk = ga.pack_records(genomes)
+    sk, lens = gpu_ctx.sketch(pk)
+    for g, recs in enumerate(genomes):
+        exp = oracle.sketch_records(recs) if recs else np.zeros(0, np.uint64)
+        assert lens[g] == len(exp), g
+        assert (sk[g][:lens[g]] == exp).all(), g
+
+
+def test_other_k_and_s():
+    rng = np.random.default_rng(5)
+    recs = [[np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 20000)].tobytes()] for _ in range(3)]
+    for k, s in [(21, 10), (16, 500), (31, 2000), (32, 64), (11, 100), (5, 50), (21, 10000)]:
+        with ga.Context(k=k, sketch_size=s) as ctx:
+            pk = ga.pack_records(recs, k=k)
+            sk, lens = ctx.sketch(pk)
+            for g in range(3):
+                exp = oracle.sketch_records(recs[g], k=k, s=s)
+                assert lens[g] == len(exp) and (sk[g][:lens[g]] == exp).all(), (k, s, g)
+
+
+def random_sketch_set(rng, n, s, n_clusters):
+    """Sketch-like rows: clustered shared hashes, some short and empty rows."""
+    sk = np.zeros((n, s), np.uint64)
+    lens = np.zeros(n, np.uint32)
+    pools = [np.unique(rng.integers(0, 2**52, 3 * s, dtype=np.uint64)) for _ in range(n_clusters)]
+    for i in range(n):
+        pool = pools[i % n_clusters]
+        m = s if i % 17 else int(rng.integers(0, s))
+        if i % 29 == 0:
+            m = 0
+        share = rng.random()
+        a = pool[rng.random(len(pool)) < share]
+        b = rng.integers(0, 2**52, s, dtype=np.uint64)
+        v = np.unique(np.concatenate([a, b]))[:m]
+        sk[i, :len(v)] = v
+        lens[i] = len(v)
+    return sk, lens
+
+
+@pytest.mark.parametrize("min_ani", [0.0, 0.9, 0.95, 0.99])
+def test_random_pairs_vs_oracle(gpu_ctx, min_ani):
+    rng = np.random.default_rng(3)
+    sk, lens = random_sketch_set(rng, 300, 1000, 7)
+    p = gpu_ctx.pairs(sk, lens, np.float32(min_ani))
+    o = oracle.pairs(sk, lens.astype(np.int32), np.float32(min_ani))
+    assert as_tuples(p) == [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+
+
+def test_pairs_device_partition_union(gpu_ctx):
+    torch = torch_dev()
+    rng = np.random.default_rng(9)
+    n = 333
+    sk, lens = random_sketch_set(rng, n, 1000, 5)
+    d_sk = torch.from_numpy(sk.view(np.int64)).cuda()
+    d_lens = torch.from_numpy(lens.view(np.int32)).cuda()
+    cap = n * n
+    full = None
+    for parts in (1, 2, 3, 5):
+        got = []
+        for part in range(parts):
+            b, e = ga.pair_partition(n, parts, part)
+            d_out = torch.zeros(cap * 4, dtype=torch.int32, device="cuda")
+            d_cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            gpu_ctx.pairs_device(d_sk, d_lens, n, b, e, np.float32(0.9), d_out, cap, d_cnt)
+            torch.cuda.synchronize()
+            c = int(d_cnt.item())
+            assert c <= cap
+            arr = d_out[:c * 4].cpu().numpy().view(np.uint32).reshape(-1, 4)
+            got += [tuple(map(int, r)) for r in arr]
+        got.sort()
+        if full is None:
+            full = got
+            o = oracle.pairs(sk, lens.astype(np.int32), np.float32(0.9))
+            assert full == [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+        assert got == full
+
+
+def synth_packed(ctx, n, glen, cl, rate, seed):
+    torch = torch_dev()
+    d_words = torch.empty(n * glen // 16, dtype=torch.int32, device="cuda")
+    runs = ctx.synth_device(n, glen, cl, rate, seed, d_words)
+    torch.cuda.synchronize()
+    return d_words, runs
+
+
+def test_synthetic_genomes_sketch_and_pairs_vs_oracle(gpu_ctx):
+    torch = torch_dev()
+    n, glen = 24, 200000
+    d_words, runs = synth_packed(gpu_ctx, n, glen, 4, 0.07, 1234)
+    d_out = torch.zeros((n, 1000), dtype=torch.int64, device="cuda")
+    d_lens = torch.zeros(n, dtype=torch.int32, device="cuda")
+    gpu_ctx.sketch_device(d_words, runs, n, d_out, d_lens)
+    torch.cuda.synchronize()
+    words = d_words.cpu().numpy().view(np.uint32)
+    sk = d_out.cpu().numpy().view(np.uint64)
+    lens = d_lens.cpu().numpy().view(np.uint32)
+    osk = np.zeros((n, 1000), np.uint64)
+    for g in range(n):
+        seq = unpack_run(words, int(runs[g]["base"]), glen)
+        exp = oracle.sketch_sequence(seq)
+        assert lens[g] == len(exp) and (sk[g][:lens[g]] == exp).all(), g
+        osk[g] = exp
+    # clusters: members of a cluster are related, clusters are not
+    o = oracle.pairs(osk, lens.astype(np.int32), np.float32(0.9))
+    p = gpu_ctx.pairs(sk, lens, np.float32(0.9))
+    assert as_tuples(p) == [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+    assert all(r["i"] // 4 == r["j"] // 4 for r in p)
+    assert len(p) > 0
+
+
+def test_full_size_properties_c2(gpu_ctx):
+    """C2 shape (1k x 3 Mbp): size-independent properties + oracle spot checks."""
+    torch = torch_dev()
+    n, glen, cl = 1000, 3000000, 10
+    d_words, runs = synth_packed(gpu_ctx, n, glen, cl, 0.07, 2)
+    d_out = torch.zeros((n, 1000), dtype=torch.int64, device="cuda")
+    d_lens = torch.zeros(n, dtype=torch.int32, device="cuda")
+    gpu_ctx.sketch_device(d_words, runs, n, d_out, d_lens)
+    torch.cuda.synchronize()
+    sk = d_out.cpu().numpy().view(np.uint64)
+    lens = d_lens.cpu().numpy().view(np.uint32)
+    assert (lens == 1000).all()
+    assert (np.diff(sk, axis=1) > 0).all()  # ascending, distinct
+    words = None
+    for g in (0, 1, 517, 999):
+        if words is None:
+            words = d_words.cpu().numpy().view(np.uint32)
+        exp = oracle.sketch_sequence(unpack_run(words, int(runs[g]["base"]), glen))
+        assert (sk[g] == exp).all(), g
+    p = gpu_ctx.pairs(sk, lens, np.float32(0.95))
+    assert all(r["i"] // cl == r["j"] // cl for r in p)
+    # spot-check (common, total) of 200 random pairs against the oracle merge
+    rng = np.random.default_rng(0)
+    passing = {(int(r["i"]), int(r["j"])): (int(r["common"]), int(r["total"])) for r in p}
+    for _ in range(200):
+        i, j = sorted(rng.choice(n, 2, replace=False))
+        if rng.random() < 0.5:
+            j = min(n - 1, (i // cl) * cl + int(rng.integers(0, cl)))
+            if j == i:
+                continue
+            i, j = min(i, j), max(i, j)
+        c, t = oracle.raw_distance(sk[i], sk[j])
+        passes = oracle.ani(c, t) >= np.float64(np.float32(0.95))
+        assert ((i, j) in passing) == passes
+        if passes:
+            assert passing[(i, j)] == (c, t)
