@@ -66,6 +66,15 @@ class _Packed(ctypes.Structure):
 
 RUN_DTYPE = np.dtype([("genome", np.uint32), ("len", np.uint32), ("base", np.uint64)])
 
+# torch ships its own libamdhip64 (same SONAME as /opt/rocm's).  Load it
+# first when it is installed so the process has ONE HIP runtime, shared by
+# torch tensors/streams and libgalahgpu; loading ours first would make
+# torch load a second runtime beside it.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover - torch is optional for the ABI
+    torch = None
+
 if not os.path.exists(LIB_PATH):
     raise ImportError("libgalahgpu.so is not built (%s); run `make -C galah_amd/csrc` "
                       "or __graft_entry__.build()" % LIB_PATH)

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -33,6 +34,8 @@ struct gg_ctx {
     hipEvent_t a, b;
     uint64_t work;
   };
+  std::vector<gg::PairSeg> seg_host;
+  bool force_merge = false;  // GALAHGPU_PAIRS_KERNEL=merge (testing)
   bool timing = false;
   std::vector<Timed> timed;
   std::vector<hipEvent_t> spare_events;
@@ -392,7 +395,41 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
   a.out_cap = cap;
   a.count = (unsigned long long*)d_count;
   const uint64_t work = c->timing ? pairs_in_tiles(n, a.tile_begin, a.tile_end) : 0;
-  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs(a, st); }));
+  if (c->force_merge || pairs_table_rows(c->s) == 0) {
+    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs(a, st); }));
+    return GG_OK;
+  }
+  // table kernel: segments of <= kSegTiles column tiles of one tile row
+  c->seg_host.clear();
+  const uint64_t nb = a.n_row_tiles;
+  uint64_t t = 0;
+  for (uint64_t I = 0; I < nb && t < a.tile_end; ++I) {
+    const uint64_t first = t, last = t + (nb - I);
+    const uint64_t lo = std::max(first, a.tile_begin), hi = std::min(last, a.tile_end);
+    for (uint64_t x = lo; x < hi; x += kSegTiles) {
+      const uint64_t y = std::min(hi, x + kSegTiles);
+      c->seg_host.push_back(PairSeg{(uint32_t)I, (uint32_t)(I + (x - first)), (uint32_t)(I + (y - first)), 0});
+    }
+    t = last;
+  }
+  PairSeg* d_segs;
+  GG_HIP(c, scratch_t(c, "pair_segs", std::max<size_t>(c->seg_host.size(), 1), &d_segs));
+  if (!c->seg_host.empty())
+    GG_HIP(c, hipMemcpyAsync(d_segs, c->seg_host.data(), c->seg_host.size() * sizeof(PairSeg),
+                             hipMemcpyHostToDevice, st));
+  PairsTableLaunch b;
+  b.sketches = d_sk;
+  b.lens = d_lens;
+  b.n = n;
+  b.stride = c->s;
+  b.segs = d_segs;
+  b.n_segs = (uint32_t)c->seg_host.size();
+  b.cmin = d_cmin;
+  b.tmax = 2 * c->s;
+  b.out = d_out;
+  b.out_cap = cap;
+  b.count = (unsigned long long*)d_count;
+  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs_table(b, st); }));
   return GG_OK;
 }
 
@@ -531,6 +568,8 @@ gg_ctx* gg_create(int kmer_length, uint32_t sketch_size, uint64_t hash_seed, int
   c->s = sketch_size;
   c->seed = hash_seed;
   c->device = dev;
+  const char* pk = getenv("GALAHGPU_PAIRS_KERNEL");
+  c->force_merge = pk && strcmp(pk, "merge") == 0;
   hipError_t e = hipSetDevice(dev);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   (void)e;
@@ -567,7 +606,7 @@ gg_status gg_sketch_device(gg_ctx* ctx, const uint32_t* d_words, uint64_t n_word
   if ((n_runs && (!runs || !d_words)) || (n_genomes && (!d_out || !d_lens)))
     return fail(ctx, GG_ERR_INVALID_ARG, "gg_sketch_device: null buffer");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
-  hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
   return sketch_core(ctx, d_words, n_words, runs, n_runs, n_genomes, d_out, d_lens, st);
 }
 
@@ -643,7 +682,7 @@ gg_status gg_pairs_device(gg_ctx* ctx, const uint64_t* d_sketches, const uint32_
     return fail(ctx, GG_ERR_INVALID_ARG, "gg_pairs_device: null buffer");
   if (std::isnan(min_ani)) return fail(ctx, GG_ERR_INVALID_ARG, "min_ani is NaN");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
-  hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
   return pairs_core(ctx, d_sketches, d_lens, n, tile_begin, tile_end, min_ani, d_out, out_cap,
                     d_count, st);
 }
@@ -789,7 +828,7 @@ gg_status gg_synth_clustered_device(gg_ctx* ctx, uint32_t first_genome, uint32_t
   if (!d_words || !runs || genome_len % 16 || genome_len < (uint32_t)ctx->k || cluster_size == 0)
     return fail(ctx, GG_ERR_INVALID_ARG, "gg_synth_clustered_device: bad arguments");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
-  hipStream_t st = stream ? (hipStream_t)stream : ctx->stream;
+  hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
   GG_HIP(ctx, launch_synth(first_genome, n_genomes, genome_len, cluster_size, max_sub_rate, seed, d_words, st));
   for (uint32_t g = 0; g < n_genomes; ++g) runs[g] = gg_run{g, genome_len, (uint64_t)g * genome_len};
   return GG_OK;

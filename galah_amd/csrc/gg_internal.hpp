@@ -73,6 +73,28 @@ struct PairsLaunch {
 };
 hipError_t launch_pairs(const PairsLaunch& a, hipStream_t st);
 
+// Table kernel work unit: tile row I, column tiles [J0, J1) (same row).
+struct PairSeg {
+  uint32_t I, J0, J1, pad;
+};
+constexpr uint32_t kSegTiles = 16;
+struct PairsTableLaunch {
+  const uint64_t* sketches;
+  const uint32_t* lens;
+  uint32_t n;
+  uint32_t stride;
+  const PairSeg* segs;
+  uint32_t n_segs;
+  const uint32_t* cmin;
+  uint32_t tmax;
+  gg_pair* out;
+  uint64_t out_cap;
+  unsigned long long* count;
+};
+// rows per LDS table for sketch size s (0: table kernel not applicable)
+uint32_t pairs_table_rows(uint32_t s);
+hipError_t launch_pairs_table(const PairsTableLaunch& a, hipStream_t st);
+
 // synth.hip
 hipError_t launch_synth(uint32_t first_genome, uint32_t n_genomes, uint32_t genome_len,
                         uint32_t cluster_size, float max_sub_rate,

@@ -80,7 +80,349 @@ __global__ __launch_bounds__(kBlock) void pairs_merge_kernel(PairsLaunch a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// K2 table kernel.
+//
+// A workgroup owns R consecutive row sketches (a "row block") and a run of
+// up to kSegTiles column tiles of the same tile row.  It builds, in LDS, a
+// value-bucketed table of the row block's hashes: keys sorted inside each
+// bucket, an R-bit row mask per entry (a hash shared by several rows is
+// several entries).  Its 16 waves then stream column sketches: each lane
+// looks one column hash up (bucket directory read + short sorted scan), and
+// the hit masks are accumulated per row in byte counters.  For a column
+// this replaces R sorted merges of ~2s steps by s table lookups.
+//
+// total = i + j - common at first exhaustion of finch's merge equals
+//   |A| + rank_B(last A) - common        if last A <= last B
+//   rank_A(last B) + |B| - common        otherwise
+// rank_B comes from a ballot per streamed round; rank_A from a 64-way
+// search of the row sketch.  Pass test: common >= cmin[total].
+//
+// Blocks of one segment are placed 8 apart in blockIdx so they share an XCD
+// (round-robin dispatch) and stream the same columns through one L2.
+// ---------------------------------------------------------------------------
+constexpr int kTableThreads = 1024;
+constexpr int kTableWaves = kTableThreads / 64;
+constexpr uint32_t kNB = 4096;  // buckets
+constexpr uint32_t kKeyCap = 8192;
+constexpr uint32_t kEPT = kKeyCap / kTableThreads;  // entries per thread in the build
+
+// keys region doubles as the kNB u32 bucket counters during the build
+__host__ __device__ constexpr size_t table_key_bytes(uint32_t cap) {
+  return (size_t)cap * 8 > (size_t)kNB * 4 ? (size_t)cap * 8 : (size_t)kNB * 4;
+}
+__host__ __device__ constexpr size_t table_lds_bytes(uint32_t cap) {
+  return 256 + table_key_bytes(cap) + ((cap + 7) & ~7u) + (size_t)(kNB + 1) * 2;
+}
+
+struct TableMeta {
+  uint64_t last[8];     // last (largest) hash of each row
+  uint32_t len[8];
+  uint32_t pre[9];      // prefix of len
+  uint64_t maxkey;
+  uint32_t shift_r;     // top32(b) = b >> shift_r  (or << shift_l)
+  uint32_t shift_l;
+  uint32_t scale;
+  uint32_t nrows;
+};
+
+__device__ __forceinline__ uint32_t top32(uint64_t b, uint32_t sr, uint32_t sl) {
+  return (uint32_t)((b >> sr) << sl);
+}
+
+__device__ __forceinline__ uint32_t bucket_of(uint64_t b, uint32_t sr, uint32_t sl, uint32_t scale) {
+  return (uint32_t)(((uint64_t)top32(b, sr, sl) * scale) >> 32);
+}
+
+// bytes 0..3 of the result = bits 0..3 of x (x < 16)
+__device__ __forceinline__ uint32_t spread4(uint32_t x) { return (x * 0x204081u) & 0x01010101u; }
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// #{ e < len : A[e] <= x } for ascending A, all 64 lanes cooperating.
+__device__ uint32_t wave_rank(const uint64_t* __restrict__ A, uint32_t len, uint64_t x,
+                              uint32_t lane) {
+  uint32_t lo = 0, hi = len;
+  while (hi - lo > 64) {
+    const uint32_t step = (hi - lo + 63) / 64;
+    const uint32_t idx = lo + lane * step;
+    const bool p = (idx < hi) && (A[idx] <= x);
+    const uint32_t c = __popcll(__ballot(p));
+    const uint32_t nlo = c ? lo + (c - 1) * step + 1 : lo;
+    const uint32_t nhi = min(hi, lo + c * step);
+    lo = nlo;
+    hi = nhi;
+  }
+  const uint32_t idx = lo + lane;
+  const bool p = (idx < hi) && (A[idx] <= x);
+  return lo + __popcll(__ballot(p));
+}
+
+template <int R>
+__global__ __launch_bounds__(kTableThreads) void pairs_table_kernel(PairsTableLaunch a) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  TableMeta& meta = *reinterpret_cast<TableMeta*>(smem);
+  uint64_t* keys = reinterpret_cast<uint64_t*>(smem + 256);
+  const uint32_t cap = (uint32_t)R * a.stride;
+  const size_t key_bytes = table_key_bytes(cap);
+  uint8_t* masks = smem + 256 + key_bytes;
+  uint16_t* off = reinterpret_cast<uint16_t*>(smem + 256 + key_bytes + ((cap + 7) & ~7u));
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(keys);  // build-time bucket counters
+
+  constexpr uint32_t G = kTile / R;  // row blocks per segment
+  const uint32_t b = blockIdx.x;
+  const uint32_t q = b >> 3;
+  const uint32_t rb = q % G;
+  const uint32_t seg_id = (q / G) * 8 + (b & 7);
+  if (seg_id >= a.n_segs) return;
+  const PairSeg sg = a.segs[seg_id];
+  const uint32_t row0 = sg.I * kTile + rb * R;
+  if (row0 >= a.n) return;
+  const uint32_t c0 = max(sg.J0 * kTile, row0 + 1);
+  const uint32_t c1 = min(sg.J1 * kTile, a.n);
+  if (c0 >= c1) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // ---- row-block metadata
+  if (tid == 0) {
+    const uint32_t nrows = min((uint32_t)R, a.n - row0);
+    uint64_t mx = 0;
+    uint32_t acc = 0;
+    for (int r = 0; r < 8; ++r) {
+      uint32_t l = 0;
+      uint64_t last = 0;
+      if (r < (int)nrows) {
+        l = a.lens[row0 + r];
+        if (l) last = a.sketches[(uint64_t)(row0 + r) * a.stride + l - 1];
+      }
+      meta.len[r] = l;
+      meta.last[r] = last;
+      meta.pre[r] = acc;
+      acc += l;
+      if (l && last > mx) mx = last;
+    }
+    meta.pre[8] = acc;
+    meta.maxkey = mx;
+    const uint32_t L = mx ? 64 - __builtin_clzll(mx) : 1;
+    meta.shift_r = L > 32 ? L - 32 : 0;
+    meta.shift_l = L > 32 ? 0 : 32 - L;
+    const uint64_t t = (uint64_t)top32(mx, meta.shift_r, meta.shift_l) + 1;  // in (2^31, 2^32]
+    meta.scale = (uint32_t)(((uint64_t)kNB << 32) / t);
+    meta.nrows = nrows;
+  }
+  for (uint32_t i = tid; i < kNB; i += kTableThreads) cnt[i] = 0;
+  __syncthreads();
+  const uint32_t E = meta.pre[8];
+  const uint32_t sr = meta.shift_r, sl = meta.shift_l, scale = meta.scale;
+
+  // ---- build pass 1: bucket counts, each entry's rank inside its bucket
+  uint32_t pos[kEPT];
+#pragma unroll
+  for (uint32_t t = 0; t < kEPT; ++t) {
+    const uint32_t e = tid + t * kTableThreads;
+    pos[t] = 0;
+    if (e < E) {
+      uint32_t r = 0;
+#pragma unroll
+      for (int x = 1; x < R; ++x) r += (e >= meta.pre[x]) ? 1u : 0u;
+      const uint64_t key = a.sketches[(uint64_t)(row0 + r) * a.stride + (e - meta.pre[r])];
+      pos[t] = atomicAdd(&cnt[bucket_of(key, sr, sl, scale)], 1u);
+    }
+  }
+  __syncthreads();
+  // exclusive scan of kNB counters -> off (u16); kNB / 1024 = 4 per thread
+  {
+    __shared__ uint32_t wsum[kTableWaves];
+    const uint32_t base = tid * (kNB / kTableThreads);
+    uint32_t v[kNB / kTableThreads];
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kNB / kTableThreads; ++i) {
+      v[i] = cnt[base + i];
+      s += v[i];
+    }
+    // inclusive scan of s across the wave
+    uint32_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t wpre = 0;
+    for (uint32_t w = 0; w < wave; ++w) wpre += wsum[w];
+    uint32_t run = wpre + inc - s;
+#pragma unroll
+    for (uint32_t i = 0; i < kNB / kTableThreads; ++i) {
+      off[base + i] = (uint16_t)run;
+      run += v[i];
+    }
+    if (tid == kTableThreads - 1) off[kNB] = (uint16_t)run;
+  }
+  __syncthreads();
+  // ---- build pass 2: scatter keys and row bits
+#pragma unroll
+  for (uint32_t t = 0; t < kEPT; ++t) {
+    const uint32_t e = tid + t * kTableThreads;
+    if (e < E) {
+      uint32_t r = 0;
+#pragma unroll
+      for (int x = 1; x < R; ++x) r += (e >= meta.pre[x]) ? 1u : 0u;
+      const uint64_t key = a.sketches[(uint64_t)(row0 + r) * a.stride + (e - meta.pre[r])];
+      const uint32_t slot = off[bucket_of(key, sr, sl, scale)] + pos[t];
+      keys[slot] = key;
+      masks[slot] = (uint8_t)(1u << r);
+    }
+  }
+  __syncthreads();
+  // ---- sort each bucket (insertion sort; buckets hold ~E/kNB entries)
+  for (uint32_t bk = tid; bk < kNB; bk += kTableThreads) {
+    const uint32_t s0 = off[bk], s1 = off[bk + 1];
+    for (uint32_t i = s0 + 1; i < s1; ++i) {
+      const uint64_t k = keys[i];
+      const uint8_t m = masks[i];
+      uint32_t j = i;
+      while (j > s0 && keys[j - 1] > k) {
+        keys[j] = keys[j - 1];
+        masks[j] = masks[j - 1];
+        --j;
+      }
+      keys[j] = k;
+      masks[j] = m;
+    }
+  }
+  __syncthreads();
+
+  // ---- stream columns
+  const uint64_t maxkey = meta.maxkey;
+  const uint32_t nrows = meta.nrows;
+  uint64_t xr[R];
+  uint32_t lr[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    xr[r] = meta.last[r];
+    lr[r] = meta.len[r];
+  }
+  for (uint32_t j = c0 + wave; j < c1; j += kTableWaves) {
+    const uint32_t lb = a.lens[j];
+    const uint64_t* B = a.sketches + (uint64_t)j * a.stride;
+    const uint64_t lastB = lb ? B[lb - 1] : 0;
+    uint32_t acc_lo = 0, acc_hi = 0;
+    uint32_t cntB[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) cntB[r] = 0;
+    for (uint32_t base = 0; base < lb; base += 64) {
+      const uint32_t e = base + lane;
+      const bool valid = e < lb;
+      const uint64_t bv = valid ? B[e] : ~0ull;
+      uint32_t m = 0;
+      if (valid && bv <= maxkey) {
+        const uint32_t bk = bucket_of(bv, sr, sl, scale);
+        uint32_t k = off[bk];
+        const uint32_t en = off[bk + 1];
+        while (k < en && keys[k] < bv) ++k;
+        while (k < en && keys[k] == bv) {
+          m |= masks[k];
+          ++k;
+        }
+      }
+      acc_lo += spread4(m & 15u);
+      if (R > 4) acc_hi += spread4(m >> 4);
+#pragma unroll
+      for (int r = 0; r < R; ++r) cntB[r] += __popcll(__ballot(valid && bv <= xr[r]));
+    }
+    // per-row common counts
+    const uint32_t s0 = wave_sum(acc_lo & 0x00FF00FFu);
+    const uint32_t s1 = wave_sum((acc_lo >> 8) & 0x00FF00FFu);
+    uint32_t s2 = 0, s3 = 0;
+    if (R > 4) {
+      s2 = wave_sum(acc_hi & 0x00FF00FFu);
+      s3 = wave_sum((acc_hi >> 8) & 0x00FF00FFu);
+    }
+    uint32_t rankA[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      rankA[r] = 0;
+      if (r < (int)nrows && lr[r] && lb && xr[r] > lastB)
+        rankA[r] = wave_rank(a.sketches + (uint64_t)(row0 + r) * a.stride, lr[r], lastB, lane);
+    }
+    // lane r < R evaluates pair (row0 + r, j)
+    uint32_t cb = 0, ra = 0, la = 0;
+    uint64_t x = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (lane == (uint32_t)r) {
+        cb = cntB[r];
+        ra = rankA[r];
+        la = lr[r];
+        x = xr[r];
+      }
+    }
+    const uint32_t which = (lane & 1) + 2 * ((lane >> 2) & 1);
+    const uint32_t sv = which == 0 ? s0 : which == 1 ? s1 : which == 2 ? s2 : s3;
+    uint32_t common = (sv >> (16 * ((lane >> 1) & 1))) & 0xFFFFu;
+    uint32_t total;
+    if (la == 0 || lb == 0) {
+      common = 0;
+      total = 0;
+    } else if (x <= lastB) {
+      total = la + cb - common;
+    } else {
+      total = ra + lb - common;
+    }
+    const uint32_t i = row0 + lane;
+    const bool pass = (lane < nrows) && (j > i) && (total <= a.tmax) && (common >= a.cmin[total]);
+    const unsigned long long mk = __ballot(pass);
+    if (mk) {
+      const uint32_t first = __builtin_ctzll(mk);
+      unsigned long long obase = 0;
+      if (lane == first) obase = atomicAdd(a.count, (unsigned long long)__popcll(mk));
+      obase = __shfl(obase, first);
+      if (pass) {
+        const unsigned long long slot = obase + __popcll(mk & ((1ull << lane) - 1ull));
+        if (slot < a.out_cap) a.out[slot] = gg_pair{i, j, common, total};
+      }
+    }
+  }
+}
+
+template <int R>
+hipError_t launch_table_r(const PairsTableLaunch& a, hipStream_t st) {
+  const size_t lds = table_lds_bytes((uint32_t)R * a.stride);
+  hipError_t e = hipFuncSetAttribute((const void*)pairs_table_kernel<R>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  constexpr uint32_t G = kTile / R;
+  const uint64_t groups = (a.n_segs + 7) / 8;
+  const uint64_t blocks = groups * 8 * G;
+  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pairs_table_kernel<R>, dim3((uint32_t)blocks), dim3(kTableThreads), lds, st, a);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+uint32_t pairs_table_rows(uint32_t s) {
+  uint32_t R = 8;
+  while (R > 1 && R * s > kKeyCap) R >>= 1;
+  return (R * s <= kKeyCap) ? R : 0;
+}
+
+hipError_t launch_pairs_table(const PairsTableLaunch& a, hipStream_t st) {
+  if (a.n_segs == 0) return hipSuccess;
+  switch (pairs_table_rows(a.stride)) {
+    case 8: return launch_table_r<8>(a, st);
+    case 4: return launch_table_r<4>(a, st);
+    case 2: return launch_table_r<2>(a, st);
+    case 1: return launch_table_r<1>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 hipError_t launch_pairs(const PairsLaunch& a, hipStream_t st) {
   if (a.tile_end <= a.tile_begin) return hipSuccess;

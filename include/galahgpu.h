@@ -29,8 +29,11 @@
  *   - There is NO CPU fallback: gg_create fails with GG_ERR_NO_DEVICE when
  *     no MI355X (gfx950) device is visible.
  *   - *_device entry points take device pointers on the context's device
- *     and enqueue on the given hipStream_t (passed as void*); they do not
- *     synchronise unless stated.
+ *     and enqueue on the given hipStream_t (passed as void*; NULL is the
+ *     default stream, as in HIP); they do not synchronise unless stated.
+ *     When the caller shares the process with PyTorch, torch's bundled
+ *     libamdhip64 must be the one loaded (import torch first) so that
+ *     streams and device pointers belong to one HIP runtime.
  */
 #ifndef GALAHGPU_H
 #define GALAHGPU_H

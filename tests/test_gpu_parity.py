@@ -227,3 +227,57 @@ def test_full_size_properties_c2(gpu_ctx):
         assert ((i, j) in passing) == passes
         if passes:
             assert passing[(i, j)] == (c, t)
+
+
+def adversarial_sketches(rng, n, s):
+    """Identical rows, prefix rows, extreme values (0 and 2^64-1), equal
+    last elements, empty and singleton rows, a spread of genome-size-like
+    value ranges."""
+    rows = []
+    base = np.unique(rng.integers(0, 2**63, 4 * s, dtype=np.uint64))
+    for i in range(n):
+        kind = i % 9
+        if kind == 0:
+            v = base[:s]
+        elif kind == 1:
+            v = base[: s // 2]                       # prefix of kind 0
+        elif kind == 2:
+            v = np.unique(np.concatenate([base[:s - 1], [np.uint64(2**64 - 1)]]))
+        elif kind == 3:
+            v = np.unique(np.concatenate([[np.uint64(0)], base[1:s]]))
+        elif kind == 4:
+            v = np.zeros(0, np.uint64)
+        elif kind == 5:
+            v = base[s // 3: s // 3 + 1]
+        elif kind == 6:                              # small "genome": large hash range
+            v = np.unique(rng.integers(0, 2**64 - 1, s, dtype=np.uint64))
+        elif kind == 7:                              # shares the last element with kind 0
+            v = np.unique(np.concatenate([base[s // 2: s - 1][rng.random(s // 2 - 1) < 0.7], [base[s - 1]]]))
+        else:
+            scale = np.uint64(2 ** int(rng.integers(40, 63)))
+            v = np.unique(np.concatenate([base[:s][rng.random(s) < 0.5],
+                                          rng.integers(0, int(scale), s, dtype=np.uint64)]))[:s]
+        rows.append(v[:s])
+    sk = np.zeros((n, s), np.uint64)
+    lens = np.zeros(n, np.uint32)
+    for i, v in enumerate(rows):
+        sk[i, :len(v)] = v
+        lens[i] = len(v)
+    return sk, lens
+
+
+@pytest.mark.parametrize("s", [1000, 2000, 4000, 8000, 10000, 100, 37])
+@pytest.mark.parametrize("min_ani", [0.0, 0.9])
+def test_table_and_merge_kernels_match_oracle(monkeypatch, s, min_ani):
+    rng = np.random.default_rng(s)
+    n = 150 if s >= 4000 else 260
+    sk, lens = adversarial_sketches(rng, n, s)
+    o = oracle.pairs(sk, lens.astype(np.int32), np.float32(min_ani))
+    exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+    got = {}
+    for kern in ("table", "merge"):
+        monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", kern)
+        with ga.Context(k=21, sketch_size=s) as ctx:
+            got[kern] = as_tuples(ctx.pairs(sk, lens, np.float32(min_ani)))
+    assert got["merge"] == exp
+    assert got["table"] == exp
