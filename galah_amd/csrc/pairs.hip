@@ -106,13 +106,19 @@ constexpr int kTableWaves = kTableThreads / 64;
 constexpr uint32_t kNB = 4096;  // buckets
 constexpr uint32_t kKeyCap = 8192;
 constexpr uint32_t kEPT = kKeyCap / kTableThreads;  // entries per thread in the build
+constexpr int kChunk = 16;                          // column rounds held in registers
 
-// keys region doubles as the kNB u32 bucket counters during the build
-__host__ __device__ constexpr size_t table_key_bytes(uint32_t cap) {
-  return (size_t)cap * 8 > (size_t)kNB * 4 ? (size_t)cap * 8 : (size_t)kNB * 4;
+// LDS layout (dynamic, base 16-B aligned):
+//   meta 256 B | keys u64[cap+2] (build: kNB u32 counters) | masks u8[cap+8]
+//   | dir u32[kNB] (start | count << 16) | samp u16[(cap/64+2)*8]
+__host__ __device__ constexpr size_t tk_keys(uint32_t cap) {
+  return ((size_t)cap + 2) * 8 > (size_t)kNB * 4 ? ((size_t)cap + 2) * 8 : (size_t)kNB * 4;
 }
+__host__ __device__ constexpr size_t tk_masks(uint32_t cap) { return ((size_t)cap + 8 + 15) & ~(size_t)15; }
+__host__ __device__ constexpr size_t tk_dir() { return (size_t)kNB * 4; }
+__host__ __device__ constexpr size_t tk_samp(uint32_t cap) { return (((size_t)cap / 64 + 2) * 8 * 2 + 15) & ~(size_t)15; }
 __host__ __device__ constexpr size_t table_lds_bytes(uint32_t cap) {
-  return 256 + table_key_bytes(cap) + ((cap + 7) & ~7u) + (size_t)(kNB + 1) * 2;
+  return 256 + tk_keys(cap) + tk_masks(cap) + tk_dir() + tk_samp(cap);
 }
 
 struct TableMeta {
@@ -120,7 +126,7 @@ struct TableMeta {
   uint32_t len[8];
   uint32_t pre[9];      // prefix of len
   uint64_t maxkey;
-  uint32_t shift_r;     // top32(b) = b >> shift_r  (or << shift_l)
+  uint32_t shift_r;     // top32(b) = (b >> shift_r) << shift_l
   uint32_t shift_l;
   uint32_t scale;
   uint32_t nrows;
@@ -130,6 +136,8 @@ __device__ __forceinline__ uint32_t top32(uint64_t b, uint32_t sr, uint32_t sl) 
   return (uint32_t)((b >> sr) << sl);
 }
 
+// Monotone in b: the table is globally sorted by key (bucket order, then
+// sorted inside a bucket), which rank_A relies on.
 __device__ __forceinline__ uint32_t bucket_of(uint64_t b, uint32_t sr, uint32_t sl, uint32_t scale) {
   return (uint32_t)(((uint64_t)top32(b, sr, sl) * scale) >> 32);
 }
@@ -143,34 +151,15 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-// #{ e < len : A[e] <= x } for ascending A, all 64 lanes cooperating.
-__device__ uint32_t wave_rank(const uint64_t* __restrict__ A, uint32_t len, uint64_t x,
-                              uint32_t lane) {
-  uint32_t lo = 0, hi = len;
-  while (hi - lo > 64) {
-    const uint32_t step = (hi - lo + 63) / 64;
-    const uint32_t idx = lo + lane * step;
-    const bool p = (idx < hi) && (A[idx] <= x);
-    const uint32_t c = __popcll(__ballot(p));
-    const uint32_t nlo = c ? lo + (c - 1) * step + 1 : lo;
-    const uint32_t nhi = min(hi, lo + c * step);
-    lo = nlo;
-    hi = nhi;
-  }
-  const uint32_t idx = lo + lane;
-  const bool p = (idx < hi) && (A[idx] <= x);
-  return lo + __popcll(__ballot(p));
-}
-
 template <int R>
-__global__ __launch_bounds__(kTableThreads) void pairs_table_kernel(PairsTableLaunch a) {
+__global__ __launch_bounds__(kTableThreads, 1) void pairs_table_kernel(PairsTableLaunch a) {
   extern __shared__ __align__(16) uint8_t smem[];
   TableMeta& meta = *reinterpret_cast<TableMeta*>(smem);
-  uint64_t* keys = reinterpret_cast<uint64_t*>(smem + 256);
   const uint32_t cap = (uint32_t)R * a.stride;
-  const size_t key_bytes = table_key_bytes(cap);
-  uint8_t* masks = smem + 256 + key_bytes;
-  uint16_t* off = reinterpret_cast<uint16_t*>(smem + 256 + key_bytes + ((cap + 7) & ~7u));
+  uint64_t* keys = reinterpret_cast<uint64_t*>(smem + 256);
+  uint8_t* masks = smem + 256 + tk_keys(cap);
+  uint32_t* dir = reinterpret_cast<uint32_t*>(smem + 256 + tk_keys(cap) + tk_masks(cap));
+  uint16_t* samp = reinterpret_cast<uint16_t*>(smem + 256 + tk_keys(cap) + tk_masks(cap) + tk_dir());
   uint32_t* cnt = reinterpret_cast<uint32_t*>(keys);  // build-time bucket counters
 
   constexpr uint32_t G = kTile / R;  // row blocks per segment
@@ -234,18 +223,18 @@ __global__ __launch_bounds__(kTableThreads) void pairs_table_kernel(PairsTableLa
     }
   }
   __syncthreads();
-  // exclusive scan of kNB counters -> off (u16); kNB / 1024 = 4 per thread
+  // exclusive scan of the kNB counters -> dir = start | count << 16
   {
     __shared__ uint32_t wsum[kTableWaves];
-    const uint32_t base = tid * (kNB / kTableThreads);
-    uint32_t v[kNB / kTableThreads];
+    constexpr uint32_t PT = kNB / kTableThreads;
+    const uint32_t base = tid * PT;
+    uint32_t v[PT];
     uint32_t s = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < kNB / kTableThreads; ++i) {
+    for (uint32_t i = 0; i < PT; ++i) {
       v[i] = cnt[base + i];
       s += v[i];
     }
-    // inclusive scan of s across the wave
     uint32_t inc = s;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -254,15 +243,13 @@ __global__ __launch_bounds__(kTableThreads) void pairs_table_kernel(PairsTableLa
     }
     if (lane == 63) wsum[wave] = inc;
     __syncthreads();
-    uint32_t wpre = 0;
-    for (uint32_t w = 0; w < wave; ++w) wpre += wsum[w];
-    uint32_t run = wpre + inc - s;
+    uint32_t run = inc - s;
+    for (uint32_t w = 0; w < wave; ++w) run += wsum[w];
 #pragma unroll
-    for (uint32_t i = 0; i < kNB / kTableThreads; ++i) {
-      off[base + i] = (uint16_t)run;
+    for (uint32_t i = 0; i < PT; ++i) {
+      dir[base + i] = run | (v[i] << 16);
       run += v[i];
     }
-    if (tid == kTableThreads - 1) off[kNB] = (uint16_t)run;
   }
   __syncthreads();
   // ---- build pass 2: scatter keys and row bits
@@ -274,15 +261,20 @@ __global__ __launch_bounds__(kTableThreads) void pairs_table_kernel(PairsTableLa
 #pragma unroll
       for (int x = 1; x < R; ++x) r += (e >= meta.pre[x]) ? 1u : 0u;
       const uint64_t key = a.sketches[(uint64_t)(row0 + r) * a.stride + (e - meta.pre[r])];
-      const uint32_t slot = off[bucket_of(key, sr, sl, scale)] + pos[t];
+      const uint32_t slot = (dir[bucket_of(key, sr, sl, scale)] & 0xFFFFu) + pos[t];
       keys[slot] = key;
       masks[slot] = (uint8_t)(1u << r);
     }
   }
+  if (tid < 2) {
+    keys[E + tid] = ~0ull;  // pads for paired reads past a bucket's end
+    masks[E + tid] = 0;
+  }
   __syncthreads();
   // ---- sort each bucket (insertion sort; buckets hold ~E/kNB entries)
   for (uint32_t bk = tid; bk < kNB; bk += kTableThreads) {
-    const uint32_t s0 = off[bk], s1 = off[bk + 1];
+    const uint32_t d = dir[bk];
+    const uint32_t s0 = d & 0xFFFFu, s1 = s0 + (d >> 16);
     for (uint32_t i = s0 + 1; i < s1; ++i) {
       const uint64_t k = keys[i];
       const uint8_t m = masks[i];
@@ -294,6 +286,27 @@ __global__ __launch_bounds__(kTableThreads) void pairs_table_kernel(PairsTableLa
       }
       keys[j] = k;
       masks[j] = m;
+    }
+  }
+  __syncthreads();
+  // ---- per-row prefix counts every 64 entries (rank_A support)
+  const uint32_t nblk = (E + 63) / 64;
+  for (uint32_t blk = wave; blk < nblk; blk += kTableWaves) {
+    const uint32_t e = blk * 64 + lane;
+    const uint32_t m = e < E ? masks[e] : 0u;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const uint32_t c = __popcll(__ballot((m >> r) & 1u));
+      if (lane == (uint32_t)r) samp[(blk + 1) * 8 + r] = (uint16_t)c;
+    }
+  }
+  __syncthreads();
+  if (tid < 8) {
+    uint32_t run = 0;
+    samp[tid] = 0;
+    for (uint32_t blk = 1; blk <= nblk; ++blk) {
+      run += samp[blk * 8 + tid];
+      samp[blk * 8 + tid] = (uint16_t)run;
     }
   }
   __syncthreads();
@@ -316,25 +329,34 @@ __global__ __launch_bounds__(kTableThreads) void pairs_table_kernel(PairsTableLa
     uint32_t cntB[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) cntB[r] = 0;
-    for (uint32_t base = 0; base < lb; base += 64) {
-      const uint32_t e = base + lane;
-      const bool valid = e < lb;
-      const uint64_t bv = valid ? B[e] : ~0ull;
-      uint32_t m = 0;
-      if (valid && bv <= maxkey) {
-        const uint32_t bk = bucket_of(bv, sr, sl, scale);
-        uint32_t k = off[bk];
-        const uint32_t en = off[bk + 1];
-        while (k < en && keys[k] < bv) ++k;
-        while (k < en && keys[k] == bv) {
-          m |= masks[k];
-          ++k;
-        }
-      }
-      acc_lo += spread4(m & 15u);
-      if (R > 4) acc_hi += spread4(m >> 4);
+    for (uint32_t cb = 0; cb < lb; cb += kChunk * 64) {
+      uint64_t v[kChunk];
 #pragma unroll
-      for (int r = 0; r < R; ++r) cntB[r] += __popcll(__ballot(valid && bv <= xr[r]));
+      for (int t = 0; t < kChunk; ++t) {
+        const uint32_t e = cb + t * 64 + lane;
+        v[t] = e < lb ? B[e] : ~0ull;
+      }
+#pragma unroll
+      for (int t = 0; t < kChunk; ++t) {
+        if (cb + t * 64 >= lb) break;
+        const uint64_t bv = v[t];
+        const bool valid = cb + t * 64 + lane < lb;
+        uint32_t m = 0;
+        if (valid && bv <= maxkey) {
+          const uint32_t d = dir[bucket_of(bv, sr, sl, scale)];
+          const uint32_t st = d & 0xFFFFu, n = d >> 16;
+          for (uint32_t k = 0; k < n; k += 2) {
+            const uint64_t k0 = keys[st + k], k1 = keys[st + k + 1];
+            if (k0 == bv) m |= masks[st + k];
+            if (k1 == bv && k + 1 < n) m |= masks[st + k + 1];
+            if (k1 > bv) break;
+          }
+        }
+        acc_lo += spread4(m & 15u);
+        if (R > 4) acc_hi += spread4(m >> 4);
+#pragma unroll
+        for (int r = 0; r < R; ++r) cntB[r] += __popcll(__ballot(valid && bv <= xr[r]));
+      }
     }
     // per-row common counts
     const uint32_t s0 = wave_sum(acc_lo & 0x00FF00FFu);
@@ -344,21 +366,38 @@ __global__ __launch_bounds__(kTableThreads) void pairs_table_kernel(PairsTableLa
       s2 = wave_sum(acc_hi & 0x00FF00FFu);
       s3 = wave_sum((acc_hi >> 8) & 0x00FF00FFu);
     }
-    uint32_t rankA[R];
+    // rank_A(last B) for every row from the sorted table: entries [0, p)
+    // are the keys <= last B
+    uint32_t rank_lane = 0;  // lane r < 8: #entries of row r with key <= last B
+    if (lb) {
+      uint32_t p;
+      if (lastB >= maxkey) {
+        p = E;
+      } else {
+        const uint32_t d = dir[bucket_of(lastB, sr, sl, scale)];
+        const uint32_t st = d & 0xFFFFu, n = d >> 16;
+        p = st;
+        for (uint32_t k0 = 0; k0 < n; k0 += 64) {
+          const uint32_t k = k0 + lane;
+          p += __popcll(__ballot(k < n && keys[st + k] <= lastB));
+        }
+      }
+      const uint32_t blk = p >> 6;
+      const uint32_t e = (blk << 6) + lane;
+      const uint32_t mm = e < p ? masks[e] : 0u;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      rankA[r] = 0;
-      if (r < (int)nrows && lr[r] && lb && xr[r] > lastB)
-        rankA[r] = wave_rank(a.sketches + (uint64_t)(row0 + r) * a.stride, lr[r], lastB, lane);
+      for (int r = 0; r < 8; ++r) {
+        const uint32_t c = __popcll(__ballot((mm >> r) & 1u));
+        if (lane == (uint32_t)r) rank_lane = samp[blk * 8 + r] + c;
+      }
     }
     // lane r < R evaluates pair (row0 + r, j)
-    uint32_t cb = 0, ra = 0, la = 0;
+    uint32_t cb = 0, la = 0;
     uint64_t x = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (lane == (uint32_t)r) {
         cb = cntB[r];
-        ra = rankA[r];
         la = lr[r];
         x = xr[r];
       }
@@ -373,7 +412,7 @@ __global__ __launch_bounds__(kTableThreads) void pairs_table_kernel(PairsTableLa
     } else if (x <= lastB) {
       total = la + cb - common;
     } else {
-      total = ra + lb - common;
+      total = rank_lane + lb - common;
     }
     const uint32_t i = row0 + lane;
     const bool pass = (lane < nrows) && (j > i) && (total <= a.tmax) && (common >= a.cmin[total]);

@@ -252,7 +252,8 @@ def adversarial_sketches(rng, n, s):
         elif kind == 6:                              # small "genome": large hash range
             v = np.unique(rng.integers(0, 2**64 - 1, s, dtype=np.uint64))
         elif kind == 7:                              # shares the last element with kind 0
-            v = np.unique(np.concatenate([base[s // 2: s - 1][rng.random(s // 2 - 1) < 0.7], [base[s - 1]]]))
+            mid = base[s // 2: s - 1]
+            v = np.unique(np.concatenate([mid[rng.random(len(mid)) < 0.7], [base[s - 1]]]))
         else:
             scale = np.uint64(2 ** int(rng.integers(40, 63)))
             v = np.unique(np.concatenate([base[:s][rng.random(s) < 0.5],
