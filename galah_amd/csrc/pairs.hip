@@ -104,21 +104,24 @@ __global__ __launch_bounds__(kBlock) void pairs_merge_kernel(PairsLaunch a) {
 constexpr int kTableThreads = 1024;
 constexpr int kTableWaves = kTableThreads / 64;
 constexpr uint32_t kNB = 4096;  // buckets
+constexpr uint32_t kNG = kNB / 64;  // bucket groups (rank_A prefix samples)
 constexpr uint32_t kKeyCap = 8192;
 constexpr uint32_t kEPT = kKeyCap / kTableThreads;  // entries per thread in the build
 constexpr int kChunk = 16;                          // column rounds held in registers
 
 // LDS layout (dynamic, base 16-B aligned):
-//   meta 256 B | keys u64[cap+2] (build: kNB u32 counters) | masks u8[cap+8]
-//   | dir u32[kNB] (start | count << 16) | samp u16[(cap/64+2)*8]
-__host__ __device__ constexpr size_t tk_keys(uint32_t cap) {
+//   meta 256 B | ent u64[cap+2] (build: kNB u32 counters) | masks u8[cap+8]
+//   | dir u32[kNB] (start | count << 16) | samp u16[(kNG+1)*8]
+// Packed mode (row block max key < 2^56): ent = key << 8 | row mask.
+// Otherwise ent = key and masks[] holds the row mask.
+__host__ __device__ constexpr size_t tk_ent(uint32_t cap) {
   return ((size_t)cap + 2) * 8 > (size_t)kNB * 4 ? ((size_t)cap + 2) * 8 : (size_t)kNB * 4;
 }
 __host__ __device__ constexpr size_t tk_masks(uint32_t cap) { return ((size_t)cap + 8 + 15) & ~(size_t)15; }
 __host__ __device__ constexpr size_t tk_dir() { return (size_t)kNB * 4; }
-__host__ __device__ constexpr size_t tk_samp(uint32_t cap) { return (((size_t)cap / 64 + 2) * 8 * 2 + 15) & ~(size_t)15; }
+__host__ __device__ constexpr size_t tk_samp() { return (((size_t)kNG + 1) * 8 * 2 + 15) & ~(size_t)15; }
 __host__ __device__ constexpr size_t table_lds_bytes(uint32_t cap) {
-  return 256 + tk_keys(cap) + tk_masks(cap) + tk_dir() + tk_samp(cap);
+  return 256 + tk_ent(cap) + tk_masks(cap) + tk_dir() + tk_samp();
 }
 
 struct TableMeta {
@@ -130,20 +133,22 @@ struct TableMeta {
   uint32_t shift_l;
   uint32_t scale;
   uint32_t nrows;
+  uint32_t packed;
 };
 
 __device__ __forceinline__ uint32_t top32(uint64_t b, uint32_t sr, uint32_t sl) {
   return (uint32_t)((b >> sr) << sl);
 }
 
-// Monotone in b: the table is globally sorted by key (bucket order, then
-// sorted inside a bucket), which rank_A relies on.
+// Monotone in b, so bucket order is key order.
 __device__ __forceinline__ uint32_t bucket_of(uint64_t b, uint32_t sr, uint32_t sl, uint32_t scale) {
   return (uint32_t)(((uint64_t)top32(b, sr, sl) * scale) >> 32);
 }
 
-// bytes 0..3 of the result = bits 0..3 of x (x < 16)
-__device__ __forceinline__ uint32_t spread4(uint32_t x) { return (x * 0x204081u) & 0x01010101u; }
+// bytes 0..3 of the result = bits 0..3 of x
+__device__ __forceinline__ uint32_t spread4(uint32_t x) {
+  return ((x & 15u) * 0x204081u) & 0x01010101u;
+}
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -151,60 +156,71 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-template <int R>
-__global__ __launch_bounds__(kTableThreads, 1) void pairs_table_kernel(PairsTableLaunch a) {
-  extern __shared__ __align__(16) uint8_t smem[];
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Per-row byte counters (acc_lo: rows 0-3, acc_hi: rows 4-7) summed over
+// the wave; lane r < 8 receives row r's total.
+__device__ __forceinline__ uint32_t row_totals(uint32_t acc_lo, uint32_t acc_hi, uint32_t lane) {
+  const uint32_t s0 = wave_sum(acc_lo & 0x00FF00FFu);         // rows 0, 2
+  const uint32_t s1 = wave_sum((acc_lo >> 8) & 0x00FF00FFu);  // rows 1, 3
+  const uint32_t s2 = wave_sum(acc_hi & 0x00FF00FFu);         // rows 4, 6
+  const uint32_t s3 = wave_sum((acc_hi >> 8) & 0x00FF00FFu);  // rows 5, 7
+  const uint32_t which = (lane & 1) + 2 * ((lane >> 2) & 1);
+  const uint32_t sv = which == 0 ? s0 : which == 1 ? s1 : which == 2 ? s2 : s3;
+  return (sv >> (16 * ((lane >> 1) & 1))) & 0xFFFFu;
+}
+
+template <bool PACKED>
+__device__ __forceinline__ uint64_t ent_key(const uint64_t* ent, uint32_t i) {
+  return PACKED ? (ent[i] >> 8) : ent[i];
+}
+template <bool PACKED>
+__device__ __forceinline__ uint32_t ent_mask(const uint64_t* ent, const uint8_t* masks, uint32_t i) {
+  return PACKED ? (uint32_t)(ent[i] & 0xFFu) : (uint32_t)masks[i];
+}
+
+// Row mask of column hash bv (0 when absent).  Buckets hold distinct keys
+// in ascending order; entries past a bucket's count are ignored.
+template <bool PACKED>
+__device__ __forceinline__ uint32_t lookup(const uint64_t* __restrict__ ent,
+                                           const uint8_t* __restrict__ masks, uint32_t st,
+                                           uint32_t n, uint64_t bv) {
+  uint32_t m = 0;
+  if (PACKED) {
+    const uint64_t bvs = bv << 8, top = bvs | 0xFFull;
+    for (uint32_t k = 0; k < n; k += 2) {
+      const uint64_t e0 = ent[st + k], e1 = ent[st + k + 1];
+      const uint64_t x0 = e0 ^ bvs, x1 = e1 ^ bvs;
+      if (x0 < 256) m = (uint32_t)x0;
+      if (x1 < 256 && k + 1 < n) m = (uint32_t)x1;
+      if (e1 > top) break;
+    }
+  } else {
+    for (uint32_t k = 0; k < n; k += 2) {
+      const uint64_t k0 = ent[st + k], k1 = ent[st + k + 1];
+      if (k0 == bv) m = masks[st + k];
+      if (k1 == bv && k + 1 < n) m = masks[st + k + 1];
+      if (k1 >= bv) break;
+    }
+  }
+  return m;
+}
+
+template <int R, bool PACKED>
+__device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a, uint8_t* smem,
+                                                       uint32_t row0, uint32_t c0, uint32_t c1) {
   TableMeta& meta = *reinterpret_cast<TableMeta*>(smem);
   const uint32_t cap = (uint32_t)R * a.stride;
-  uint64_t* keys = reinterpret_cast<uint64_t*>(smem + 256);
-  uint8_t* masks = smem + 256 + tk_keys(cap);
-  uint32_t* dir = reinterpret_cast<uint32_t*>(smem + 256 + tk_keys(cap) + tk_masks(cap));
-  uint16_t* samp = reinterpret_cast<uint16_t*>(smem + 256 + tk_keys(cap) + tk_masks(cap) + tk_dir());
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(keys);  // build-time bucket counters
-
-  constexpr uint32_t G = kTile / R;  // row blocks per segment
-  const uint32_t b = blockIdx.x;
-  const uint32_t q = b >> 3;
-  const uint32_t rb = q % G;
-  const uint32_t seg_id = (q / G) * 8 + (b & 7);
-  if (seg_id >= a.n_segs) return;
-  const PairSeg sg = a.segs[seg_id];
-  const uint32_t row0 = sg.I * kTile + rb * R;
-  if (row0 >= a.n) return;
-  const uint32_t c0 = max(sg.J0 * kTile, row0 + 1);
-  const uint32_t c1 = min(sg.J1 * kTile, a.n);
-  if (c0 >= c1) return;
+  uint64_t* ent = reinterpret_cast<uint64_t*>(smem + 256);
+  uint8_t* masks = smem + 256 + tk_ent(cap);
+  uint32_t* dir = reinterpret_cast<uint32_t*>(smem + 256 + tk_ent(cap) + tk_masks(cap));
+  uint16_t* samp = reinterpret_cast<uint16_t*>(smem + 256 + tk_ent(cap) + tk_masks(cap) + tk_dir());
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(ent);  // build-time bucket counters
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-  // ---- row-block metadata
-  if (tid == 0) {
-    const uint32_t nrows = min((uint32_t)R, a.n - row0);
-    uint64_t mx = 0;
-    uint32_t acc = 0;
-    for (int r = 0; r < 8; ++r) {
-      uint32_t l = 0;
-      uint64_t last = 0;
-      if (r < (int)nrows) {
-        l = a.lens[row0 + r];
-        if (l) last = a.sketches[(uint64_t)(row0 + r) * a.stride + l - 1];
-      }
-      meta.len[r] = l;
-      meta.last[r] = last;
-      meta.pre[r] = acc;
-      acc += l;
-      if (l && last > mx) mx = last;
-    }
-    meta.pre[8] = acc;
-    meta.maxkey = mx;
-    const uint32_t L = mx ? 64 - __builtin_clzll(mx) : 1;
-    meta.shift_r = L > 32 ? L - 32 : 0;
-    meta.shift_l = L > 32 ? 0 : 32 - L;
-    const uint64_t t = (uint64_t)top32(mx, meta.shift_r, meta.shift_l) + 1;  // in (2^31, 2^32]
-    meta.scale = (uint32_t)(((uint64_t)kNB << 32) / t);
-    meta.nrows = nrows;
-  }
-  for (uint32_t i = tid; i < kNB; i += kTableThreads) cnt[i] = 0;
-  __syncthreads();
   const uint32_t E = meta.pre[8];
   const uint32_t sr = meta.shift_r, sl = meta.shift_l, scale = meta.scale;
 
@@ -252,7 +268,7 @@ __global__ __launch_bounds__(kTableThreads, 1) void pairs_table_kernel(PairsTabl
     }
   }
   __syncthreads();
-  // ---- build pass 2: scatter keys and row bits
+  // ---- build pass 2: scatter
 #pragma unroll
   for (uint32_t t = 0; t < kEPT; ++t) {
     const uint32_t e = tid + t * kTableThreads;
@@ -262,51 +278,68 @@ __global__ __launch_bounds__(kTableThreads, 1) void pairs_table_kernel(PairsTabl
       for (int x = 1; x < R; ++x) r += (e >= meta.pre[x]) ? 1u : 0u;
       const uint64_t key = a.sketches[(uint64_t)(row0 + r) * a.stride + (e - meta.pre[r])];
       const uint32_t slot = (dir[bucket_of(key, sr, sl, scale)] & 0xFFFFu) + pos[t];
-      keys[slot] = key;
-      masks[slot] = (uint8_t)(1u << r);
+      if (PACKED) {
+        ent[slot] = (key << 8) | (1ull << r);
+      } else {
+        ent[slot] = key;
+        masks[slot] = (uint8_t)(1u << r);
+      }
     }
   }
   if (tid < 2) {
-    keys[E + tid] = ~0ull;  // pads for paired reads past a bucket's end
+    ent[E + tid] = ~0ull;  // pads for paired reads past the last bucket
     masks[E + tid] = 0;
   }
   __syncthreads();
-  // ---- sort each bucket (insertion sort; buckets hold ~E/kNB entries)
+  // ---- per bucket: insertion sort, merge equal keys (OR the row masks)
   for (uint32_t bk = tid; bk < kNB; bk += kTableThreads) {
     const uint32_t d = dir[bk];
     const uint32_t s0 = d & 0xFFFFu, s1 = s0 + (d >> 16);
     for (uint32_t i = s0 + 1; i < s1; ++i) {
-      const uint64_t k = keys[i];
-      const uint8_t m = masks[i];
+      const uint64_t k = ent[i];
+      const uint8_t m = PACKED ? 0 : masks[i];
       uint32_t j = i;
-      while (j > s0 && keys[j - 1] > k) {
-        keys[j] = keys[j - 1];
-        masks[j] = masks[j - 1];
+      while (j > s0 && ent[j - 1] > k) {
+        ent[j] = ent[j - 1];
+        if (!PACKED) masks[j] = masks[j - 1];
         --j;
       }
-      keys[j] = k;
-      masks[j] = m;
+      ent[j] = k;
+      if (!PACKED) masks[j] = m;
     }
+    uint32_t w = s0;
+    for (uint32_t i = s0; i < s1; ++i) {
+      if (i > s0 && ent_key<PACKED>(ent, i) == ent_key<PACKED>(ent, w - 1)) {
+        if (PACKED) ent[w - 1] |= ent[i] & 0xFFull;
+        else masks[w - 1] |= masks[i];
+      } else {
+        ent[w] = ent[i];
+        if (!PACKED) masks[w] = masks[i];
+        ++w;
+      }
+    }
+    dir[bk] = s0 | ((w - s0) << 16);
   }
   __syncthreads();
-  // ---- per-row prefix counts every 64 entries (rank_A support)
-  const uint32_t nblk = (E + 63) / 64;
-  for (uint32_t blk = wave; blk < nblk; blk += kTableWaves) {
-    const uint32_t e = blk * 64 + lane;
-    const uint32_t m = e < E ? masks[e] : 0u;
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const uint32_t c = __popcll(__ballot((m >> r) & 1u));
-      if (lane == (uint32_t)r) samp[(blk + 1) * 8 + r] = (uint16_t)c;
+  // ---- rank_A support: per-row entry counts before each 64-bucket group
+  for (uint32_t g = wave; g < kNG; g += kTableWaves) {
+    const uint32_t d = dir[g * 64 + lane];
+    uint32_t lo = 0, hi = 0;
+    for (uint32_t k = 0; k < (d >> 16); ++k) {
+      const uint32_t m = ent_mask<PACKED>(ent, masks, (d & 0xFFFFu) + k);
+      lo += spread4(m);
+      hi += spread4(m >> 4);
     }
+    const uint32_t c = row_totals(lo, hi, lane);
+    if (lane < 8) samp[(g + 1) * 8 + lane] = (uint16_t)c;
   }
   __syncthreads();
   if (tid < 8) {
     uint32_t run = 0;
     samp[tid] = 0;
-    for (uint32_t blk = 1; blk <= nblk; ++blk) {
-      run += samp[blk * 8 + tid];
-      samp[blk * 8 + tid] = (uint16_t)run;
+    for (uint32_t g = 1; g <= kNG; ++g) {
+      run += samp[g * 8 + tid];
+      samp[g * 8 + tid] = (uint16_t)run;
     }
   }
   __syncthreads();
@@ -326,7 +359,7 @@ __global__ __launch_bounds__(kTableThreads, 1) void pairs_table_kernel(PairsTabl
     const uint64_t* B = a.sketches + (uint64_t)j * a.stride;
     const uint64_t lastB = lb ? B[lb - 1] : 0;
     uint32_t acc_lo = 0, acc_hi = 0;
-    uint32_t cntB[R];
+    uint32_t cntB[R];  // rank_B(last A_r), wave-uniform
 #pragma unroll
     for (int r = 0; r < R; ++r) cntB[r] = 0;
     for (uint32_t cb = 0; cb < lb; cb += kChunk * 64) {
@@ -338,58 +371,48 @@ __global__ __launch_bounds__(kTableThreads, 1) void pairs_table_kernel(PairsTabl
       }
 #pragma unroll
       for (int t = 0; t < kChunk; ++t) {
-        if (cb + t * 64 >= lb) break;
+        const uint32_t rb0 = cb + t * 64;
+        if (rb0 >= lb) continue;  // wave-uniform; keeps the loop unrollable
         const uint64_t bv = v[t];
-        const bool valid = cb + t * 64 + lane < lb;
+        const bool valid = rb0 + lane < lb;
         uint32_t m = 0;
         if (valid && bv <= maxkey) {
           const uint32_t d = dir[bucket_of(bv, sr, sl, scale)];
-          const uint32_t st = d & 0xFFFFu, n = d >> 16;
-          for (uint32_t k = 0; k < n; k += 2) {
-            const uint64_t k0 = keys[st + k], k1 = keys[st + k + 1];
-            if (k0 == bv) m |= masks[st + k];
-            if (k1 == bv && k + 1 < n) m |= masks[st + k + 1];
-            if (k1 > bv) break;
-          }
+          m = lookup<PACKED>(ent, masks, d & 0xFFFFu, d >> 16, bv);
         }
-        acc_lo += spread4(m & 15u);
+        acc_lo += spread4(m);
         if (R > 4) acc_hi += spread4(m >> 4);
+        // rank_B: this round's values are ascending across lanes
+        const uint32_t nvalid = min(64u, lb - rb0);
+        const uint64_t vfirst = readlane64(bv, 0);
+        const uint64_t vlast = readlane64(bv, (int)nvalid - 1);
 #pragma unroll
-        for (int r = 0; r < R; ++r) cntB[r] += __popcll(__ballot(valid && bv <= xr[r]));
-      }
-    }
-    // per-row common counts
-    const uint32_t s0 = wave_sum(acc_lo & 0x00FF00FFu);
-    const uint32_t s1 = wave_sum((acc_lo >> 8) & 0x00FF00FFu);
-    uint32_t s2 = 0, s3 = 0;
-    if (R > 4) {
-      s2 = wave_sum(acc_hi & 0x00FF00FFu);
-      s3 = wave_sum((acc_hi >> 8) & 0x00FF00FFu);
-    }
-    // rank_A(last B) for every row from the sorted table: entries [0, p)
-    // are the keys <= last B
-    uint32_t rank_lane = 0;  // lane r < 8: #entries of row r with key <= last B
-    if (lb) {
-      uint32_t p;
-      if (lastB >= maxkey) {
-        p = E;
-      } else {
-        const uint32_t d = dir[bucket_of(lastB, sr, sl, scale)];
-        const uint32_t st = d & 0xFFFFu, n = d >> 16;
-        p = st;
-        for (uint32_t k0 = 0; k0 < n; k0 += 64) {
-          const uint32_t k = k0 + lane;
-          p += __popcll(__ballot(k < n && keys[st + k] <= lastB));
+        for (int r = 0; r < R; ++r) {
+          if (xr[r] >= vlast) cntB[r] += nvalid;
+          else if (xr[r] >= vfirst) cntB[r] += __popcll(__ballot(valid && bv <= xr[r]));
         }
       }
-      const uint32_t blk = p >> 6;
-      const uint32_t e = (blk << 6) + lane;
-      const uint32_t mm = e < p ? masks[e] : 0u;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) {
-        const uint32_t c = __popcll(__ballot((mm >> r) & 1u));
-        if (lane == (uint32_t)r) rank_lane = samp[blk * 8 + r] + c;
+    }
+    const uint32_t common_lane = row_totals(acc_lo, acc_hi, lane);
+    // rank_A(last B): entries of row r with key <= last B, from the sorted
+    // buckets; needed only when last B < last A_r <= maxkey
+    uint32_t rank_lane = 0;
+    if (lb && lastB < maxkey) {
+      const uint32_t bk = bucket_of(lastB, sr, sl, scale);
+      const uint32_t g = bk >> 6;
+      const uint32_t bl = g * 64 + lane;
+      uint32_t lo = 0, hi = 0;
+      if (bl <= bk) {
+        const uint32_t d = dir[bl];
+        const uint32_t st = d & 0xFFFFu, n = d >> 16;
+        for (uint32_t k = 0; k < n; ++k) {
+          if (bl == bk && ent_key<PACKED>(ent, st + k) > lastB) break;
+          const uint32_t m = ent_mask<PACKED>(ent, masks, st + k);
+          lo += spread4(m);
+          hi += spread4(m >> 4);
+        }
       }
+      rank_lane = row_totals(lo, hi, lane) + (lane < 8 ? samp[g * 8 + lane] : 0u);
     }
     // lane r < R evaluates pair (row0 + r, j)
     uint32_t cb = 0, la = 0;
@@ -402,9 +425,7 @@ __global__ __launch_bounds__(kTableThreads, 1) void pairs_table_kernel(PairsTabl
         x = xr[r];
       }
     }
-    const uint32_t which = (lane & 1) + 2 * ((lane >> 2) & 1);
-    const uint32_t sv = which == 0 ? s0 : which == 1 ? s1 : which == 2 ? s2 : s3;
-    uint32_t common = (sv >> (16 * ((lane >> 1) & 1))) & 0xFFFFu;
+    uint32_t common = common_lane;
     uint32_t total;
     if (la == 0 || lb == 0) {
       common = 0;
@@ -428,6 +449,59 @@ __global__ __launch_bounds__(kTableThreads, 1) void pairs_table_kernel(PairsTabl
       }
     }
   }
+}
+
+template <int R>
+__global__ __launch_bounds__(kTableThreads, 1) void pairs_table_kernel(PairsTableLaunch a) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  TableMeta& meta = *reinterpret_cast<TableMeta*>(smem);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + 256);
+
+  constexpr uint32_t G = kTile / R;  // row blocks per segment
+  const uint32_t b = blockIdx.x;
+  const uint32_t q = b >> 3;
+  const uint32_t rb = q % G;
+  const uint32_t seg_id = (q / G) * 8 + (b & 7);
+  if (seg_id >= a.n_segs) return;
+  const PairSeg sg = a.segs[seg_id];
+  const uint32_t row0 = sg.I * kTile + rb * R;
+  if (row0 >= a.n) return;
+  const uint32_t c0 = max(sg.J0 * kTile, row0 + 1);
+  const uint32_t c1 = min(sg.J1 * kTile, a.n);
+  if (c0 >= c1) return;
+  const uint32_t tid = threadIdx.x;
+
+  if (tid == 0) {
+    const uint32_t nrows = min((uint32_t)R, a.n - row0);
+    uint64_t mx = 0;
+    uint32_t acc = 0;
+    for (int r = 0; r < 8; ++r) {
+      uint32_t l = 0;
+      uint64_t last = 0;
+      if (r < (int)nrows) {
+        l = a.lens[row0 + r];
+        if (l) last = a.sketches[(uint64_t)(row0 + r) * a.stride + l - 1];
+      }
+      meta.len[r] = l;
+      meta.last[r] = last;
+      meta.pre[r] = acc;
+      acc += l;
+      if (l && last > mx) mx = last;
+    }
+    meta.pre[8] = acc;
+    meta.maxkey = mx;
+    const uint32_t L = mx ? 64 - __builtin_clzll(mx) : 1;
+    meta.shift_r = L > 32 ? L - 32 : 0;
+    meta.shift_l = L > 32 ? 0 : 32 - L;
+    const uint64_t t = (uint64_t)top32(mx, meta.shift_r, meta.shift_l) + 1;  // in (2^31, 2^32]
+    meta.scale = (uint32_t)(((uint64_t)kNB << 32) / t);
+    meta.nrows = nrows;
+    meta.packed = (mx >> 56) == 0;
+  }
+  for (uint32_t i = tid; i < kNB; i += kTableThreads) cnt[i] = 0;
+  __syncthreads();
+  if (meta.packed) table_build_and_stream<R, true>(a, smem, row0, c0, c1);
+  else table_build_and_stream<R, false>(a, smem, row0, c0, c1);
 }
 
 template <int R>
