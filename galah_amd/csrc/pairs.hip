@@ -174,6 +174,26 @@ __device__ __forceinline__ uint32_t row_totals(uint32_t acc_lo, uint32_t acc_hi,
   return (sv >> (16 * ((lane >> 1) & 1))) & 0xFFFFu;
 }
 
+// Per-row 16-bit counters for walks over whole buckets (a bucket can hold
+// more than 255 entries): c[0] rows 0|2, c[1] rows 1|3, c[2] rows 4|6,
+// c[3] rows 5|7, row in the low / high half.
+struct RowCount16 {
+  uint32_t c[4] = {0, 0, 0, 0};
+  __device__ __forceinline__ void add(uint32_t m) {
+    c[0] += (m & 1u) | ((m & 4u) << 14);
+    c[1] += ((m >> 1) & 1u) | ((m & 8u) << 13);
+    c[2] += ((m >> 4) & 1u) | ((m & 64u) << 10);
+    c[3] += ((m >> 5) & 1u) | ((m & 128u) << 9);
+  }
+  // lane r < 8 receives row r's wave total
+  __device__ __forceinline__ uint32_t totals(uint32_t lane) const {
+    const uint32_t s0 = wave_sum(c[0]), s1 = wave_sum(c[1]), s2 = wave_sum(c[2]), s3 = wave_sum(c[3]);
+    const uint32_t which = (lane & 1) + 2 * ((lane >> 2) & 1);
+    const uint32_t sv = which == 0 ? s0 : which == 1 ? s1 : which == 2 ? s2 : s3;
+    return (sv >> (16 * ((lane >> 1) & 1))) & 0xFFFFu;
+  }
+};
+
 template <bool PACKED>
 __device__ __forceinline__ uint64_t ent_key(const uint64_t* ent, uint32_t i) {
   return PACKED ? (ent[i] >> 8) : ent[i];
@@ -324,13 +344,9 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
   // ---- rank_A support: per-row entry counts before each 64-bucket group
   for (uint32_t g = wave; g < kNG; g += kTableWaves) {
     const uint32_t d = dir[g * 64 + lane];
-    uint32_t lo = 0, hi = 0;
-    for (uint32_t k = 0; k < (d >> 16); ++k) {
-      const uint32_t m = ent_mask<PACKED>(ent, masks, (d & 0xFFFFu) + k);
-      lo += spread4(m);
-      hi += spread4(m >> 4);
-    }
-    const uint32_t c = row_totals(lo, hi, lane);
+    RowCount16 rc;
+    for (uint32_t k = 0; k < (d >> 16); ++k) rc.add(ent_mask<PACKED>(ent, masks, (d & 0xFFFFu) + k));
+    const uint32_t c = rc.totals(lane);
     if (lane < 8) samp[(g + 1) * 8 + lane] = (uint16_t)c;
   }
   __syncthreads();
@@ -401,18 +417,16 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
       const uint32_t bk = bucket_of(lastB, sr, sl, scale);
       const uint32_t g = bk >> 6;
       const uint32_t bl = g * 64 + lane;
-      uint32_t lo = 0, hi = 0;
+      RowCount16 rc;
       if (bl <= bk) {
         const uint32_t d = dir[bl];
         const uint32_t st = d & 0xFFFFu, n = d >> 16;
         for (uint32_t k = 0; k < n; ++k) {
           if (bl == bk && ent_key<PACKED>(ent, st + k) > lastB) break;
-          const uint32_t m = ent_mask<PACKED>(ent, masks, st + k);
-          lo += spread4(m);
-          hi += spread4(m >> 4);
+          rc.add(ent_mask<PACKED>(ent, masks, st + k));
         }
       }
-      rank_lane = row_totals(lo, hi, lane) + (lane < 8 ? samp[g * 8 + lane] : 0u);
+      rank_lane = rc.totals(lane) + (lane < 8 ? samp[g * 8 + lane] : 0u);
     }
     // lane r < R evaluates pair (row0 + r, j)
     uint32_t cb = 0, la = 0;

@@ -27,6 +27,14 @@ for st in $STAGES; do
       run bench_1k 300 python -u bench.py --genomes 1000 --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
     bench)
       run bench 600 python -u bench.py --steps 3 --warmup 1 || exit $? ;;
+    k2)
+      run k2_probe 300 python -u scripts/k2_probe.py || exit $? ;;
+    pmc_k2)
+      run pmc_k2 900 bash scripts/pmc.sh gpurun_out/pmc_k2 pairs_table -- python3 -u scripts/k2_probe.py --reps 1 || exit $? ;;
+    pmc_k1)
+      run pmc_k1 900 bash scripts/pmc.sh gpurun_out/pmc_k1 sketch_candidates -- python3 -u scripts/k2_probe.py --reps 1 || exit $? ;;
+    counters)
+      run counters 120 rocprofv3 -L || exit $? ;;
     prof)
       run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
   esac
