@@ -103,7 +103,7 @@ __global__ __launch_bounds__(kBlock) void pairs_merge_kernel(PairsLaunch a) {
 // ---------------------------------------------------------------------------
 constexpr int kTableThreads = 1024;
 constexpr int kTableWaves = kTableThreads / 64;
-constexpr uint32_t kNB = 4096;  // buckets
+constexpr uint32_t kNB = 8192;  // buckets
 constexpr uint32_t kNG = kNB / 64;  // bucket groups (rank_A prefix samples)
 constexpr uint32_t kKeyCap = 8192;
 constexpr uint32_t kEPT = kKeyCap / kTableThreads;  // entries per thread in the build
@@ -156,11 +156,43 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return v;
 }
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, l);
-  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-  return ((uint64_t)hi << 32) | lo;
+__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
 }
+
+// Lane r < R receives #{ e < lb : B[e] <= x_r } (B ascending, lb > 0).
+// Level 1: 64 samples shared by all rows; level 2: 64/R lanes per row scan
+// the remaining window.  x[] and B are wave-uniform.
+template <int R>
+__device__ __forceinline__ uint32_t rank_rows_B(const uint64_t* __restrict__ B, uint32_t lb,
+                                               const uint64_t* __restrict__ meta_last,
+                                               const uint64_t (&x)[R], uint32_t lane) {
+  const uint32_t step = (lb + 63) / 64;
+  const uint32_t e = (lane + 1) * step - 1;  // sample index; past the end for some lanes
+  const bool ok = e < lb;
+  const uint64_t sv = ok ? B[e] : 0;
+  uint32_t cvec = 0;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t c = __popcll(__ballot(ok && sv <= x[r]));
+    if (lane == (uint32_t)r) cvec = c;
+  }
+  constexpr uint32_t LPR = 64 / R;  // lanes per row
+  const uint32_t my_row = lane / LPR, sub = lane % LPR;
+  const uint32_t c_my = __shfl(cvec, my_row);
+  const uint64_t x_my = meta_last[my_row];
+  const uint32_t w0 = c_my * step;
+  const uint32_t w1 = min(lb, w0 + step - 1);
+  uint32_t cnt = 0;
+  for (uint32_t i = w0 + sub; i < w1; i += LPR) cnt += (B[i] <= x_my) ? 1u : 0u;
+#pragma unroll
+  for (uint32_t o = LPR / 2; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  // lane r (r < R) reads the group total of row r (group leader lane r*LPR)
+  const uint32_t tot = w0 + cnt;
+  return __shfl(tot, (lane % R) * LPR);
+}
+
 
 // Per-row byte counters (acc_lo: rows 0-3, acc_hi: rows 4-7) summed over
 // the wave; lane r < 8 receives row r's total.
@@ -361,23 +393,20 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
   __syncthreads();
 
   // ---- stream columns
-  const uint64_t maxkey = meta.maxkey;
-  const uint32_t nrows = meta.nrows;
+  const uint64_t maxkey = uni64(meta.maxkey);
+  const uint32_t nrows = uni32(meta.nrows);
   uint64_t xr[R];
   uint32_t lr[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    xr[r] = meta.last[r];
-    lr[r] = meta.len[r];
+    xr[r] = uni64(meta.last[r]);
+    lr[r] = uni32(meta.len[r]);
   }
   for (uint32_t j = c0 + wave; j < c1; j += kTableWaves) {
-    const uint32_t lb = a.lens[j];
+    const uint32_t lb = uni32(a.lens[j]);
     const uint64_t* B = a.sketches + (uint64_t)j * a.stride;
-    const uint64_t lastB = lb ? B[lb - 1] : 0;
+    const uint64_t lastB = lb ? uni64(B[lb - 1]) : 0;
     uint32_t acc_lo = 0, acc_hi = 0;
-    uint32_t cntB[R];  // rank_B(last A_r), wave-uniform
-#pragma unroll
-    for (int r = 0; r < R; ++r) cntB[r] = 0;
     for (uint32_t cb = 0; cb < lb; cb += kChunk * 64) {
       uint64_t v[kChunk];
 #pragma unroll
@@ -390,23 +419,13 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
         const uint32_t rb0 = cb + t * 64;
         if (rb0 >= lb) continue;  // wave-uniform; keeps the loop unrollable
         const uint64_t bv = v[t];
-        const bool valid = rb0 + lane < lb;
         uint32_t m = 0;
-        if (valid && bv <= maxkey) {
+        if (rb0 + lane < lb && bv <= maxkey) {
           const uint32_t d = dir[bucket_of(bv, sr, sl, scale)];
           m = lookup<PACKED>(ent, masks, d & 0xFFFFu, d >> 16, bv);
         }
         acc_lo += spread4(m);
         if (R > 4) acc_hi += spread4(m >> 4);
-        // rank_B: this round's values are ascending across lanes
-        const uint32_t nvalid = min(64u, lb - rb0);
-        const uint64_t vfirst = readlane64(bv, 0);
-        const uint64_t vlast = readlane64(bv, (int)nvalid - 1);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if (xr[r] >= vlast) cntB[r] += nvalid;
-          else if (xr[r] >= vfirst) cntB[r] += __popcll(__ballot(valid && bv <= xr[r]));
-        }
       }
     }
     const uint32_t common_lane = row_totals(acc_lo, acc_hi, lane);
@@ -428,13 +447,14 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
       }
       rank_lane = rc.totals(lane) + (lane < 8 ? samp[g * 8 + lane] : 0u);
     }
+    // rank_B(last A_r) for the rows with last A_r <= last B
+    const uint32_t cb = lb ? rank_rows_B<R>(B, lb, meta.last, xr, lane) : 0u;
     // lane r < R evaluates pair (row0 + r, j)
-    uint32_t cb = 0, la = 0;
+    uint32_t la = 0;
     uint64_t x = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       if (lane == (uint32_t)r) {
-        cb = cntB[r];
         la = lr[r];
         x = xr[r];
       }
