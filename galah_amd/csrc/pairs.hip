@@ -120,8 +120,10 @@ __host__ __device__ constexpr size_t tk_ent(uint32_t cap) {
 __host__ __device__ constexpr size_t tk_masks(uint32_t cap) { return ((size_t)cap + 8 + 15) & ~(size_t)15; }
 __host__ __device__ constexpr size_t tk_dir() { return (size_t)kNB * 4; }
 __host__ __device__ constexpr size_t tk_samp() { return (((size_t)kNG + 1) * 8 * 2 + 15) & ~(size_t)15; }
+constexpr uint32_t kRing = 128;  // per-wave ring of column hashes needing a full bucket walk
+__host__ __device__ constexpr size_t tk_ring() { return (size_t)kTableWaves * kRing * 8; }
 __host__ __device__ constexpr size_t table_lds_bytes(uint32_t cap) {
-  return 256 + tk_ent(cap) + tk_masks(cap) + tk_dir() + tk_samp();
+  return 256 + tk_ent(cap) + tk_masks(cap) + tk_dir() + tk_samp() + tk_ring();
 }
 
 struct TableMeta {
@@ -233,6 +235,29 @@ __device__ __forceinline__ uint64_t ent_key(const uint64_t* ent, uint32_t i) {
 template <bool PACKED>
 __device__ __forceinline__ uint32_t ent_mask(const uint64_t* ent, const uint8_t* masks, uint32_t i) {
   return PACKED ? (uint32_t)(ent[i] & 0xFFu) : (uint32_t)masks[i];
+}
+
+// First-probe lookup: examines the first two entries of the bucket only.
+// Returns the row mask when the key is among them; sets `more` when the
+// key may sit further in the bucket (count > 2 and both entries smaller).
+template <bool PACKED>
+__device__ __forceinline__ uint32_t lookup2(const uint64_t* __restrict__ ent,
+                                            const uint8_t* __restrict__ masks, uint32_t st,
+                                            uint32_t n, uint64_t bv, bool& more) {
+  const uint64_t e0 = ent[st], e1 = ent[st + 1];
+  uint32_t m = 0;
+  if (PACKED) {
+    const uint64_t bvs = bv << 8;
+    const uint64_t x0 = e0 ^ bvs, x1 = e1 ^ bvs;
+    if (n > 1 && x1 < 256) m = (uint32_t)x1;
+    if (n > 0 && x0 < 256) m = (uint32_t)x0;
+    more = (n > 2) && (e1 < bvs);
+  } else {
+    if (n > 1 && e1 == bv) m = masks[st + 1];
+    if (n > 0 && e0 == bv) m = masks[st];
+    more = (n > 2) && (e1 < bv);
+  }
+  return m;
 }
 
 // Row mask of column hash bv (0 when absent).  Buckets hold distinct keys
@@ -402,11 +427,26 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
     xr[r] = uni64(meta.last[r]);
     lr[r] = uni32(meta.len[r]);
   }
+  uint64_t* ring = reinterpret_cast<uint64_t*>(smem + 256 + tk_ent(cap) + tk_masks(cap) + tk_dir() + tk_samp()) +
+                   wave * kRing;
   for (uint32_t j = c0 + wave; j < c1; j += kTableWaves) {
     const uint32_t lb = uni32(a.lens[j]);
     const uint64_t* B = a.sketches + (uint64_t)j * a.stride;
     const uint64_t lastB = lb ? uni64(B[lb - 1]) : 0;
     uint32_t acc_lo = 0, acc_hi = 0;
+    uint32_t head = 0, tail = 0;  // ring indices (wave-uniform)
+    // full bucket walks for up to 64 queued hashes
+    auto drain = [&](uint32_t count) {
+      uint32_t m = 0;
+      if (lane < count) {
+        const uint64_t bv = ring[(head + lane) & (kRing - 1)];
+        const uint32_t d = dir[bucket_of(bv, sr, sl, scale)];
+        m = lookup<PACKED>(ent, masks, d & 0xFFFFu, d >> 16, bv);
+      }
+      acc_lo += spread4(m);
+      if (R > 4) acc_hi += spread4(m >> 4);
+      head += count;
+    };
     for (uint32_t cb = 0; cb < lb; cb += kChunk * 64) {
       uint64_t v[kChunk];
 #pragma unroll
@@ -420,14 +460,22 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
         if (rb0 >= lb) continue;  // wave-uniform; keeps the loop unrollable
         const uint64_t bv = v[t];
         uint32_t m = 0;
+        bool more = false;
         if (rb0 + lane < lb && bv <= maxkey) {
           const uint32_t d = dir[bucket_of(bv, sr, sl, scale)];
-          m = lookup<PACKED>(ent, masks, d & 0xFFFFu, d >> 16, bv);
+          m = lookup2<PACKED>(ent, masks, d & 0xFFFFu, d >> 16, bv, more);
         }
         acc_lo += spread4(m);
         if (R > 4) acc_hi += spread4(m >> 4);
+        const unsigned long long mm = __ballot(more);
+        if (mm) {
+          if (more) ring[(tail + __popcll(mm & ((1ull << lane) - 1ull))) & (kRing - 1)] = bv;
+          tail += __popcll(mm);
+          if (tail - head >= 64) drain(64);
+        }
       }
     }
+    while (tail != head) drain(min(64u, tail - head));
     const uint32_t common_lane = row_totals(acc_lo, acc_hi, lane);
     // rank_A(last B): entries of row r with key <= last B, from the sorted
     // buckets; needed only when last B < last A_r <= maxkey
