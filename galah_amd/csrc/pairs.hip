@@ -108,6 +108,7 @@ constexpr uint32_t kNG = kNB / 64;  // bucket groups (rank_A prefix samples)
 constexpr uint32_t kKeyCap = 8192;
 constexpr uint32_t kEPT = kKeyCap / kTableThreads;  // entries per thread in the build
 constexpr int kChunk = 16;                          // column rounds held in registers
+constexpr int kGroup = 8;                           // rounds whose LDS probes are issued together
 
 // LDS layout (dynamic, base 16-B aligned):
 //   meta 256 B | ent u64[cap+2] (build: kNB u32 counters) | masks u8[cap+8]
@@ -302,18 +303,23 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
   const uint32_t sr = meta.shift_r, sl = meta.shift_l, scale = meta.scale;
 
   // ---- build pass 1: bucket counts, each entry's rank inside its bucket
+  // (all kEPT loads issued before the first use)
+  uint64_t bkey[kEPT];
+  uint32_t brow[kEPT];
+#pragma unroll
+  for (uint32_t t = 0; t < kEPT; ++t) {
+    const uint32_t e = min(tid + t * kTableThreads, E ? E - 1 : 0u);
+    uint32_t r = 0;
+#pragma unroll
+    for (int x = 1; x < R; ++x) r += (e >= meta.pre[x]) ? 1u : 0u;
+    brow[t] = r;
+    bkey[t] = E ? a.sketches[(uint64_t)(row0 + r) * a.stride + (e - meta.pre[r])] : 0ull;
+  }
   uint32_t pos[kEPT];
 #pragma unroll
   for (uint32_t t = 0; t < kEPT; ++t) {
-    const uint32_t e = tid + t * kTableThreads;
     pos[t] = 0;
-    if (e < E) {
-      uint32_t r = 0;
-#pragma unroll
-      for (int x = 1; x < R; ++x) r += (e >= meta.pre[x]) ? 1u : 0u;
-      const uint64_t key = a.sketches[(uint64_t)(row0 + r) * a.stride + (e - meta.pre[r])];
-      pos[t] = atomicAdd(&cnt[bucket_of(key, sr, sl, scale)], 1u);
-    }
+    if (tid + t * kTableThreads < E) pos[t] = atomicAdd(&cnt[bucket_of(bkey[t], sr, sl, scale)], 1u);
   }
   __syncthreads();
   // exclusive scan of the kNB counters -> dir = start | count << 16
@@ -348,18 +354,14 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
   // ---- build pass 2: scatter
 #pragma unroll
   for (uint32_t t = 0; t < kEPT; ++t) {
-    const uint32_t e = tid + t * kTableThreads;
-    if (e < E) {
-      uint32_t r = 0;
-#pragma unroll
-      for (int x = 1; x < R; ++x) r += (e >= meta.pre[x]) ? 1u : 0u;
-      const uint64_t key = a.sketches[(uint64_t)(row0 + r) * a.stride + (e - meta.pre[r])];
+    if (tid + t * kTableThreads < E) {
+      const uint64_t key = bkey[t];
       const uint32_t slot = (dir[bucket_of(key, sr, sl, scale)] & 0xFFFFu) + pos[t];
       if (PACKED) {
-        ent[slot] = (key << 8) | (1ull << r);
+        ent[slot] = (key << 8) | (1ull << brow[t]);
       } else {
         ent[slot] = key;
-        masks[slot] = (uint8_t)(1u << r);
+        masks[slot] = (uint8_t)(1u << brow[t]);
       }
     }
   }
@@ -441,7 +443,7 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
       if (lane < count) {
         const uint64_t bv = ring[(head + lane) & (kRing - 1)];
         const uint32_t d = dir[bucket_of(bv, sr, sl, scale)];
-        m = lookup<PACKED>(ent, masks, d & 0xFFFFu, d >> 16, bv);
+        m = lookup<PACKED>(ent, masks, (d & 0xFFFFu) + 2, (d >> 16) - 2, bv);
       }
       acc_lo += spread4(m);
       if (R > 4) acc_hi += spread4(m >> 4);
@@ -454,24 +456,64 @@ __device__ __forceinline__ void table_build_and_stream(const PairsTableLaunch& a
         const uint32_t e = cb + t * 64 + lane;
         v[t] = e < lb ? B[e] : ~0ull;
       }
+      // groups of kGroup rounds: all directory reads, then all entry
+      // reads, then the compares -- branch-free so the LDS latencies of
+      // the group overlap; lanes past the column end or above maxkey probe
+      // bucket 0 and are masked out.
 #pragma unroll
-      for (int t = 0; t < kChunk; ++t) {
-        const uint32_t rb0 = cb + t * 64;
-        if (rb0 >= lb) continue;  // wave-uniform; keeps the loop unrollable
-        const uint64_t bv = v[t];
-        uint32_t m = 0;
-        bool more = false;
-        if (rb0 + lane < lb && bv <= maxkey) {
-          const uint32_t d = dir[bucket_of(bv, sr, sl, scale)];
-          m = lookup2<PACKED>(ent, masks, d & 0xFFFFu, d >> 16, bv, more);
+      for (int g0 = 0; g0 < kChunk; g0 += kGroup) {
+        if (cb + g0 * 64 >= lb) continue;  // wave-uniform
+        uint32_t d[kGroup];
+        bool ok[kGroup];
+#pragma unroll
+        for (int t = 0; t < kGroup; ++t) {
+          const uint64_t bv = v[g0 + t];
+          ok[t] = (cb + (g0 + t) * 64 + lane < lb) && (bv <= maxkey);
+          const uint32_t bk = ok[t] ? bucket_of(bv, sr, sl, scale) : 0u;
+          d[t] = dir[bk];
         }
-        acc_lo += spread4(m);
-        if (R > 4) acc_hi += spread4(m >> 4);
-        const unsigned long long mm = __ballot(more);
-        if (mm) {
-          if (more) ring[(tail + __popcll(mm & ((1ull << lane) - 1ull))) & (kRing - 1)] = bv;
-          tail += __popcll(mm);
-          if (tail - head >= 64) drain(64);
+        uint64_t e0[kGroup], e1[kGroup];
+#pragma unroll
+        for (int t = 0; t < kGroup; ++t) {
+          const uint32_t st = d[t] & 0xFFFFu;
+          e0[t] = ent[st];
+          e1[t] = ent[st + 1];
+        }
+        uint32_t more_bits = 0;
+#pragma unroll
+        for (int t = 0; t < kGroup; ++t) {
+          const uint64_t bv = v[g0 + t];
+          const uint32_t n = d[t] >> 16;
+          uint32_t m = 0;
+          bool more;
+          if (PACKED) {
+            const uint64_t bvs = bv << 8;
+            const uint64_t x0 = e0[t] ^ bvs, x1 = e1[t] ^ bvs;
+            m = (n > 1 && x1 < 256) ? (uint32_t)x1 : 0u;
+            m = (n > 0 && x0 < 256) ? (uint32_t)x0 : m;
+            more = (n > 2) && (e1[t] < bvs);
+          } else {
+            const uint32_t st = d[t] & 0xFFFFu;
+            const uint32_t m0 = masks[st], m1 = masks[st + 1];
+            m = (n > 1 && e1[t] == bv) ? m1 : 0u;
+            m = (n > 0 && e0[t] == bv) ? m0 : m;
+            more = (n > 2) && (e1[t] < bv);
+          }
+          m = ok[t] ? m : 0u;
+          more_bits |= (ok[t] && more) ? (1u << t) : 0u;
+          acc_lo += spread4(m);
+          if (R > 4) acc_hi += spread4(m >> 4);
+        }
+        // queue the lanes whose key may sit past the first two entries
+#pragma unroll
+        for (int t = 0; t < kGroup; ++t) {
+          const bool more = (more_bits >> t) & 1u;
+          const unsigned long long mm = __ballot(more);
+          if (mm) {
+            if (more) ring[(tail + __popcll(mm & ((1ull << lane) - 1ull))) & (kRing - 1)] = v[g0 + t];
+            tail += __popcll(mm);
+            if (tail - head >= 64) drain(64);
+          }
         }
       }
     }
