@@ -15,7 +15,8 @@
 //       fl = LSB-first code (byte p of the hash input = base p)
 //     The reverse complement needs no separate state:
 //       rc MSB-first = ~fl, rc LSB-first = ~fm   (within 2k bits).
-//   * ASCII bytes come from a 256-entry LDS table (4 bases -> 4 bytes).
+//   * The first multiply of each murmur3 input word and the ASCII byte
+//     assembly are folded into LDS tables (see hash_code).
 //   * Bottom-s selection is a threshold prefilter: a k-mer survives iff
 //     h <= tau[g] where tau[g] ~ C*s/nk_g * 2^64, so only ~C*s of the
 //     ~nk_g hashes per genome reach a per-genome open-addressing set in HBM
@@ -47,40 +48,52 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
 
 // murmurhash3_x64_128(bytes, seed).0 where byte p = ASCII of base p of the
 // LSB-first 2-bit code `code` (K <= 32 bases).
+//
+// Every 8-byte word w of the input enters murmur3 as w * c (c = c1 for the
+// k1 words, c2 for the k2 words).  Multiplication mod 2^64 distributes over
+// the word's bytes, and the bytes are ASCII images of 2-bit codes, so
+//   w * c = T[2i][g_2i] + T[2i+1][g_2i+1]      (mod 2^64)
+// with g_q the 8-bit code of bases 4q..4q+3 and
+//   T[q][g] = ascii4(g) * (c << 32*(q & 1))  (bytes past K masked out).
+// The tables (NW x 256 u64 in LDS) replace the first multiply of every
+// word and the byte assembly.
 template <int K>
 __device__ __forceinline__ uint64_t hash_code(uint64_t code,
-                                              const uint32_t* __restrict__ lut,
+                                              const uint64_t* __restrict__ tab,
                                               uint64_t seed) {
-  constexpr int NW = (K + 3) / 4;  // ASCII words of 4 bytes
-  uint32_t w[8];
+  constexpr int NW = (K + 3) / 4;     // 4-base groups
+  constexpr int NWORD = (NW + 1) / 2;  // 8-byte words
+  uint64_t wp[4];                      // word products
 #pragma unroll
-  for (int q = 0; q < 8; ++q) w[q] = 0;
-#pragma unroll
-  for (int q = 0; q < NW; ++q) w[q] = lut[(uint32_t)(code >> (8 * q)) & 0xFFu];
-  if (K % 4) w[NW - 1] &= (1u << (8 * (K % 4))) - 1u;  // bytes past K are not input
-
+  for (int i = 0; i < NWORD; ++i) {
+    const uint32_t ga = (uint32_t)(code >> (16 * i)) & 0xFFu;
+    uint64_t v = tab[(2 * i) * 256 + ga];
+    if (2 * i + 1 < NW) {
+      const uint32_t gb = (uint32_t)(code >> (16 * i + 8)) & 0xFFu;
+      v += tab[(2 * i + 1) * 256 + gb];
+    }
+    wp[i] = v;
+  }
   const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
   uint64_t h1 = seed, h2 = seed;
   constexpr int NBLK = K / 16;
 #pragma unroll
   for (int b = 0; b < NBLK; ++b) {
-    uint64_t k1 = (uint64_t)w[4 * b] | ((uint64_t)w[4 * b + 1] << 32);
-    uint64_t k2 = (uint64_t)w[4 * b + 2] | ((uint64_t)w[4 * b + 3] << 32);
-    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    uint64_t k1 = wp[2 * b];  // = k1 * c1
+    uint64_t k2 = wp[2 * b + 1];  // = k2 * c2
+    k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
     h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
-    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
     h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
   }
   constexpr int TAIL = K % 16;
   if (TAIL > 8) {
-    uint64_t k2 = (uint64_t)w[4 * NBLK + 2];
-    if (TAIL > 12) k2 |= (uint64_t)w[4 * NBLK + 3] << 32;
-    k2 *= c2; k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    uint64_t k2 = wp[2 * NBLK + 1];
+    k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
   }
   if (TAIL > 0) {
-    uint64_t k1 = (uint64_t)w[4 * NBLK];
-    if (TAIL > 4) k1 |= (uint64_t)w[4 * NBLK + 1] << 32;
-    k1 *= c1; k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    uint64_t k1 = wp[2 * NBLK];
+    k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
   }
   h1 ^= (uint64_t)K;
   h2 ^= (uint64_t)K;
@@ -91,17 +104,23 @@ __device__ __forceinline__ uint64_t hash_code(uint64_t code,
   return h1 + h2;
 }
 
-__device__ __forceinline__ void build_lut(uint32_t* lut) {
-  // ASCII 'A','C','G','T' indexed by 2-bit code; lut[x] = 4 bytes for the
-  // 4 codes of x, code j in bits 2j..2j+1 -> byte j.
-  for (uint32_t x = threadIdx.x; x < 256; x += blockDim.x) {
+// T[q][g] for q < NW (see hash_code).
+template <int K>
+__device__ __forceinline__ void build_tables(uint64_t* tab) {
+  constexpr int NW = (K + 3) / 4;
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)NW * 256; i += blockDim.x) {
+    const uint32_t q = i >> 8, g = i & 255u;
     uint32_t v = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint32_t c = (x >> (2 * j)) & 3u;
-      v |= ((0x54474341u >> (8 * c)) & 0xFFu) << (8 * j);
+      if ((int)(4 * q + j) < K) {
+        const uint32_t c = (g >> (2 * j)) & 3u;
+        v |= ((0x54474341u >> (8 * c)) & 0xFFu) << (8 * j);  // 'A','C','G','T'
+      }
     }
-    lut[x] = v;
+    const uint64_t cw = ((q >> 1) & 1u) ? c2 : c1;  // k1 words: c1, k2 words: c2
+    tab[i] = ((uint64_t)v << (32 * (q & 1u))) * cw;
   }
 }
 
@@ -160,8 +179,8 @@ __device__ __forceinline__ uint32_t find_run(const uint64_t* __restrict__ ks,
 
 template <int K>
 __global__ __launch_bounds__(kBlock) void sketch_candidates_kernel(SketchLaunch a) {
-  __shared__ uint32_t lut[256];
-  build_lut(lut);
+  __shared__ uint64_t mtab[((K + 3) / 4) * 256];  // murmur word tables (hash_code)
+  build_tables<K>(mtab);
   __syncthreads();
 
   constexpr uint64_t MASK = (K == 32) ? ~0ull : ((1ull << (2 * K)) - 1ull);
@@ -179,7 +198,7 @@ __global__ __launch_bounds__(kBlock) void sketch_candidates_kernel(SketchLaunch 
       const uint64_t stop = min(pend, a.run_kstart[r + 1]);
       const uint32_t slot = a.run_slot[r];
       const uint64_t tau = a.tau[slot];
-      uint64_t* tab = a.table + ((uint64_t)slot << a.cap_log2);
+      uint64_t* gset = a.table + ((uint64_t)slot << a.cap_log2);
       uint64_t b = a.run_base[r] + (p - rk0);  // first base of k-mer p
 
       // word cursor
@@ -203,8 +222,8 @@ __global__ __launch_bounds__(kBlock) void sketch_candidates_kernel(SketchLaunch 
         fl = (fl >> 2) | (c << (2 * K - 2));
         const uint64_t rcm = fl ^ MASK;             // reverse complement, MSB-first
         const uint64_t can = (fm < rcm) ? fl : (fm ^ MASK);  // canonical, LSB-first
-        const uint64_t h = hash_code<K>(can, lut, a.seed);
-        if (h <= tau) insert_candidate(tab, cap_mask, a.count + slot, a.limit, a.flags + slot, h);
+        const uint64_t h = hash_code<K>(can, mtab, a.seed);
+        if (h <= tau) insert_candidate(gset, cap_mask, a.count + slot, a.limit, a.flags + slot, h);
       }
       if (p < pend) ++r;
     }
