@@ -30,8 +30,22 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import galah_amd as ga  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-LDS_PEAK_GBS = 256 * 128 * 2.4  # 256 CU x 128 B/clk (ds_read_b32 rate) x 2.4 GHz, GB/s
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+CLK_GHZ = 2.4          # max engine clock
+N_SIMD = 256 * 4       # 256 CUs x 4 SIMD-32
+# K1 (sketch) is VALU-issue bound.  Its per-k-mer instruction mix, counted in
+# the gfx950 ISA of sketch_candidates_kernel<21> and confirmed by PMC
+# (SQ_INSTS_VALU x 64 / k-mers = 116.7, profiles/r01_pmc_sketch.txt):
+# 25 quarter-rate integer multiplies (v_mul_lo_u32 / v_mad_u64_u32, 8 cycles
+# per wave64 on a SIMD-32) + 92 full-rate VALU ops (2 cycles per wave64).
+K1_CYCLES_PER_WAVE_KMER = 25 * 8 + 92 * 2
+K1_PEAK_GKMER = N_SIMD * CLK_GHZ * 64 / K1_CYCLES_PER_WAVE_KMER  # Gkmer/s
+# K2 (pairs): SURVEY 8(d) prices a pair at the reference merge's bytes,
+# 8 B x (|A| + |B|), against LDS bandwidth: 256 B/clk/CU for 64-bit reads.
+LDS_PEAK_GBS = 256 * 256 * CLK_GHZ
+# HBM bytes per K1 launch on this workload from the PMC pass (FETCH_SIZE x 2,
+# the gfx950 correction of MI355X_MICROARCH.md), profiles/r01_pmc_sketch.txt
+K1_PMC_HBM_BYTES_C3 = 3.96e6 * 1024 * 2
 
 
 def parse():
@@ -196,20 +210,24 @@ def main():
     pr_ms = kst["pairs"]["ms"] / max(1, kst["pairs"]["launches"])
     kmers_per_launch = kst["sketch"]["work"] / max(1, kst["sketch"]["launches"])
     pairs_per_launch = kst["pairs"]["work"] / max(1, kst["pairs"]["launches"])
-    k1 = {"kernel": "sketch_candidates_kernel<21>", "bound": "hbm", "unit": "GB/s",
-          "achieved": kmers_per_launch * 0.25 / (sk_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-          "avg_ms": sk_ms, "work_per_launch": kmers_per_launch,
-          "note": "algorithmic bytes = 0.25 B per k-mer position (2-bit input read once)"}
-    k2 = {"kernel": "pairs_merge_kernel", "bound": "lds", "unit": "GB/s",
+    k1_gkmer = kmers_per_launch / (sk_ms * 1e-3) / 1e9
+    k1 = {"kernel": "sketch_candidates_kernel<21>", "bound": "valu", "unit": "Gkmer/s",
+          "achieved": k1_gkmer, "peak": K1_PEAK_GKMER, "avg_ms": sk_ms, "work_per_launch": kmers_per_launch,
+          "hbm_achieved_GBps": kmers_per_launch * 0.25 / (sk_ms * 1e-3) / 1e9, "hbm_peak_GBps": HBM_PEAK_GBS,
+          "traffic": (K1_PMC_HBM_BYTES_C3 if (N == 10000 and glen == 3000000 and world == 1) else None),
+          "note": ("VALU-issue ceiling of the murmur3 mix (25 quarter-rate multiplies + 92 full-rate ops per "
+                   "k-mer, %d cycles per wave64 k-mer, 1024 SIMDs at %.1f GHz); input is 0.25 B/k-mer, so "
+                   "the HBM fraction is small by design" % (K1_CYCLES_PER_WAVE_KMER, CLK_GHZ))}
+    k2 = {"kernel": "pairs_table_kernel<8>", "bound": "lds", "unit": "GB/s",
           "achieved": pairs_per_launch * 16.0 * s / (pr_ms * 1e-3) / 1e9, "peak": LDS_PEAK_GBS,
-          "avg_ms": pr_ms, "work_per_launch": pairs_per_launch,
-          "note": "algorithmic bytes = 8 B x (|A|+|B|) = 16 KB per pair at s=1000"}
+          "avg_ms": pr_ms, "work_per_launch": pairs_per_launch, "traffic": None,
+          "note": "SURVEY 8(d) pricing: 8 B x (|A|+|B|) = 16 KB per pair at s=1000 vs 256 B/clk/CU LDS"}
     dom = k1 if sk_ms * kst["sketch"]["launches"] >= pr_ms * kst["pairs"]["launches"] else k2
-    roof = {"bound": dom["bound"], "achieved": round(dom["achieved"], 3), "peak": dom["peak"],
-            "unit": dom["unit"], "frac": round(dom["achieved"] / dom["peak"], 5), "traffic": None,
+    roof = {"bound": dom["bound"], "achieved": round(dom["achieved"], 3), "peak": round(dom["peak"], 3),
+            "unit": dom["unit"], "frac": round(dom["achieved"] / dom["peak"], 4), "traffic": dom["traffic"],
             "kernel": dom["kernel"], "avg_launch_ms": round(dom["avg_ms"], 4), "note": dom["note"],
-            "other_kernels": [{kk: (round(v, 5) if isinstance(v, float) else v) for kk, v in x.items()}
-                              for x in (k1, k2) if x is not dom]}
+            "kernels": [{kk: (round(v, 5) if isinstance(v, float) else v) for kk, v in x.items()}
+                        for x in (k1, k2)]}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

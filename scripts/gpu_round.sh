@@ -36,7 +36,7 @@ for st in $STAGES; do
     counters)
       run counters 120 rocprofv3 -L || exit $? ;;
     prof)
-      run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
+      run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
   esac
 done
 exit 0
