@@ -29,6 +29,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 import galah_amd as ga  # noqa: E402
+from galah_amd import sharding  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 CLK_GHZ = 2.4          # max engine clock
@@ -123,9 +124,9 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     N, glen, s = a.genomes, a.genome_len, a.sketch
-    assert N % world == 0, "genome count must divide by the GPU count"
-    n_loc = N // world
-    g0 = rank * n_loc
+    g0, g1 = sharding.shard_range(N, world, rank)
+    n_loc = g1 - g0
+    even = N % world == 0
     min_ani = ga.parse_percentage(a.min_ani)
     ctx = ga.Context(k=a.k, sketch_size=s, seed=0, device=local)
     stream = torch.cuda.current_stream()
@@ -141,7 +142,7 @@ def main():
         d_len = torch.empty(N, dtype=torch.int32, device="cuda")
     else:
         d_sk, d_len = d_sk_loc, d_len_loc
-    tb, te = ga.pair_partition(N, world, rank)
+    tb, te = sharding.rank_tiles(N, world, rank)
     cap = max(1 << 22, N * 64)
     d_out = torch.empty(cap * 4, dtype=torch.int32, device="cuda")
     d_cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -155,9 +156,13 @@ def main():
         ctx.sketch_device(d_words, runs, n_loc, d_sk_loc, d_len_loc, stream=sh)
         ev["sketch"][1].record(stream)
         ev["gather"][0].record(stream)
-        if world > 1:
+        if world > 1 and even:
             dist.all_gather_into_tensor(d_sk, d_sk_loc)
             dist.all_gather_into_tensor(d_len, d_len_loc)
+        elif world > 1:
+            gsk, gln = sharding.all_gather_sketches(d_sk_loc, d_len_loc, N, world, rank, dist)
+            d_sk.copy_(gsk)
+            d_len.copy_(gln)
         ev["gather"][1].record(stream)
         d_cnt.zero_()
         ev["pairs"][0].record(stream)

@@ -1,0 +1,114 @@
+// galah_finch.hpp -- C++ mirror of galah's finch precluster interface over
+// the C ABI of libgalahgpu.so (galahgpu.h).  Header-only.
+//
+//   reference (AroneyS/galah @ 2024-12-18)               here
+//   src/lib.rs:23-27   trait PreclusterDistanceFinder     galah::PreclusterDistanceFinder
+//   src/finch.rs:4-24  struct FinchPreclusterer           galah::FinchPreclusterer
+//   src/finch.rs:26-75 finch::distances(...)              galah::finch_distances(...)
+//   src/sorted_pair_genome_distance_cache.rs:4-59         galah::SortedPairGenomeDistanceCache
+//   src/cluster_argument_parsing.rs:1160-1182             galah::parse_percentage
+//
+// Errors: the reference panics ("Failed to sketch genomes with finch",
+// src/finch.rs:50); here the same message is thrown as std::runtime_error.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "galahgpu.h"
+
+namespace galah {
+
+// src/sorted_pair_genome_distance_cache.rs: BTreeMap<(usize,usize), Option<f32>>
+// with keys normalised to (min, max).
+class SortedPairGenomeDistanceCache {
+ public:
+  using Key = std::pair<size_t, size_t>;
+
+  void insert(Key ids, std::optional<float> distance) { internal_[norm(ids)] = distance; }
+  // Option<&Option<f32>>: nullptr when absent
+  const std::optional<float>* get(Key ids) const {
+    auto it = internal_.find(norm(ids));
+    return it == internal_.end() ? nullptr : &it->second;
+  }
+  bool contains_key(Key ids) const { return internal_.count(norm(ids)) != 0; }
+  // :47-58
+  SortedPairGenomeDistanceCache transform_ids(const std::vector<size_t>& input_ids) const {
+    SortedPairGenomeDistanceCache out;
+    for (size_t i = 0; i < input_ids.size(); ++i)
+      for (size_t j = i + 1; j < input_ids.size(); ++j)
+        if (const auto* v = get({input_ids[i], input_ids[j]})) out.insert({i, j}, *v);
+    return out;
+  }
+  size_t size() const { return internal_.size(); }
+  const std::map<Key, std::optional<float>>& internal() const { return internal_; }
+  bool operator==(const SortedPairGenomeDistanceCache& o) const { return internal_ == o.internal_; }
+
+ private:
+  static Key norm(Key k) { return k.first < k.second ? k : Key{k.second, k.first}; }
+  std::map<Key, std::optional<float>> internal_;
+};
+
+// src/lib.rs:23-27
+class PreclusterDistanceFinder {
+ public:
+  virtual ~PreclusterDistanceFinder() = default;
+  virtual SortedPairGenomeDistanceCache distances(const std::vector<std::string>& genome_fasta_paths) = 0;
+  virtual const char* method_name() const = 0;
+};
+
+// CAP:1160-1182 (the --precluster-ani value)
+inline float parse_percentage(float value) {
+  float out = 0.f;
+  if (gg_parse_percentage(value, &out) != GG_OK) throw std::invalid_argument(gg_thread_last_error());
+  return out;
+}
+
+// src/finch.rs:26-75 on the GPU: sketch (K1), all pairs (K2), keep ani >= min_ani.
+inline SortedPairGenomeDistanceCache finch_distances(const std::vector<std::string>& paths,
+                                                     float min_ani, size_t num_kmers,
+                                                     uint8_t kmer_length, int device = -1) {
+  gg_status st = GG_OK;
+  gg_ctx* ctx = gg_create(kmer_length, (uint32_t)num_kmers, 0, device, &st);
+  if (!ctx)
+    throw std::runtime_error(std::string("Failed to sketch genomes with finch: ") + gg_thread_last_error());
+  std::vector<const char*> c_paths;
+  for (const auto& p : paths) c_paths.push_back(p.c_str());
+  gg_pair* pairs = nullptr;
+  float* ani = nullptr;
+  uint64_t n = 0;
+  st = gg_precluster_files(ctx, c_paths.data(), (uint32_t)c_paths.size(), min_ani, &pairs, &ani, &n);
+  if (st != GG_OK) {
+    std::string msg = gg_last_error(ctx);
+    gg_destroy(ctx);
+    throw std::runtime_error("Failed to sketch genomes with finch: " + msg);
+  }
+  SortedPairGenomeDistanceCache cache;
+  for (uint64_t i = 0; i < n; ++i) cache.insert({pairs[i].i, pairs[i].j}, ani[i]);
+  gg_free(pairs);
+  gg_free(ani);
+  gg_destroy(ctx);
+  return cache;
+}
+
+// src/finch.rs:4-24
+class FinchPreclusterer : public PreclusterDistanceFinder {
+ public:
+  FinchPreclusterer(float min_ani, size_t num_kmers = 1000, uint8_t kmer_length = 21)
+      : min_ani(min_ani), num_kmers(num_kmers), kmer_length(kmer_length) {}
+  SortedPairGenomeDistanceCache distances(const std::vector<std::string>& paths) override {
+    return finch_distances(paths, min_ani, num_kmers, kmer_length);
+  }
+  const char* method_name() const override { return "finch"; }
+
+  float min_ani;  // fraction, not percentage
+  size_t num_kmers;
+  uint8_t kmer_length;
+};
+
+}  // namespace galah
