@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo stages collectives through host memory (testing ranks that share one GPU)")
     return ap.parse_args()
 
 
@@ -120,9 +122,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gloo = a.dist_backend == "gloo"
+    if gloo:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     N, glen, s = a.genomes, a.genome_len, a.sketch
     g0, g1 = sharding.shard_range(N, world, rank)
     n_loc = g1 - g0
@@ -156,7 +164,11 @@ def main():
         ctx.sketch_device(d_words, runs, n_loc, d_sk_loc, d_len_loc, stream=sh)
         ev["sketch"][1].record(stream)
         ev["gather"][0].record(stream)
-        if world > 1 and even:
+        if world > 1 and gloo:
+            gsk, gln = sharding.all_gather_sketches(d_sk_loc.cpu(), d_len_loc.cpu(), N, world, rank, dist)
+            d_sk.copy_(gsk)
+            d_len.copy_(gln)
+        elif world > 1 and even:
             dist.all_gather_into_tensor(d_sk, d_sk_loc)
             dist.all_gather_into_tensor(d_len, d_len_loc)
         elif world > 1:
@@ -198,6 +210,8 @@ def main():
     t = torch.tensor([elapsed, phase["sketch"], phase["pairs"], phase["gather"], float(found)],
                      dtype=torch.float64, device="cuda")
     if world > 1:
+        if gloo:
+            t = t.cpu()
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t.clone()
