@@ -46,6 +46,29 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
   return k;
 }
 
+// h * 5 + c with one full-rate v_lshl_add_u64 (hipcc otherwise lowers the
+// multiply by 5 to two quarter-rate v_mad_u64_u32).
+__device__ __forceinline__ uint64_t times5_plus(uint64_t h, uint64_t c) {
+  uint64_t r;
+  asm("v_lshl_add_u64 %0, %1, 2, %1" : "=v"(r) : "v"(h));
+  return r + c;
+}
+
+// Tail words of at most kTailMaxBases bases get a whole-word table.
+constexpr int kTailMaxBases = 5;
+
+template <int K>
+struct HashShape {
+  static constexpr int NW = (K + 3) / 4;          // 4-base groups
+  static constexpr int NBLK = K / 16;             // full 16-byte blocks
+  static constexpr int TAIL = K % 16;             // tail bytes
+  static constexpr bool TAIL_TAB = TAIL >= 1 && TAIL <= kTailMaxBases;
+  // groups that need a group table (all but the tail word's when TAIL_TAB)
+  static constexpr int NG = TAIL_TAB ? 4 * NBLK : NW;
+  static constexpr int TAIL_ENTRIES = TAIL_TAB ? (1 << (2 * TAIL)) : 0;
+  static constexpr int TAB_U64 = NG * 256 + TAIL_ENTRIES;
+};
+
 // murmurhash3_x64_128(bytes, seed).0 where byte p = ASCII of base p of the
 // LSB-first 2-bit code `code` (K <= 32 bases).
 //
@@ -55,45 +78,42 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
 //   w * c = T[2i][g_2i] + T[2i+1][g_2i+1]      (mod 2^64)
 // with g_q the 8-bit code of bases 4q..4q+3 and
 //   T[q][g] = ascii4(g) * (c << 32*(q & 1))  (bytes past K masked out).
-// The tables (NW x 256 u64 in LDS) replace the first multiply of every
-// word and the byte assembly.
+// A tail k1 word of <= 5 bases (k = 21: bases 16..20) is a function of at
+// most 10 bits, so its whole contribution rotl(w * c1, 31) * c2 is one
+// table entry.  Tables live in LDS (tab, HashShape<K>::TAB_U64 entries).
 template <int K>
 __device__ __forceinline__ uint64_t hash_code(uint64_t code,
                                               const uint64_t* __restrict__ tab,
                                               uint64_t seed) {
-  constexpr int NW = (K + 3) / 4;     // 4-base groups
-  constexpr int NWORD = (NW + 1) / 2;  // 8-byte words
-  uint64_t wp[4];                      // word products
-#pragma unroll
-  for (int i = 0; i < NWORD; ++i) {
-    const uint32_t ga = (uint32_t)(code >> (16 * i)) & 0xFFu;
-    uint64_t v = tab[(2 * i) * 256 + ga];
-    if (2 * i + 1 < NW) {
-      const uint32_t gb = (uint32_t)(code >> (16 * i + 8)) & 0xFFu;
-      v += tab[(2 * i + 1) * 256 + gb];
-    }
-    wp[i] = v;
-  }
+  using S = HashShape<K>;
   const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
   uint64_t h1 = seed, h2 = seed;
-  constexpr int NBLK = K / 16;
 #pragma unroll
-  for (int b = 0; b < NBLK; ++b) {
-    uint64_t k1 = wp[2 * b];  // = k1 * c1
-    uint64_t k2 = wp[2 * b + 1];  // = k2 * c2
+  for (int b = 0; b < S::NBLK; ++b) {
+    uint64_t k1 = tab[(4 * b) * 256 + ((uint32_t)(code >> (32 * b)) & 0xFFu)] +
+                  tab[(4 * b + 1) * 256 + ((uint32_t)(code >> (32 * b + 8)) & 0xFFu)];  // = k1 * c1
+    uint64_t k2 = tab[(4 * b + 2) * 256 + ((uint32_t)(code >> (32 * b + 16)) & 0xFFu)] +
+                  tab[(4 * b + 3) * 256 + ((uint32_t)(code >> (32 * b + 24)) & 0xFFu)];  // = k2 * c2
     k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
-    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = times5_plus(h1, 0x52dce729);
     k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
-    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = times5_plus(h2, 0x38495ab5);
   }
-  constexpr int TAIL = K % 16;
-  if (TAIL > 8) {
-    uint64_t k2 = wp[2 * NBLK + 1];
-    k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
-  }
-  if (TAIL > 0) {
-    uint64_t k1 = wp[2 * NBLK];
-    k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+  if (S::TAIL_TAB) {
+    const uint32_t x = (uint32_t)(code >> (32 * S::NBLK)) & (uint32_t)(S::TAIL_ENTRIES - 1);
+    h1 ^= tab[S::NG * 256 + x];
+  } else {
+    constexpr int q0 = 4 * S::NBLK;  // first group of the tail
+    if (S::TAIL > 8) {
+      uint64_t k2 = tab[(q0 + 2) * 256 + ((uint32_t)(code >> (32 * S::NBLK + 16)) & 0xFFu)];
+      if (q0 + 3 < S::NW) k2 += tab[(q0 + 3) * 256 + ((uint32_t)(code >> (32 * S::NBLK + 24)) & 0xFFu)];
+      k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+    }
+    if (S::TAIL > 0) {
+      uint64_t k1 = tab[q0 * 256 + ((uint32_t)(code >> (32 * S::NBLK)) & 0xFFu)];
+      if (q0 + 1 < S::NW) k1 += tab[(q0 + 1) * 256 + ((uint32_t)(code >> (32 * S::NBLK + 8)) & 0xFFu)];
+      k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+    }
   }
   h1 ^= (uint64_t)K;
   h2 ^= (uint64_t)K;
@@ -104,23 +124,34 @@ __device__ __forceinline__ uint64_t hash_code(uint64_t code,
   return h1 + h2;
 }
 
-// T[q][g] for q < NW (see hash_code).
+__device__ __forceinline__ uint32_t ascii_bytes(uint32_t codes, int nbases) {
+  uint32_t v = 0;
+  for (int j = 0; j < nbases; ++j) {
+    const uint32_t c = (codes >> (2 * j)) & 3u;
+    v |= ((0x54474341u >> (8 * c)) & 0xFFu) << (8 * j);  // 'A','C','G','T'
+  }
+  return v;
+}
+
 template <int K>
 __device__ __forceinline__ void build_tables(uint64_t* tab) {
-  constexpr int NW = (K + 3) / 4;
+  using S = HashShape<K>;
   const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
-  for (uint32_t i = threadIdx.x; i < (uint32_t)NW * 256; i += blockDim.x) {
-    const uint32_t q = i >> 8, g = i & 255u;
-    uint32_t v = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if ((int)(4 * q + j) < K) {
-        const uint32_t c = (g >> (2 * j)) & 3u;
-        v |= ((0x54474341u >> (8 * c)) & 0xFFu) << (8 * j);  // 'A','C','G','T'
-      }
+  for (uint32_t i = threadIdx.x; i < (uint32_t)S::TAB_U64; i += blockDim.x) {
+    if (i < (uint32_t)S::NG * 256) {
+      const uint32_t q = i >> 8, g = i & 255u;
+      const int nb = min(4, K - 4 * (int)q);                // valid bases of the group
+      const uint64_t cw = ((q >> 1) & 1u) ? c2 : c1;      // k1 words: c1, k2 words: c2
+      tab[i] = ((uint64_t)ascii_bytes(g, nb) << (32 * (q & 1u))) * cw;
+    } else {
+      // whole tail k1 word: bases 16*NBLK .. +TAIL-1 -> rotl(w * c1, 31) * c2
+      const uint32_t x = i - (uint32_t)S::NG * 256;
+      uint64_t w = ascii_bytes(x & 0xFFu, min(4, S::TAIL));
+      if (S::TAIL > 4) w |= (uint64_t)ascii_bytes(x >> 8, S::TAIL - 4) << 32;
+      uint64_t k1 = w * c1;
+      k1 = rotl64(k1, 31);
+      tab[i] = k1 * c2;
     }
-    const uint64_t cw = ((q >> 1) & 1u) ? c2 : c1;  // k1 words: c1, k2 words: c2
-    tab[i] = ((uint64_t)v << (32 * (q & 1u))) * cw;
   }
 }
 
@@ -179,7 +210,7 @@ __device__ __forceinline__ uint32_t find_run(const uint64_t* __restrict__ ks,
 
 template <int K>
 __global__ __launch_bounds__(kBlock) void sketch_candidates_kernel(SketchLaunch a) {
-  __shared__ uint64_t mtab[((K + 3) / 4) * 256];  // murmur word tables (hash_code)
+  __shared__ uint64_t mtab[HashShape<K>::TAB_U64];  // murmur word tables (hash_code)
   build_tables<K>(mtab);
   __syncthreads();
 
