@@ -35,11 +35,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 CLK_GHZ = 2.4          # max engine clock
 N_SIMD = 256 * 4       # 256 CUs x 4 SIMD-32
 # K1 (sketch) is VALU-issue bound.  Its per-k-mer instruction mix, counted in
-# the gfx950 ISA of sketch_candidates_kernel<21> and confirmed by PMC
-# (SQ_INSTS_VALU x 64 / k-mers = 116.7, profiles/r01_pmc_sketch.txt):
-# 25 quarter-rate integer multiplies (v_mul_lo_u32 / v_mad_u64_u32, 8 cycles
-# per wave64 on a SIMD-32) + 92 full-rate VALU ops (2 cycles per wave64).
-K1_CYCLES_PER_WAVE_KMER = 25 * 8 + 92 * 2
+# the gfx950 ISA of sketch_candidates_kernel<21> (hot loop: 96 VALU) and
+# checked against PMC SQ_INSTS_VALU (profiles/r01_pmc_sketch*.txt):
+# 18 quarter-rate integer multiplies (v_mul_lo_u32 / v_mad_u64_u32, 8 cycles
+# per wave64 on a SIMD-32) + 78 full-rate VALU ops (2 cycles per wave64).
+K1_CYCLES_PER_WAVE_KMER = 18 * 8 + 78 * 2
 K1_PEAK_GKMER = N_SIMD * CLK_GHZ * 64 / K1_CYCLES_PER_WAVE_KMER  # Gkmer/s
 # K2 (pairs): SURVEY 8(d) prices a pair at the reference merge's bytes,
 # 8 B x (|A| + |B|), against LDS bandwidth: 256 B/clk/CU for 64-bit reads.
@@ -234,7 +234,7 @@ def main():
           "achieved": k1_gkmer, "peak": K1_PEAK_GKMER, "avg_ms": sk_ms, "work_per_launch": kmers_per_launch,
           "hbm_achieved_GBps": kmers_per_launch * 0.25 / (sk_ms * 1e-3) / 1e9, "hbm_peak_GBps": HBM_PEAK_GBS,
           "traffic": (K1_PMC_HBM_BYTES_C3 if (N == 10000 and glen == 3000000 and world == 1) else None),
-          "note": ("VALU-issue ceiling of the murmur3 mix (25 quarter-rate multiplies + 92 full-rate ops per "
+          "note": ("VALU-issue ceiling of the murmur3 mix (18 quarter-rate multiplies + 78 full-rate ops per "
                    "k-mer, %d cycles per wave64 k-mer, 1024 SIMDs at %.1f GHz); input is 0.25 B/k-mer, so "
                    "the HBM fraction is small by design" % (K1_CYCLES_PER_WAVE_KMER, CLK_GHZ))}
     k2 = {"kernel": "pairs_table_kernel<8>", "bound": "lds", "unit": "GB/s",
