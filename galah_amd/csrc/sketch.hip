@@ -245,17 +245,41 @@ __global__ __launch_bounds__(kBlock) void sketch_candidates_kernel(SketchLaunch 
         fm = (fm << 2) | c;
         fl = (fl >> 2) | (c << (2 * K - 2));
       }
-      for (; p < stop; ++p) {
+      // two k-mers per iteration: two independent hash chains interleave
+      uint32_t todo = (uint32_t)(stop - p);
+      for (; todo >= 2; todo -= 2) {
+        if (left == 0) { cur = a.words[++wi]; left = 16; }
+        const uint64_t ca = cur >> 30;
+        cur <<= 2; --left;
+        if (left == 0) { cur = a.words[++wi]; left = 16; }
+        const uint64_t cb = cur >> 30;
+        cur <<= 2; --left;
+        const uint64_t fma = ((fm << 2) | ca) & MASK;
+        const uint64_t fla = (fl >> 2) | (ca << (2 * K - 2));
+        fm = ((fma << 2) | cb) & MASK;
+        fl = (fla >> 2) | (cb << (2 * K - 2));
+        // reverse complement MSB-first = ~fl; canonical in LSB-first order
+        const uint64_t cana = (fma < (fla ^ MASK)) ? fla : (fma ^ MASK);
+        const uint64_t canb = (fm < (fl ^ MASK)) ? fl : (fm ^ MASK);
+        const uint64_t ha = hash_code<K>(cana, mtab, a.seed);
+        const uint64_t hb = hash_code<K>(canb, mtab, a.seed);
+        // one branch for both so neither hash chain is sunk past it
+        if ((ha <= tau) | (hb <= tau)) {
+          if (ha <= tau) insert_candidate(gset, cap_mask, a.count + slot, a.limit, a.flags + slot, ha);
+          if (hb <= tau) insert_candidate(gset, cap_mask, a.count + slot, a.limit, a.flags + slot, hb);
+        }
+      }
+      if (todo) {
         if (left == 0) { cur = a.words[++wi]; left = 16; }
         const uint64_t c = cur >> 30;
         cur <<= 2; --left;
         fm = ((fm << 2) | c) & MASK;
         fl = (fl >> 2) | (c << (2 * K - 2));
-        const uint64_t rcm = fl ^ MASK;             // reverse complement, MSB-first
-        const uint64_t can = (fm < rcm) ? fl : (fm ^ MASK);  // canonical, LSB-first
+        const uint64_t can = (fm < (fl ^ MASK)) ? fl : (fm ^ MASK);
         const uint64_t h = hash_code<K>(can, mtab, a.seed);
         if (h <= tau) insert_candidate(gset, cap_mask, a.count + slot, a.limit, a.flags + slot, h);
       }
+      p = stop;
       if (p < pend) ++r;
     }
   }
