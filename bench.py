@@ -33,20 +33,23 @@ from galah_amd import sharding  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 CLK_GHZ = 2.4          # max engine clock
-N_SIMD = 256 * 4       # 256 CUs x 4 SIMD-32
-# K1 (sketch) is VALU-issue bound.  Its per-k-mer instruction mix, counted in
-# the gfx950 ISA of sketch_candidates_kernel<21> (hot loop: 96 VALU) and
-# checked against PMC SQ_INSTS_VALU (profiles/r01_pmc_sketch*.txt):
-# 18 quarter-rate integer multiplies (v_mul_lo_u32 / v_mad_u64_u32, 8 cycles
-# per wave64 on a SIMD-32) + 78 full-rate VALU ops (2 cycles per wave64).
-K1_CYCLES_PER_WAVE_KMER = 18 * 8 + 78 * 2
-K1_PEAK_GKMER = N_SIMD * CLK_GHZ * 64 / K1_CYCLES_PER_WAVE_KMER  # Gkmer/s
+N_SIMD = 256 * 4       # 256 CUs x 4 SIMDs
+# K1 (sketch) is VALU-issue bound.  A SIMD issues one wave64 integer VALU
+# instruction per 4 cycles (16 lanes x 4 passes; multiplies included --
+# scripts/ubench_valu.hip, profiles/r01_ubench_valu.txt).  K1's VALU count per
+# k-mer (all of the kernel: hashing, windows, segment setup, candidate
+# inserts) is SQ_INSTS_VALU / (k-mers / 64) from the PMC pass over the C3
+# launch (profiles/r01_pmc_sketch.txt).  Ceiling = 1024 SIMDs x 2.4 GHz x 64
+# lanes / (4 cycles x VALU per k-mer).
+K1_CYCLES_PER_VALU = 4
+K1_VALU_PER_KMER = 3.667e10 / (29999800000 / 64)
+K1_PEAK_GKMER = N_SIMD * CLK_GHZ * 64 / (K1_CYCLES_PER_VALU * K1_VALU_PER_KMER)  # Gkmer/s
 # K2 (pairs): SURVEY 8(d) prices a pair at the reference merge's bytes,
 # 8 B x (|A| + |B|), against LDS bandwidth: 256 B/clk/CU for 64-bit reads.
 LDS_PEAK_GBS = 256 * 256 * CLK_GHZ
 # HBM bytes per K1 launch on this workload from the PMC pass (FETCH_SIZE x 2,
 # the gfx950 correction of MI355X_MICROARCH.md), profiles/r01_pmc_sketch.txt
-K1_PMC_HBM_BYTES_C3 = 3.96e6 * 1024 * 2
+K1_PMC_HBM_BYTES_C3 = 4.002e6 * 1024 * 2
 
 
 def parse():
@@ -234,9 +237,10 @@ def main():
           "achieved": k1_gkmer, "peak": K1_PEAK_GKMER, "avg_ms": sk_ms, "work_per_launch": kmers_per_launch,
           "hbm_achieved_GBps": kmers_per_launch * 0.25 / (sk_ms * 1e-3) / 1e9, "hbm_peak_GBps": HBM_PEAK_GBS,
           "traffic": (K1_PMC_HBM_BYTES_C3 if (N == 10000 and glen == 3000000 and world == 1) else None),
-          "note": ("VALU-issue ceiling of the murmur3 mix (18 quarter-rate multiplies + 78 full-rate ops per "
-                   "k-mer, %d cycles per wave64 k-mer, 1024 SIMDs at %.1f GHz); input is 0.25 B/k-mer, so "
-                   "the HBM fraction is small by design" % (K1_CYCLES_PER_WAVE_KMER, CLK_GHZ))}
+          "valu_per_kmer": K1_VALU_PER_KMER,
+          "note": ("VALU-issue ceiling: %.1f VALU per wave64 k-mer (PMC) x %d cycles each, 1024 SIMDs at "
+                   "%.1f GHz; input is 0.25 B/k-mer, so the HBM fraction is small by design"
+                   % (K1_VALU_PER_KMER, K1_CYCLES_PER_VALU, CLK_GHZ))}
     k2 = {"kernel": "pairs_table_kernel<8>", "bound": "lds", "unit": "GB/s",
           "achieved": pairs_per_launch * 16.0 * s / (pr_ms * 1e-3) / 1e9, "peak": LDS_PEAK_GBS,
           "avg_ms": pr_ms, "work_per_launch": pairs_per_launch, "traffic": None,

@@ -29,7 +29,8 @@ __all__ = [
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libgalahgpu.so")
+# GALAHGPU_LIB points at an alternate build (A/B kernel experiments)
+LIB_PATH = os.environ.get("GALAHGPU_LIB") or os.path.join(HERE, "lib", "libgalahgpu.so")
 
 PAIR_DTYPE = np.dtype([("i", np.uint32), ("j", np.uint32), ("common", np.uint32), ("total", np.uint32)])
 

@@ -325,6 +325,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       }
       SketchLaunch a;
       a.words = d_words;
+      a.n_words = n_words;
       a.run_base = d_rb;
       a.run_kstart = d_rk;
       a.run_slot = d_rs;

@@ -30,6 +30,7 @@ constexpr uint32_t kSortCap = 16384;
 
 struct SketchLaunch {
   const uint32_t* words;
+  uint64_t n_words;
   const uint64_t* run_base;    // [n_runs]
   const uint64_t* run_kstart;  // [n_runs + 1] exclusive prefix of k-mer counts
   const uint32_t* run_slot;    // [n_runs] genome slot within the batch

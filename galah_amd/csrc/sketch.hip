@@ -31,10 +31,29 @@ namespace gg {
 namespace {
 
 constexpr int kSeg = 32;        // k-mer positions per lane per segment
+constexpr int kGroup = 4;       // k-mers per tau-check branch
 constexpr int kBlock = 256;
+// min waves per SIMD forced on the register allocator (8 = 64 VGPRs; the
+// k = 21 body then spills a few dwords and runs ~1% slower than at 66 VGPRs)
+#ifndef GG_K1_MIN_WAVES
+#define GG_K1_MIN_WAVES 1
+#endif
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
-  return (x << r) | (x >> (64 - r));
+// 64-bit rotate left by a compile-time amount as two v_alignbit_b32
+// (hipcc otherwise emits a 64-bit shift + shift + or).
+template <int R>
+__device__ __forceinline__ uint64_t rotl64(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  if (R >= 32) {
+    const uint32_t t = lo;
+    lo = hi;
+    hi = t;
+  }
+  constexpr int r = R & 31;
+  if (r == 0) return ((uint64_t)hi << 32) | lo;
+  const uint32_t nh = __builtin_amdgcn_alignbit(hi, lo, 32 - r);
+  const uint32_t nl = __builtin_amdgcn_alignbit(lo, hi, 32 - r);
+  return ((uint64_t)nh << 32) | nl;
 }
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
@@ -46,8 +65,8 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
   return k;
 }
 
-// h * 5 + c with one full-rate v_lshl_add_u64 (hipcc otherwise lowers the
-// multiply by 5 to two quarter-rate v_mad_u64_u32).
+// h * 5 + c with one v_lshl_add_u64 (hipcc otherwise lowers the multiply by
+// 5 to v_mad_u64_u32 sequences).
 __device__ __forceinline__ uint64_t times5_plus(uint64_t h, uint64_t c) {
   uint64_t r;
   asm("v_lshl_add_u64 %0, %1, 2, %1" : "=v"(r) : "v"(h));
@@ -69,8 +88,16 @@ struct HashShape {
   static constexpr int TAB_U64 = NG * 256 + TAIL_ENTRIES;
 };
 
+// 8-bit code of bases 4q..4q+3 of a top-aligned MSB-first k-mer code
+// (base 0 in bits 63..62): byte 3 - q%4 of word q/4.
+__device__ __forceinline__ uint32_t group_byte(uint32_t hi, uint32_t lo, int q) {
+  const uint32_t w = (q < 4) ? hi : lo;
+  return (w >> (8 * (3 - (q & 3)))) & 0xFFu;
+}
+
 // murmurhash3_x64_128(bytes, seed).0 where byte p = ASCII of base p of the
-// LSB-first 2-bit code `code` (K <= 32 bases).
+// k-mer whose MSB-first 2-bit code is top-aligned in `code` (base 0 in bits
+// 63..62; bits below 64-2K are ignored, K <= 32).
 //
 // Every 8-byte word w of the input enters murmur3 as w * c (c = c1 for the
 // k1 words, c2 for the k2 words).  Multiplication mod 2^64 distributes over
@@ -79,43 +106,45 @@ struct HashShape {
 // with g_q the 8-bit code of bases 4q..4q+3 and
 //   T[q][g] = ascii4(g) * (c << 32*(q & 1))  (bytes past K masked out).
 // A tail k1 word of <= 5 bases (k = 21: bases 16..20) is a function of at
-// most 10 bits, so its whole contribution rotl(w * c1, 31) * c2 is one
-// table entry.  Tables live in LDS (tab, HashShape<K>::TAB_U64 entries).
+// most 10 bits, so its whole contribution rotl(w * c1, 31) * c2, and the
+// final h1 ^= len, is one table entry.  Tables live in LDS
+// (HashShape<K>::TAB_U64 entries).
 template <int K>
 __device__ __forceinline__ uint64_t hash_code(uint64_t code,
                                               const uint64_t* __restrict__ tab,
                                               uint64_t seed) {
   using S = HashShape<K>;
   const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  const uint32_t hi = (uint32_t)(code >> 32), lo = (uint32_t)code;
   uint64_t h1 = seed, h2 = seed;
 #pragma unroll
   for (int b = 0; b < S::NBLK; ++b) {
-    uint64_t k1 = tab[(4 * b) * 256 + ((uint32_t)(code >> (32 * b)) & 0xFFu)] +
-                  tab[(4 * b + 1) * 256 + ((uint32_t)(code >> (32 * b + 8)) & 0xFFu)];  // = k1 * c1
-    uint64_t k2 = tab[(4 * b + 2) * 256 + ((uint32_t)(code >> (32 * b + 16)) & 0xFFu)] +
-                  tab[(4 * b + 3) * 256 + ((uint32_t)(code >> (32 * b + 24)) & 0xFFu)];  // = k2 * c2
-    k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
-    h1 = rotl64(h1, 27); h1 += h2; h1 = times5_plus(h1, 0x52dce729);
-    k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
-    h2 = rotl64(h2, 31); h2 += h1; h2 = times5_plus(h2, 0x38495ab5);
+    uint64_t k1 = tab[(4 * b) * 256 + group_byte(hi, lo, 4 * b)] +
+                  tab[(4 * b + 1) * 256 + group_byte(hi, lo, 4 * b + 1)];  // = k1 * c1
+    uint64_t k2 = tab[(4 * b + 2) * 256 + group_byte(hi, lo, 4 * b + 2)] +
+                  tab[(4 * b + 3) * 256 + group_byte(hi, lo, 4 * b + 3)];  // = k2 * c2
+    k1 = rotl64<31>(k1); k1 *= c2; h1 ^= k1;
+    h1 = rotl64<27>(h1); h1 += h2; h1 = times5_plus(h1, 0x52dce729);
+    k2 = rotl64<33>(k2); k2 *= c1; h2 ^= k2;
+    h2 = rotl64<31>(h2); h2 += h1; h2 = times5_plus(h2, 0x38495ab5);
   }
   if (S::TAIL_TAB) {
-    const uint32_t x = (uint32_t)(code >> (32 * S::NBLK)) & (uint32_t)(S::TAIL_ENTRIES - 1);
-    h1 ^= tab[S::NG * 256 + x];
+    const uint32_t w = S::NBLK ? lo : hi;
+    h1 ^= tab[S::NG * 256 + (w >> (32 - 2 * S::TAIL))];  // includes ^= len
   } else {
     constexpr int q0 = 4 * S::NBLK;  // first group of the tail
     if (S::TAIL > 8) {
-      uint64_t k2 = tab[(q0 + 2) * 256 + ((uint32_t)(code >> (32 * S::NBLK + 16)) & 0xFFu)];
-      if (q0 + 3 < S::NW) k2 += tab[(q0 + 3) * 256 + ((uint32_t)(code >> (32 * S::NBLK + 24)) & 0xFFu)];
-      k2 = rotl64(k2, 33); k2 *= c1; h2 ^= k2;
+      uint64_t k2 = tab[(q0 + 2) * 256 + group_byte(hi, lo, q0 + 2)];
+      if (q0 + 3 < S::NW) k2 += tab[(q0 + 3) * 256 + group_byte(hi, lo, q0 + 3)];
+      k2 = rotl64<33>(k2); k2 *= c1; h2 ^= k2;
     }
     if (S::TAIL > 0) {
-      uint64_t k1 = tab[q0 * 256 + ((uint32_t)(code >> (32 * S::NBLK)) & 0xFFu)];
-      if (q0 + 1 < S::NW) k1 += tab[(q0 + 1) * 256 + ((uint32_t)(code >> (32 * S::NBLK + 8)) & 0xFFu)];
-      k1 = rotl64(k1, 31); k1 *= c2; h1 ^= k1;
+      uint64_t k1 = tab[q0 * 256 + group_byte(hi, lo, q0)];
+      if (q0 + 1 < S::NW) k1 += tab[(q0 + 1) * 256 + group_byte(hi, lo, q0 + 1)];
+      k1 = rotl64<31>(k1); k1 *= c2; h1 ^= k1;
     }
+    h1 ^= (uint64_t)K;
   }
-  h1 ^= (uint64_t)K;
   h2 ^= (uint64_t)K;
   h1 += h2;
   h2 += h1;
@@ -124,11 +153,13 @@ __device__ __forceinline__ uint64_t hash_code(uint64_t code,
   return h1 + h2;
 }
 
-__device__ __forceinline__ uint32_t ascii_bytes(uint32_t codes, int nbases) {
-  uint32_t v = 0;
+// ASCII bytes of `nbases` bases of an MSB-first code of `width` bases
+// (base j of the code -> byte j).
+__device__ __forceinline__ uint64_t ascii_msb(uint32_t codes, int width, int nbases) {
+  uint64_t v = 0;
   for (int j = 0; j < nbases; ++j) {
-    const uint32_t c = (codes >> (2 * j)) & 3u;
-    v |= ((0x54474341u >> (8 * c)) & 0xFFu) << (8 * j);  // 'A','C','G','T'
+    const uint32_t c = (codes >> (2 * (width - 1 - j))) & 3u;
+    v |= (uint64_t)((0x54474341u >> (8 * c)) & 0xFFu) << (8 * j);  // 'A','C','G','T'
   }
   return v;
 }
@@ -142,15 +173,12 @@ __device__ __forceinline__ void build_tables(uint64_t* tab) {
       const uint32_t q = i >> 8, g = i & 255u;
       const int nb = min(4, K - 4 * (int)q);                // valid bases of the group
       const uint64_t cw = ((q >> 1) & 1u) ? c2 : c1;      // k1 words: c1, k2 words: c2
-      tab[i] = ((uint64_t)ascii_bytes(g, nb) << (32 * (q & 1u))) * cw;
+      tab[i] = (ascii_msb(g, 4, nb) << (32 * (q & 1u))) * cw;
     } else {
-      // whole tail k1 word: bases 16*NBLK .. +TAIL-1 -> rotl(w * c1, 31) * c2
+      // whole tail k1 word: bases 16*NBLK .. +TAIL-1 -> rotl(w * c1, 31) * c2 ^ len
       const uint32_t x = i - (uint32_t)S::NG * 256;
-      uint64_t w = ascii_bytes(x & 0xFFu, min(4, S::TAIL));
-      if (S::TAIL > 4) w |= (uint64_t)ascii_bytes(x >> 8, S::TAIL - 4) << 32;
-      uint64_t k1 = w * c1;
-      k1 = rotl64(k1, 31);
-      tab[i] = k1 * c2;
+      const uint64_t w = ascii_msb(x, S::TAIL, S::TAIL);
+      tab[i] = (rotl64<31>(w * c1) * c2) ^ (uint64_t)K;
     }
   }
 }
@@ -208,13 +236,40 @@ __device__ __forceinline__ uint32_t find_run(const uint64_t* __restrict__ ks,
   return lo;
 }
 
-template <int K>
-__global__ __launch_bounds__(kBlock) void sketch_candidates_kernel(SketchLaunch a) {
+// Reverse complement of 16 MSB-first 2-bit bases: reverse the base order
+// (bit reverse, then swap the two bits of each base) and complement.
+__device__ __forceinline__ uint32_t revcomp16(uint32_t x) {
+  const uint32_t y = __builtin_bitreverse32(x);
+  return ~(((y >> 1) & 0x55555555u) | ((y << 1) & 0xAAAAAAAAu));
+}
+
+// 32 bits of the base stream held in w[0..3] (MSB-first, 16 bases per word)
+// starting at base t; bases past the window read as 0.  t is a compile-time
+// constant after unrolling, so this is a register pick or one v_alignbit_b32.
+__device__ __forceinline__ uint32_t window32(const uint32_t (&w)[4], int t) {
+  const int a = t >> 4, sh = t & 15;
+  const uint32_t x = a < 4 ? w[a] : 0u;
+  if (sh == 0) return x;
+  const uint32_t y = a + 1 < 4 ? w[a + 1] : 0u;
+  return __builtin_amdgcn_alignbit(x, y, 32 - 2 * sh);
+}
+
+// Each lane owns kSeg consecutive k-mer positions.  For every maximal piece
+// of the segment inside one run it loads the 64-base window starting at the
+// piece's first base (5 words, funnel-shifted to the base offset) and its
+// reverse complement.  The forward and reverse-complement codes of k-mer i
+// of the window are then static 64-bit slices of the two windows, top-aligned
+// (bits below the k-mer hold the following bases and are ignored): no
+// rolling state, and the canonical code is a 64-bit min.  K-mers past the
+// piece (i >= cnt) are hashed but never inserted.
+template <int K, bool SEED0>
+__global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_kernel(SketchLaunch a) {
+  static_assert(K >= 1 && K <= 32 && kSeg + K - 1 <= 64, "window");
   __shared__ uint64_t mtab[HashShape<K>::TAB_U64];  // murmur word tables (hash_code)
   build_tables<K>(mtab);
   __syncthreads();
 
-  constexpr uint64_t MASK = (K == 32) ? ~0ull : ((1ull << (2 * K)) - 1ull);
+  const uint64_t seed = SEED0 ? 0ull : a.seed;
   const uint32_t cap_mask = (1u << a.cap_log2) - 1u;
   const uint64_t nseg = (a.n_kmers + kSeg - 1) / kSeg;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
@@ -227,57 +282,52 @@ __global__ __launch_bounds__(kBlock) void sketch_candidates_kernel(SketchLaunch 
     while (p < pend) {
       const uint64_t rk0 = a.run_kstart[r];
       const uint64_t stop = min(pend, a.run_kstart[r + 1]);
+      const uint32_t cnt = (uint32_t)(stop - p);
       const uint32_t slot = a.run_slot[r];
       const uint64_t tau = a.tau[slot];
       uint64_t* gset = a.table + ((uint64_t)slot << a.cap_log2);
-      uint64_t b = a.run_base[r] + (p - rk0);  // first base of k-mer p
+      const uint64_t b = a.run_base[r] + (p - rk0);  // first base of k-mer p
 
-      // word cursor
-      uint64_t wi = b >> 4;
-      uint32_t cur = a.words[wi] << (2 * (uint32_t)(b & 15));
-      uint32_t left = 16 - (uint32_t)(b & 15);
-      uint64_t fm = 0, fl = 0;
+      const uint64_t wi = b >> 4;
+      const uint32_t off = (uint32_t)b & 15u;
+      uint32_t w[5];
 #pragma unroll
-      for (int i = 0; i < K - 1; ++i) {
-        if (left == 0) { cur = a.words[++wi]; left = 16; }
-        const uint64_t c = cur >> 30;
-        cur <<= 2; --left;
-        fm = (fm << 2) | c;
-        fl = (fl >> 2) | (c << (2 * K - 2));
-      }
-      // two k-mers per iteration: two independent hash chains interleave
-      uint32_t todo = (uint32_t)(stop - p);
-      for (; todo >= 2; todo -= 2) {
-        if (left == 0) { cur = a.words[++wi]; left = 16; }
-        const uint64_t ca = cur >> 30;
-        cur <<= 2; --left;
-        if (left == 0) { cur = a.words[++wi]; left = 16; }
-        const uint64_t cb = cur >> 30;
-        cur <<= 2; --left;
-        const uint64_t fma = ((fm << 2) | ca) & MASK;
-        const uint64_t fla = (fl >> 2) | (ca << (2 * K - 2));
-        fm = ((fma << 2) | cb) & MASK;
-        fl = (fla >> 2) | (cb << (2 * K - 2));
-        // reverse complement MSB-first = ~fl; canonical in LSB-first order
-        const uint64_t cana = (fma < (fla ^ MASK)) ? fla : (fma ^ MASK);
-        const uint64_t canb = (fm < (fl ^ MASK)) ? fl : (fm ^ MASK);
-        const uint64_t ha = hash_code<K>(cana, mtab, a.seed);
-        const uint64_t hb = hash_code<K>(canb, mtab, a.seed);
-        // one branch for both so neither hash chain is sunk past it
-        if ((ha <= tau) | (hb <= tau)) {
-          if (ha <= tau) insert_candidate(gset, cap_mask, a.count + slot, a.limit, a.flags + slot, ha);
-          if (hb <= tau) insert_candidate(gset, cap_mask, a.count + slot, a.limit, a.flags + slot, hb);
+      for (int j = 0; j < 5; ++j) w[j] = (wi + j < a.n_words) ? a.words[wi + j] : 0u;
+      uint32_t F[4], R[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        F[j] = off ? __builtin_amdgcn_alignbit(w[j], w[j + 1], 32 - 2 * off) : w[j];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) R[m] = revcomp16(F[3 - m]);
+
+#pragma unroll
+      for (int g = 0; g < kSeg / kGroup; ++g) {
+        uint64_t h[kGroup];
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) {
+          const int i = g * kGroup + j;
+          const uint64_t fwd = ((uint64_t)window32(F, i) << 32) | window32(F, i + 16);
+          const int t0 = 64 - K - i;  // reverse complement of k-mer i starts here
+          const uint64_t rev = ((uint64_t)window32(R, t0) << 32) | window32(R, t0 + 16);
+          h[j] = hash_code<K>(fwd < rev ? fwd : rev, mtab, seed);
         }
-      }
-      if (todo) {
-        if (left == 0) { cur = a.words[++wi]; left = 16; }
-        const uint64_t c = cur >> 30;
-        cur <<= 2; --left;
-        fm = ((fm << 2) | c) & MASK;
-        fl = (fl >> 2) | (c << (2 * K - 2));
-        const uint64_t can = (fm < (fl ^ MASK)) ? fl : (fm ^ MASK);
-        const uint64_t h = hash_code<K>(can, mtab, a.seed);
-        if (h <= tau) insert_candidate(gset, cap_mask, a.count + slot, a.limit, a.flags + slot, h);
+        bool any = false;
+#pragma unroll
+        for (int j = 0; j < kGroup; ++j) any |= h[j] <= tau;
+        if (any) {
+          uint32_t pending = 0;
+#pragma unroll
+          for (int j = 0; j < kGroup; ++j)
+            pending |= ((h[j] <= tau) & ((uint32_t)(g * kGroup + j) < cnt)) ? (1u << j) : 0u;
+          while (pending) {
+            const int j = __builtin_ctz(pending);
+            pending &= pending - 1;
+            uint64_t hv = h[0];
+#pragma unroll
+            for (int q = 1; q < kGroup; ++q) hv = (j == q) ? h[q] : hv;
+            insert_candidate(gset, cap_mask, a.count + slot, a.limit, a.flags + slot, hv);
+          }
+        }
       }
       p = stop;
       if (p < pend) ++r;
@@ -355,7 +405,12 @@ __global__ __launch_bounds__(kBlock) void sketch_finalize_kernel(
 
 template <int K>
 hipError_t launch_k(const SketchLaunch& a, int grid, hipStream_t st) {
-  hipLaunchKernelGGL(sketch_candidates_kernel<K>, dim3(grid), dim3(kBlock), 0, st, a);
+  // finch always hashes with seed 0 (src/finch.rs:41); that variant drops the
+  // seed terms from the murmur3 block at compile time.
+  if (a.seed == 0)
+    hipLaunchKernelGGL((sketch_candidates_kernel<K, true>), dim3(grid), dim3(kBlock), 0, st, a);
+  else
+    hipLaunchKernelGGL((sketch_candidates_kernel<K, false>), dim3(grid), dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 

@@ -27,6 +27,8 @@ for st in $STAGES; do
       run bench_1k 300 python -u bench.py --genomes 1000 --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
     bench)
       run bench 600 python -u bench.py --steps 3 --warmup 1 || exit $? ;;
+    benchalt)  # same bench against an alternate build (GALAHGPU_LIB)
+      GALAHGPU_LIB="${ALT_LIB:?}" run bench_alt 600 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
     bench2r)
       run bench_2rank_gloo 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --genomes 2000 --dist-backend gloo || exit $? ;;
     k2)
