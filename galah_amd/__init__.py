@@ -26,6 +26,7 @@ __all__ = [
     "ani_f32", "ani_f64", "parse_percentage", "pair_tiles", "pair_partition",
     "SortedPairGenomeDistanceCache", "PreclusterDistanceFinder",
     "FinchPreclusterer", "distances", "PAIR_DTYPE", "LIB_PATH", "EXPORTED_SYMBOLS",
+    "partition_preclusters", "precluster_pairs", "preclusters", "LOCAL_PAIR_DTYPE",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -43,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "gg_pair_tiles", "gg_pair_partition", "gg_pairs", "gg_pairs_device",
     "gg_precluster_files", "gg_ani_f64", "gg_ani_f32", "gg_parse_percentage",
     "gg_free", "gg_synth_clustered_device", "gg_timing_enable", "gg_timing_read",
+    "gg_partition_preclusters", "gg_precluster_pairs",
 )
 
 GG_OK = 0
@@ -114,6 +116,8 @@ _sig("gg_ani_f32", ctypes.c_float, [_u32, _u32, _i32])
 _sig("gg_parse_percentage", _i32, [ctypes.c_float, ctypes.POINTER(ctypes.c_float)])
 _sig("gg_free", None, [_vp])
 _sig("gg_synth_clustered_device", _i32, [_vp, _u32, _u32, _u32, _u32, ctypes.c_float, _u64, _vp, _vp, _vp])
+_sig("gg_partition_preclusters", _i32, [_u32, _vp, _u64, _vp, _vp, ctypes.POINTER(_u32)])
+_sig("gg_precluster_pairs", _i32, [_u32, _vp, _u64, _vp, _vp, _u32, _vp, _vp])
 
 
 class _KStats(ctypes.Structure):
@@ -170,6 +174,58 @@ def pair_partition(n, parts, part):
     b, e = _u64(), _u64()
     _L.gg_pair_partition(n, parts, part, ctypes.byref(b), ctypes.byref(e))
     return b.value, e.value
+
+
+LOCAL_PAIR_DTYPE = np.dtype([("precluster", np.uint32), ("i", np.uint32), ("j", np.uint32), ("src", np.uint32)])
+
+
+def _as_pairs(pairs):
+    p = np.zeros(len(pairs), dtype=PAIR_DTYPE)
+    for f in ("i", "j"):
+        p[f] = pairs[f]
+    for f in ("common", "total"):
+        if pairs.dtype.names and f in pairs.dtype.names:
+            p[f] = pairs[f]
+    return p
+
+
+def partition_preclusters(n_genomes, pairs):
+    """src/clusterer.rs:409-431 partition_sketches + :45-57: single linkage
+    over the passing pairs -> (members, offsets): precluster s is
+    members[offsets[s]:offsets[s+1]], ascending; largest precluster first,
+    ties by smallest member.  Host C++ (union-find), linear in the pairs."""
+    p = _as_pairs(pairs)
+    members = np.zeros(max(n_genomes, 1), np.uint32)
+    offsets = np.zeros(n_genomes + 1, np.uint32)
+    ns = _u32()
+    st = _L.gg_partition_preclusters(n_genomes, _ptr(p), len(p), _ptr(members), _ptr(offsets), ctypes.byref(ns))
+    if st != GG_OK:
+        raise _thread_err(st)
+    return members[:n_genomes], offsets[:ns.value + 1].copy()
+
+
+def precluster_pairs(n_genomes, pairs, members, offsets):
+    """transform_ids (src/sorted_pair_genome_distance_cache.rs:47-58) for
+    every precluster at once -> (local pairs [LOCAL_PAIR_DTYPE] grouped by
+    precluster and sorted by (i, j), pair_offsets)."""
+    p = _as_pairs(pairs)
+    members = np.ascontiguousarray(members, dtype=np.uint32)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint32)
+    ns = len(offsets) - 1
+    out = np.zeros(max(len(p), 1), LOCAL_PAIR_DTYPE)
+    poff = np.zeros(ns + 1, np.uint64)
+    st = _L.gg_precluster_pairs(n_genomes, _ptr(p), len(p), _ptr(members), _ptr(offsets), ns, _ptr(out),
+                                _ptr(poff))
+    if st != GG_OK:
+        raise _thread_err(st)
+    return out[:len(p)], poff
+
+
+def preclusters(n_genomes, pairs):
+    """The preclusters as galah's cluster() holds them (src/clusterer.rs:45-57):
+    a list of ascending index lists, largest first."""
+    members, offsets = partition_preclusters(n_genomes, pairs)
+    return [members[offsets[s]:offsets[s + 1]].tolist() for s in range(len(offsets) - 1)]
 
 
 class Packed:

@@ -166,6 +166,39 @@ gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths,
                               uint32_t n_paths, float min_ani, gg_pair** pairs,
                               float** ani, uint64_t* n_out);
 
+/* ---- after distances(): preclusters -------- */
+/* src/clusterer.rs:409-431 partition_sketches (single linkage over the
+ * pairs the cache contains) + :45-57 (each set sorted ascending, sets
+ * ordered by size descending; ties: by smallest member).  Linear in
+ * n_pairs (union-find) instead of the reference's O(N^2) contains_key
+ * scan.  pairs may be in any order.  Output is CSR: precluster s is
+ * members[offsets[s] .. offsets[s+1]); members has n_genomes entries,
+ * offsets n_genomes + 1 (caller-owned); *n_sets receives the count. */
+gg_status gg_partition_preclusters(uint32_t n_genomes, const gg_pair* pairs,
+                                   uint64_t n_pairs, uint32_t* members,
+                                   uint32_t* offsets, uint32_t* n_sets);
+
+/* One pair of a precluster's sub-cache: src/sorted_pair_genome_distance_cache.rs
+ * :47-58 transform_ids(precluster members) keys it (i, j), i < j, by
+ * position inside the precluster; src indexes the input pairs array (for
+ * its ANI value). */
+typedef struct gg_local_pair {
+  uint32_t precluster;
+  uint32_t i;
+  uint32_t j;
+  uint32_t src;
+} gg_local_pair;
+
+/* transform_ids for every precluster at once (src/clusterer.rs:70), linear
+ * in n_pairs instead of O(m^2) per precluster.  Every pair must lie inside
+ * one precluster (true for the partition of the same pairs).  out has
+ * n_pairs entries, grouped by precluster and sorted by (i, j) inside it;
+ * pair_offsets has n_sets + 1 entries. */
+gg_status gg_precluster_pairs(uint32_t n_genomes, const gg_pair* pairs,
+                              uint64_t n_pairs, const uint32_t* members,
+                              const uint32_t* offsets, uint32_t n_sets,
+                              gg_local_pair* out, uint64_t* pair_offsets);
+
 /* ---- host arithmetic shared with the caller ---------------------------- */
 /* src/finch.rs:56-64: 1 - finch mash_distance, f64, Rust NaN semantics */
 double gg_ani_f64(uint32_t common, uint32_t total, int kmer_length);

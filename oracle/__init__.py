@@ -157,3 +157,48 @@ def pairs_parallel(sketches, lens, min_ani, k=21, threads=1):
     cnt = lib().oracle_pairs_parallel(_ptr(sketches), _ptr(lens), n, stride, k, ctypes.c_float(min_ani),
                                       threads, ctypes.byref(cs))
     return cnt, cs.value
+
+
+# --------------------------------------------------------------------------
+# After distances(): galah's own loops, restated in plain Python (small N).
+# --------------------------------------------------------------------------
+def partition_sketches(n_genomes, pair_keys):
+    """src/clusterer.rs:409-431 restated: for i, for j < i, join(i, j) iff
+    the cache contains (i, j) (key normalised to (min, max)), then
+    src/clusterer.rs:45-57: each set sorted ascending, sets ordered by size
+    descending.  Ties among equal sizes are left to the reference's
+    DisjointSetVec::sets() + sort_unstable; here they are ordered by
+    smallest member (Python's sort is stable over first-member order)."""
+    keys = {(min(a, b), max(a, b)) for a, b in pair_keys}
+    parent = list(range(n_genomes))
+
+    def find(x):
+        while parent[x] != x:
+            x = parent[x]
+        return x
+
+    for i in range(n_genomes):
+        for j in range(i):
+            if (j, i) in keys:
+                ri, rj = find(i), find(j)
+                if ri != rj:
+                    parent[max(ri, rj)] = min(ri, rj)
+    sets = {}
+    for g in range(n_genomes):
+        sets.setdefault(find(g), []).append(g)
+    out = sorted(sets.values(), key=lambda s: s[0])
+    out.sort(key=lambda s: -len(s))
+    return out
+
+
+def transform_ids(cache, input_ids):
+    """src/sorted_pair_genome_distance_cache.rs:47-58 restated over a dict
+    {(i, j): value} with i < j."""
+    out = {}
+    for i, g1 in enumerate(input_ids):
+        for j in range(i + 1, len(input_ids)):
+            g2 = input_ids[j]
+            k = (min(g1, g2), max(g1, g2))
+            if k in cache:
+                out[(i, j)] = cache[k]
+    return out
