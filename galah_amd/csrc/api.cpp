@@ -35,7 +35,8 @@ struct gg_ctx {
     uint64_t work;
   };
   std::vector<gg::PairSeg> seg_host;
-  bool force_merge = false;  // GALAHGPU_PAIRS_KERNEL=merge (testing)
+  int pairs_kernel = 0;  // GALAHGPU_PAIRS_KERNEL: 0 gate (default), 1 table, 2 merge
+  std::vector<uint32_t> sufmin_host;
   bool timing = false;
   std::vector<Timed> timed;
   std::vector<hipEvent_t> spare_events;
@@ -364,73 +365,127 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   return GG_OK;
 }
 
-gg_status ensure_cmin(gg_ctx* c, float min_ani, uint32_t** d_cmin, hipStream_t st) {
+gg_status ensure_cmin(gg_ctx* c, float min_ani, uint32_t** d_cmin, uint32_t** d_sufmin, hipStream_t st) {
   const uint32_t tmax = 2 * c->s;
-  GG_HIP(c, scratch_t(c, "cmin", tmax + 1, d_cmin));
+  GG_HIP(c, scratch_t(c, "cmin", 2 * (tmax + 1), d_cmin));
+  *d_sufmin = *d_cmin + (tmax + 1);
   if (c->cmin_key != min_ani || c->cmin_host.size() != tmax + 1) {
     c->cmin_host = build_cmin(c->s, c->k, min_ani);
+    // sufmin[t] = min(cmin[t..tmax]): a lower bound of cmin[total] for any
+    // total >= t (the gate kernel's candidate test)
+    c->sufmin_host.assign(tmax + 1, 0xFFFFFFFFu);
+    uint32_t m = 0xFFFFFFFFu;
+    for (uint32_t t = tmax + 1; t-- > 0;) {
+      m = std::min(m, c->cmin_host[t]);
+      c->sufmin_host[t] = m;
+    }
     c->cmin_key = min_ani;
   }
   GG_HIP(c, hipMemcpyAsync(*d_cmin, c->cmin_host.data(), (tmax + 1) * sizeof(uint32_t),
                            hipMemcpyHostToDevice, st));
+  GG_HIP(c, hipMemcpyAsync(*d_sufmin, c->sufmin_host.data(), (tmax + 1) * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, st));
   return GG_OK;
+}
+
+// Work items of the table kernels: runs of <= seg_tiles column tiles of one
+// tile row, inside tiles [tb, te).
+void build_segments(std::vector<PairSeg>& segs, uint64_t nb, uint64_t tb, uint64_t te, uint32_t seg_tiles) {
+  segs.clear();
+  uint64_t t = 0;
+  for (uint64_t I = 0; I < nb && t < te; ++I) {
+    const uint64_t first = t, last = t + (nb - I);
+    const uint64_t lo = std::max(first, tb), hi = std::min(last, te);
+    for (uint64_t x = lo; x < hi; x += seg_tiles) {
+      const uint64_t y = std::min(hi, x + seg_tiles);
+      segs.push_back(PairSeg{(uint32_t)I, (uint32_t)(I + (x - first)), (uint32_t)(I + (y - first)), 0});
+    }
+    t = last;
+  }
 }
 
 gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
                      uint64_t tb, uint64_t te, float min_ani, gg_pair* d_out, uint64_t cap,
                      uint64_t* d_count, hipStream_t st) {
-  uint32_t* d_cmin;
-  gg_status cs = ensure_cmin(c, min_ani, &d_cmin, st);
+  uint32_t *d_cmin, *d_sufmin;
+  gg_status cs = ensure_cmin(c, min_ani, &d_cmin, &d_sufmin, st);
   if (cs != GG_OK) return cs;
-  PairsLaunch a;
-  a.sketches = d_sk;
-  a.lens = d_lens;
-  a.n = n;
-  a.stride = c->s;
-  a.n_row_tiles = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
-  a.tile_begin = tb;
-  a.tile_end = std::min<uint64_t>(te, gg_pair_tiles(n));
-  a.cmin = d_cmin;
-  a.tmax = 2 * c->s;
-  a.out = d_out;
-  a.out_cap = cap;
-  a.count = (unsigned long long*)d_count;
-  const uint64_t work = c->timing ? pairs_in_tiles(n, a.tile_begin, a.tile_end) : 0;
-  if (c->force_merge || pairs_table_rows(c->s) == 0) {
+  const uint64_t nb = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
+  te = std::min<uint64_t>(te, gg_pair_tiles(n));
+  const uint64_t work = c->timing ? pairs_in_tiles(n, tb, te) : 0;
+  const int kern = (c->pairs_kernel == 1 && pairs_table_rows(c->s) == 0) ? 2 : c->pairs_kernel;
+  if (kern == 2) {
+    PairsLaunch a;
+    a.sketches = d_sk;
+    a.lens = d_lens;
+    a.n = n;
+    a.stride = c->s;
+    a.n_row_tiles = (uint32_t)nb;
+    a.tile_begin = tb;
+    a.tile_end = te;
+    a.cmin = d_cmin;
+    a.tmax = 2 * c->s;
+    a.out = d_out;
+    a.out_cap = cap;
+    a.count = (unsigned long long*)d_count;
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs(a, st); }));
     return GG_OK;
   }
-  // table kernel: segments of <= kSegTiles column tiles of one tile row
-  c->seg_host.clear();
-  const uint64_t nb = a.n_row_tiles;
-  uint64_t t = 0;
-  for (uint64_t I = 0; I < nb && t < a.tile_end; ++I) {
-    const uint64_t first = t, last = t + (nb - I);
-    const uint64_t lo = std::max(first, a.tile_begin), hi = std::min(last, a.tile_end);
-    for (uint64_t x = lo; x < hi; x += kSegTiles) {
-      const uint64_t y = std::min(hi, x + kSegTiles);
-      c->seg_host.push_back(PairSeg{(uint32_t)I, (uint32_t)(I + (x - first)), (uint32_t)(I + (y - first)), 0});
-    }
-    t = last;
-  }
+  build_segments(c->seg_host, nb, tb, te, kern == 0 ? kGateSegTiles : kSegTiles);
+  if (c->seg_host.empty()) return GG_OK;
   PairSeg* d_segs;
-  GG_HIP(c, scratch_t(c, "pair_segs", std::max<size_t>(c->seg_host.size(), 1), &d_segs));
-  if (!c->seg_host.empty())
-    GG_HIP(c, hipMemcpyAsync(d_segs, c->seg_host.data(), c->seg_host.size() * sizeof(PairSeg),
-                             hipMemcpyHostToDevice, st));
-  PairsTableLaunch b;
-  b.sketches = d_sk;
-  b.lens = d_lens;
-  b.n = n;
-  b.stride = c->s;
-  b.segs = d_segs;
-  b.n_segs = (uint32_t)c->seg_host.size();
-  b.cmin = d_cmin;
-  b.tmax = 2 * c->s;
-  b.out = d_out;
-  b.out_cap = cap;
-  b.count = (unsigned long long*)d_count;
-  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs_table(b, st); }));
+  GG_HIP(c, scratch_t(c, "pair_segs", c->seg_host.size(), &d_segs));
+  GG_HIP(c, hipMemcpyAsync(d_segs, c->seg_host.data(), c->seg_host.size() * sizeof(PairSeg),
+                           hipMemcpyHostToDevice, st));
+  if (kern == 1) {
+    PairsTableLaunch b;
+    b.sketches = d_sk;
+    b.lens = d_lens;
+    b.n = n;
+    b.stride = c->s;
+    b.segs = d_segs;
+    b.n_segs = (uint32_t)c->seg_host.size();
+    b.cmin = d_cmin;
+    b.tmax = 2 * c->s;
+    b.out = d_out;
+    b.out_cap = cap;
+    b.count = (unsigned long long*)d_count;
+    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs_table(b, st); }));
+    return GG_OK;
+  }
+  // gate kernel: tables for the tile rows this range touches, then the stream
+  const GateParams gp = gate_params(c->s);
+  const uint32_t I0 = c->seg_host.front().I, I1 = c->seg_host.back().I;
+  GateBuildLaunch bl;
+  bl.sketches = d_sk;
+  bl.lens = d_lens;
+  bl.n = n;
+  bl.stride = c->s;
+  bl.tile_row0 = I0;
+  bl.n_blocks = (I1 - I0 + 1) * gp.G;
+  bl.p = gp;
+  GG_HIP(c, scratch_t(c, "gate_tables", (size_t)bl.n_blocks * gp.block_bytes, &bl.tables));
+  GateLaunch g;
+  g.sketches = d_sk;
+  g.lens = d_lens;
+  g.n = n;
+  g.stride = c->s;
+  g.segs = d_segs;
+  g.n_segs = (uint32_t)c->seg_host.size();
+  g.tile_row0 = I0;
+  g.p = gp;
+  g.tables = bl.tables;
+  g.cmin = d_cmin;
+  g.sufmin = d_sufmin;
+  g.tmax = 2 * c->s;
+  g.zero_passes = c->sufmin_host[0] == 0;
+  g.out = d_out;
+  g.out_cap = cap;
+  g.count = (unsigned long long*)d_count;
+  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] {
+    hipError_t e = launch_gate_build(bl, st);
+    return e != hipSuccess ? e : launch_pairs_gate(g, st);
+  }));
   return GG_OK;
 }
 
@@ -570,7 +625,7 @@ gg_ctx* gg_create(int kmer_length, uint32_t sketch_size, uint64_t hash_seed, int
   c->seed = hash_seed;
   c->device = dev;
   const char* pk = getenv("GALAHGPU_PAIRS_KERNEL");
-  c->force_merge = pk && strcmp(pk, "merge") == 0;
+  c->pairs_kernel = !pk ? 0 : strcmp(pk, "table") == 0 ? 1 : strcmp(pk, "merge") == 0 ? 2 : 0;
   hipError_t e = hipSetDevice(dev);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   (void)e;

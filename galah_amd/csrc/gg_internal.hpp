@@ -96,6 +96,50 @@ struct PairsTableLaunch {
 uint32_t pairs_table_rows(uint32_t s);
 hipError_t launch_pairs_table(const PairsTableLaunch& a, hipStream_t st);
 
+// pairs_gate.hip: the gated-table pair kernel (default K2).
+constexpr uint32_t kGateCap = 32768;    // keys per row block (R * s)
+constexpr uint32_t kGateRowsMax = 32;   // rows per row block (bits of a row mask)
+constexpr uint32_t kGateSegTiles = 8;   // column tiles per work item
+struct GateParams {
+  uint32_t R;         // rows per row block
+  uint32_t G;         // row blocks per tile row (ceil(GG_PAIR_TILE / R))
+  uint32_t cap;       // R * s
+  uint32_t nb;        // value buckets (power of two)
+  uint32_t bm_words;  // gate bitmap words (power of two)
+  uint64_t block_bytes;
+};
+GateParams gate_params(uint32_t s);  // requires s <= kGateCap
+struct GateBuildLaunch {
+  const uint64_t* sketches;
+  const uint32_t* lens;
+  uint32_t n;
+  uint32_t stride;
+  uint32_t tile_row0;  // first tile row with a table
+  uint32_t n_blocks;   // tables to build
+  GateParams p;
+  uint8_t* tables;
+};
+struct GateLaunch {
+  const uint64_t* sketches;
+  const uint32_t* lens;
+  uint32_t n;
+  uint32_t stride;
+  const PairSeg* segs;
+  uint32_t n_segs;
+  uint32_t tile_row0;
+  GateParams p;
+  const uint8_t* tables;
+  const uint32_t* cmin;    // [tmax + 1]
+  const uint32_t* sufmin;  // [tmax + 1] min(cmin[t..tmax])
+  uint32_t tmax;
+  uint32_t zero_passes;    // cmin[t] == 0 for some t (then every pair passes)
+  gg_pair* out;
+  uint64_t out_cap;
+  unsigned long long* count;
+};
+hipError_t launch_gate_build(const GateBuildLaunch& a, hipStream_t st);
+hipError_t launch_pairs_gate(const GateLaunch& a, hipStream_t st);
+
 // synth.hip
 hipError_t launch_synth(uint32_t first_genome, uint32_t n_genomes, uint32_t genome_len,
                         uint32_t cluster_size, float max_sub_rate,

@@ -13,6 +13,7 @@
 //
 // Pair space: upper-triangle tiles of GG_PAIR_TILE x GG_PAIR_TILE, row-major.
 // Passing pairs are appended with one atomic per wave (ballot + mbcnt).
+#include "device_util.hpp"
 #include "gg_internal.hpp"
 
 namespace gg {
@@ -138,39 +139,6 @@ struct TableMeta {
   uint32_t nrows;
   uint32_t packed;
 };
-
-__device__ __forceinline__ uint32_t top32(uint64_t b, uint32_t sr, uint32_t sl) {
-  return (uint32_t)((b >> sr) << sl);
-}
-
-// Monotone in b, so bucket order is key order.
-__device__ __forceinline__ uint32_t bucket_of(uint64_t b, uint32_t sr, uint32_t sl, uint32_t scale) {
-  return (uint32_t)(((uint64_t)top32(b, sr, sl) * scale) >> 32);
-}
-
-// bytes 0..3 of the result = bits 0..3 of x
-__device__ __forceinline__ uint32_t spread4(uint32_t x) {
-  return ((x & 15u) * 0x204081u) & 0x01010101u;
-}
-
-// Sum over the 64 lanes with DPP (VALU-native; __shfl_xor would go through
-// ds_bpermute): row_shr 1/2/4/8 gives each 16-lane row's inclusive prefix,
-// row_bcast 15/31 carries the row totals, lane 63 holds the wave total.
-// The result is wave-uniform.
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);  // row_shr:1
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);  // row_shr:2
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);  // row_shr:4
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);  // row_shr:8
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-__device__ __forceinline__ uint32_t uni32(uint32_t v) { return __builtin_amdgcn_readfirstlane((int)v); }
-__device__ __forceinline__ uint64_t uni64(uint64_t v) {
-  return ((uint64_t)uni32((uint32_t)(v >> 32)) << 32) | uni32((uint32_t)v);
-}
 
 // Lane r < R receives #{ e < lb : B[e] <= x_r } (B ascending, lb > 0).
 // Level 1: 64 samples shared by all rows; level 2: 64/R lanes per row scan

@@ -1,0 +1,407 @@
+// Kernel K2, gated-table form (the default pair kernel).
+//
+// Same contract as pairs.hip (src/finch.rs:53-73: finch's merge-to-first-
+// exhaustion, common = |A n B|, total = i + j - common, pass iff
+// common >= cmin[total]), organised so that the work per pair is a few
+// VALU instructions instead of a merge:
+//
+//  * Row blocks.  The R (<= 32) rows of a row block share one table, built
+//    once per launch by gate_build_kernel into HBM: the block's distinct
+//    keys in value buckets (dir = start | count << 16), a 32-bit row mask
+//    per key, and a gate bitmap with bit (key mod 2^b) set for every key.
+//    R * s <= 32768 keys, so at s = 1000 a row block holds 32 rows.
+//  * Gate.  pairs_gate_kernel copies the row block's bitmap (64 KiB at
+//    s = 1000) into LDS and streams column sketches through it: per column
+//    hash one LDS read and a bit test.  With 32k keys in 2^19 bits ~6% of
+//    the hashes of an unrelated column pass the gate.  Passing hashes are
+//    queued per wave (LDS ring of column positions) and resolved 64 at a
+//    time by a walk of the bucket in HBM/L2.  One column hash therefore
+//    serves all R rows, and the table walk runs only for gate hits.
+//  * Totals.  A pair can pass only if common >= min(cmin[t], t >= min(|A|,
+//    |B|)) (the first exhaustion leaves total >= |A| or >= |B|), so the
+//    ranks that finch's total needs are computed (binary searches) only for
+//    those rows -- in practice for related pairs only.
+//
+// Bound: VALU issue of the gate loop (~10 instructions per 64 column
+// hashes, shared by R rows) and L2 bandwidth for the streamed columns.
+#include <algorithm>
+#include <type_traits>
+
+#include "device_util.hpp"
+#include "gg_internal.hpp"
+
+namespace gg {
+namespace {
+
+constexpr int kThreads = 1024;
+constexpr int kWaves = kThreads / 64;
+constexpr uint32_t kRing = 128;      // per-wave queue of column positions (<= 63 + 64 pending)
+constexpr int kRounds = 8;           // 64-hash rounds per register chunk
+constexpr uint32_t kMetaBytes = 512;
+
+struct GateMeta {
+  uint64_t last[kGateRowsMax];  // largest hash of each row
+  uint32_t len[kGateRowsMax];
+  uint64_t maxkey;
+  uint32_t shift_r, shift_l, scale, nrows;
+};
+static_assert(sizeof(GateMeta) <= kMetaBytes, "meta");
+
+// One row block's table in HBM: meta | dir[nb] | bitmap[bm_words] | keys[cap] | masks[cap]
+struct BlockView {
+  const GateMeta* meta;
+  uint32_t* dir;
+  uint32_t* bm;
+  uint64_t* keys;
+  uint32_t* masks;
+};
+
+__device__ __forceinline__ BlockView block_view(const uint8_t* base, const GateParams& p) {
+  uint8_t* b = const_cast<uint8_t*>(base);
+  BlockView v;
+  v.meta = reinterpret_cast<const GateMeta*>(b);
+  v.dir = reinterpret_cast<uint32_t*>(b + kMetaBytes);
+  v.bm = v.dir + p.nb;
+  v.keys = reinterpret_cast<uint64_t*>(v.bm + p.bm_words);
+  v.masks = reinterpret_cast<uint32_t*>(v.keys + p.cap);
+  return v;
+}
+
+// #{ e < n : a[e] <= x }, a ascending
+__device__ __forceinline__ uint32_t count_le(const uint64_t* __restrict__ a, uint32_t n, uint64_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// ---------------------------------------------------------------------------
+// Table build: one workgroup per row block.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void gate_build_kernel(GateBuildLaunch a) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  const GateParams p = a.p;
+  uint32_t* cnt = sm;          // [nb]: counts, then bucket starts, then bucket ends
+  uint32_t* bm = sm + p.nb;    // [bm_words]
+  __shared__ GateMeta meta;
+  __shared__ uint32_t pre[kGateRowsMax + 1];
+  __shared__ uint32_t wsum[kWaves];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t blk = blockIdx.x;
+  const uint32_t I = a.tile_row0 + blk / p.G, rb = blk % p.G;
+  const uint32_t row0 = I * GG_PAIR_TILE + rb * p.R;
+  const uint32_t row_end = min(min(row0 + p.R, (I + 1) * GG_PAIR_TILE), a.n);
+  BlockView v = block_view(a.tables + (size_t)blk * p.block_bytes, p);
+
+  if (tid == 0) {
+    const uint32_t nrows = row0 < row_end ? row_end - row0 : 0;
+    uint64_t mx = 0;
+    uint32_t acc = 0;
+    for (uint32_t r = 0; r < kGateRowsMax; ++r) {
+      uint32_t l = 0;
+      uint64_t last = 0;
+      if (r < nrows) {
+        l = a.lens[row0 + r];
+        if (l) last = a.sketches[(uint64_t)(row0 + r) * a.stride + l - 1];
+      }
+      meta.len[r] = l;
+      meta.last[r] = last;
+      pre[r] = acc;
+      acc += l;
+      if (l && last > mx) mx = last;
+    }
+    pre[kGateRowsMax] = acc;
+    meta.maxkey = mx;
+    const uint32_t L = mx ? 64 - __builtin_clzll(mx) : 1;
+    meta.shift_r = L > 32 ? L - 32 : 0;
+    meta.shift_l = L > 32 ? 0 : 32 - L;
+    const uint64_t t = (uint64_t)top32(mx, meta.shift_r, meta.shift_l) + 1;  // in (2^31, 2^32]
+    meta.scale = (uint32_t)(((uint64_t)p.nb << 32) / t);
+    meta.nrows = nrows;
+  }
+  for (uint32_t i = tid; i < p.nb + p.bm_words; i += kThreads) sm[i] = 0;
+  __syncthreads();
+  const uint32_t E = pre[kGateRowsMax];
+  const uint32_t sr = meta.shift_r, sl = meta.shift_l, scale = meta.scale;
+  const uint32_t bmask = p.bm_words * 32 - 1;
+  auto entry = [&](uint32_t e, uint32_t& r) {
+    r = 0;
+    for (uint32_t x = 1; x < p.R; ++x) r += (e >= pre[x]) ? 1u : 0u;
+    return a.sketches[(uint64_t)(row0 + r) * a.stride + (e - pre[r])];
+  };
+
+  // pass 1: bucket counts and the gate bitmap
+  for (uint32_t e = tid; e < E; e += kThreads) {
+    uint32_t r;
+    const uint64_t key = entry(e, r);
+    atomicAdd(&cnt[bucket_of(key, sr, sl, scale)], 1u);
+    const uint32_t bit = (uint32_t)key & bmask;
+    atomicOr(&bm[bit >> 5], 1u << (bit & 31));
+  }
+  __syncthreads();
+  // exclusive scan of the counts -> bucket starts
+  {
+    const uint32_t per = (p.nb + kThreads - 1) / kThreads;
+    const uint32_t b0 = min(tid * per, p.nb), b1 = min(b0 + per, p.nb);
+    uint32_t s = 0;
+    for (uint32_t b = b0; b < b1; ++b) s += cnt[b];
+    uint32_t inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t run = inc - s;
+    for (uint32_t w = 0; w < wave; ++w) run += wsum[w];
+    for (uint32_t b = b0; b < b1; ++b) {
+      const uint32_t c = cnt[b];
+      cnt[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  // pass 2: scatter (afterwards cnt[b] = end of bucket b = start of b + 1)
+  for (uint32_t e = tid; e < E; e += kThreads) {
+    uint32_t r;
+    const uint64_t key = entry(e, r);
+    const uint32_t slot = atomicAdd(&cnt[bucket_of(key, sr, sl, scale)], 1u);
+    v.keys[slot] = key;
+    v.masks[slot] = 1u << r;
+  }
+  __syncthreads();
+  // pass 3: sort each bucket, merge keys shared by several rows
+  for (uint32_t b = tid; b < p.nb; b += kThreads) {
+    const uint32_t s0 = b ? cnt[b - 1] : 0u, s1 = cnt[b];
+    for (uint32_t i = s0 + 1; i < s1; ++i) {
+      const uint64_t k = v.keys[i];
+      const uint32_t m = v.masks[i];
+      uint32_t j = i;
+      while (j > s0 && v.keys[j - 1] > k) {
+        v.keys[j] = v.keys[j - 1];
+        v.masks[j] = v.masks[j - 1];
+        --j;
+      }
+      v.keys[j] = k;
+      v.masks[j] = m;
+    }
+    uint32_t w = s0;
+    for (uint32_t i = s0; i < s1; ++i) {
+      if (w > s0 && v.keys[i] == v.keys[w - 1]) {
+        v.masks[w - 1] |= v.masks[i];
+      } else {
+        v.keys[w] = v.keys[i];
+        v.masks[w] = v.masks[i];
+        ++w;
+      }
+    }
+    v.dir[b] = s0 | ((w - s0) << 16);
+  }
+  for (uint32_t i = tid; i < p.bm_words; i += kThreads) v.bm[i] = bm[i];
+  if (tid == 0) *const_cast<GateMeta*>(v.meta) = meta;
+}
+
+// ---------------------------------------------------------------------------
+// Column streaming: one workgroup per (work item, row block).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads, 8) void pairs_gate_kernel(GateLaunch a) {
+  extern __shared__ __align__(16) uint32_t sm[];
+  const GateParams p = a.p;
+  uint32_t* bm = sm;                  // [bm_words]
+  uint32_t* rings = sm + p.bm_words;  // [kWaves][kRing]
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // The G row blocks of a work item are 8 apart in blockIdx, so they land
+  // on one XCD (round-robin dispatch) and stream the same columns through
+  // one L2.
+  const uint32_t b = blockIdx.x, q = b >> 3;
+  const uint32_t rb = q % p.G;
+  const uint32_t seg_id = (q / p.G) * 8 + (b & 7);
+  if (seg_id >= a.n_segs) return;
+  const PairSeg sg = a.segs[seg_id];
+  const uint32_t row0 = sg.I * GG_PAIR_TILE + rb * p.R;
+  if (row0 >= a.n || rb * p.R >= GG_PAIR_TILE) return;
+  const uint32_t c0 = max(sg.J0 * GG_PAIR_TILE, row0 + 1);
+  const uint32_t c1 = min(sg.J1 * GG_PAIR_TILE, a.n);
+  if (c0 >= c1) return;
+  const uint32_t blk = (sg.I - a.tile_row0) * p.G + rb;
+  const BlockView v = block_view(a.tables + (size_t)blk * p.block_bytes, p);
+
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(v.bm);
+    uint4* dst = reinterpret_cast<uint4*>(bm);
+    for (uint32_t i = tid; i < p.bm_words / 4; i += kThreads) dst[i] = src[i];
+  }
+  const GateMeta& gm = *v.meta;
+  const uint64_t maxkey = gm.maxkey;
+  const uint32_t sr = gm.shift_r, sl = gm.shift_l, scale = gm.scale, nrows = gm.nrows;
+  // lane r < R holds row r
+  const uint32_t la = lane < kGateRowsMax ? gm.len[lane] : 0u;
+  const uint64_t xa = lane < kGateRowsMax ? gm.last[lane] : 0ull;
+  const uint32_t bmask = p.bm_words * 32 - 1;
+  const uint32_t nacc = (p.R + 3) / 4;
+  uint32_t* ring = rings + wave * kRing;
+  __syncthreads();
+
+  for (uint32_t j = c0 + wave; j < c1; j += kWaves) {
+    const uint32_t lb = uni32(a.lens[j]);
+    const uint64_t* B = a.sketches + (uint64_t)j * a.stride;
+    uint32_t head = 0, tail = 0;  // wave-uniform
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // byte counters, rows 4q..4q+3
+    bool hits = false;
+    // table walk for up to 64 queued column positions
+    auto drain = [&](uint32_t count) {
+      uint32_t m = 0;
+      if (lane < count) {
+        const uint64_t bv = B[ring[(head + lane) & (kRing - 1)]];
+        if (bv <= maxkey) {
+          const uint32_t d = v.dir[bucket_of(bv, sr, sl, scale)];
+          const uint32_t st = d & 0xFFFFu, n = d >> 16;
+          for (uint32_t k = 0; k < n; ++k) {
+            const uint64_t key = v.keys[st + k];
+            if (key >= bv) {
+              if (key == bv) m = v.masks[st + k];
+              break;
+            }
+          }
+        }
+      }
+      if (__ballot(m != 0)) {
+        hits = true;
+#pragma unroll
+        for (uint32_t c = 0; c < 8; ++c)
+          if (c < nacc) acc[c] += spread4(m >> (4 * c));
+      }
+      head += count;
+    };
+
+    // the gate needs the low 32 bits of each hash only (little-endian u64)
+    const uint32_t* B32 = reinterpret_cast<const uint32_t*>(B);
+    // One chunk of kRounds x 64 column hashes: all loads, then all bitmap
+    // reads, then the tests, so the latencies overlap.  TAIL: the chunk
+    // reaches past the column end; those lanes re-read its last hash and
+    // are masked out of the hit test (branch-free).
+    auto chunk = [&](uint32_t cb, auto tail_tag) {
+      constexpr bool TAIL = decltype(tail_tag)::value;
+      uint32_t lo[kRounds], w[kRounds];
+      const uint32_t* src = B32 + 2 * (cb + lane);
+#pragma unroll
+      for (int t = 0; t < kRounds; ++t)
+        lo[t] = TAIL ? B32[2 * min(cb + t * 64 + lane, lb - 1)] : src[2 * 64 * t];
+#pragma unroll
+      for (int t = 0; t < kRounds; ++t) w[t] = bm[(lo[t] & bmask) >> 5];
+#pragma unroll
+      for (int t = 0; t < kRounds; ++t) {
+        if (TAIL && cb + t * 64 >= lb) break;  // wave-uniform
+        const uint32_t e = cb + t * 64 + lane;
+        uint32_t hit = (w[t] >> (lo[t] & 31)) & 1u;
+        if (TAIL) hit &= (e < lb) ? 1u : 0u;
+        const uint64_t mm = __ballot(hit);
+        if (mm) {
+          if (hit) ring[(tail + lanes_below(mm)) & (kRing - 1)] = e;
+          tail += __popcll(mm);
+          if (tail - head >= 64) drain(64);
+        }
+      }
+    };
+    uint32_t cb = 0;
+    for (; cb + 64 * kRounds <= lb; cb += 64 * kRounds) chunk(cb, std::false_type{});
+    if (cb < lb) chunk(cb, std::true_type{});
+    while (tail != head) drain(min(64u, tail - head));
+
+    if (!hits && !a.zero_passes) continue;  // no row shares a hash with column j
+    // lane r < R: common of pair (row0 + r, j)
+    uint32_t common = 0;
+    if (hits) {
+#pragma unroll
+      for (uint32_t c = 0; c < 8; ++c) {
+        if (c >= nacc) break;
+        const uint32_t s02 = wave_sum(acc[c] & 0x00FF00FFu);         // rows 4c, 4c+2
+        const uint32_t s13 = wave_sum((acc[c] >> 8) & 0x00FF00FFu);  // rows 4c+1, 4c+3
+        if ((lane >> 2) == c) {
+          const uint32_t w = lane & 3;
+          common = (((w & 1) ? s13 : s02) >> (16 * (w >> 1))) & 0xFFFFu;
+        }
+      }
+    }
+    const uint32_t i = row0 + lane;
+    bool cand = false;
+    if (lane < nrows && j > i) {
+      if (la == 0 || lb == 0) cand = a.cmin[0] == 0;  // finch: common 0, total 0
+      else cand = common >= a.sufmin[min(la, lb)];
+    }
+    if (!__ballot(cand)) continue;
+    bool pass = false;
+    uint32_t total = 0;
+    if (cand) {
+      if (la == 0 || lb == 0) {
+        common = 0;
+        pass = true;
+      } else {
+        const uint64_t lastB = B[lb - 1];
+        if (xa <= lastB) total = la + count_le(B, lb, xa) - common;
+        else total = count_le(a.sketches + (uint64_t)i * a.stride, la, lastB) + lb - common;
+        pass = total <= a.tmax && common >= a.cmin[total];
+      }
+    }
+    const uint64_t mk = __ballot(pass);
+    if (mk) {
+      const uint32_t first = __builtin_ctzll(mk);
+      unsigned long long obase = 0;
+      if (lane == first) obase = atomicAdd(a.count, (unsigned long long)__popcll(mk));
+      obase = __shfl(obase, first);
+      if (pass) {
+        const unsigned long long slot = obase + lanes_below(mk);
+        if (slot < a.out_cap) a.out[slot] = gg_pair{i, j, common, total};
+      }
+    }
+  }
+}
+
+uint32_t pow2_at_least(uint64_t x) {
+  uint32_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+}  // namespace
+
+GateParams gate_params(uint32_t s) {
+  GateParams g;
+  g.R = std::min<uint32_t>(kGateRowsMax, std::max<uint32_t>(1, kGateCap / std::max<uint32_t>(s, 1)));
+  g.G = (GG_PAIR_TILE + g.R - 1) / g.R;
+  g.cap = g.R * s;
+  g.nb = std::min<uint32_t>(16384, std::max<uint32_t>(64, pow2_at_least((g.cap + 1) / 2)));
+  g.bm_words = std::min<uint32_t>(1u << 14, std::max<uint32_t>(128, pow2_at_least((uint64_t)g.cap * 16) / 32));
+  const uint64_t bytes = kMetaBytes + 4ull * g.nb + 4ull * g.bm_words + 12ull * g.cap;
+  g.block_bytes = (bytes + 255) & ~255ull;
+  return g;
+}
+
+hipError_t launch_gate_build(const GateBuildLaunch& a, hipStream_t st) {
+  if (a.n_blocks == 0) return hipSuccess;
+  const size_t lds = 4ull * (a.p.nb + a.p.bm_words);
+  hipError_t e = hipFuncSetAttribute((const void*)gate_build_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(gate_build_kernel, dim3(a.n_blocks), dim3(kThreads), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pairs_gate(const GateLaunch& a, hipStream_t st) {
+  if (a.n_segs == 0) return hipSuccess;
+  const size_t lds = 4ull * (a.p.bm_words + (uint64_t)kWaves * kRing);
+  hipError_t e = hipFuncSetAttribute((const void*)pairs_gate_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  const uint64_t blocks = (uint64_t)((a.n_segs + 7) / 8) * 8 * a.p.G;
+  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pairs_gate_kernel, dim3((uint32_t)blocks), dim3(kThreads), lds, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace gg

@@ -49,7 +49,7 @@ def main():
     ms = st["ms"] / st["launches"]
     print(json.dumps({"genomes": N, "pairs_per_launch": st["work"] / st["launches"], "ms": round(ms, 3),
                       "pairs_per_s": st["work"] / st["launches"] / (ms * 1e-3), "found": int(d_cnt.item()),
-                      "kernel": os.environ.get("GALAHGPU_PAIRS_KERNEL", "table")}))
+                      "kernel": os.environ.get("GALAHGPU_PAIRS_KERNEL", "gate")}))
     ctx.close()
 
 

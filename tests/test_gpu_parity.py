@@ -269,16 +269,17 @@ def adversarial_sketches(rng, n, s):
 
 @pytest.mark.parametrize("s", [1000, 2000, 4000, 8000, 10000, 100, 37])
 @pytest.mark.parametrize("min_ani", [0.0, 0.9])
-def test_table_and_merge_kernels_match_oracle(monkeypatch, s, min_ani):
+def test_gate_table_and_merge_kernels_match_oracle(monkeypatch, s, min_ani):
     rng = np.random.default_rng(s)
     n = 150 if s >= 4000 else 260
     sk, lens = adversarial_sketches(rng, n, s)
     o = oracle.pairs(sk, lens.astype(np.int32), np.float32(min_ani))
     exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
     got = {}
-    for kern in ("table", "merge"):
+    for kern in ("gate", "table", "merge"):
         monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", kern)
         with ga.Context(k=21, sketch_size=s) as ctx:
             got[kern] = as_tuples(ctx.pairs(sk, lens, np.float32(min_ani)))
     assert got["merge"] == exp
     assert got["table"] == exp
+    assert got["gate"] == exp
