@@ -404,6 +404,92 @@ void build_segments(std::vector<PairSeg>& segs, uint64_t nb, uint64_t tb, uint64
   }
 }
 
+// Gate kernel (pairs_gate.hip): tables for the tile rows of [tb, te), then
+// the column stream.  Work items are (tile row, row block, column segment)
+// with segments aligned to absolute multiples of kGateSegTiles column
+// tiles, ordered column-segment-major, and dealt to blockIdx so that runs
+// of kGateXcdRun consecutive items land on one XCD (blockIdx mod 8 under
+// round-robin dispatch): the workgroups resident on an XCD then stream the
+// same columns through its L2.
+gg_status pairs_gate(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n, uint64_t nb,
+                     uint64_t tb, uint64_t te, const uint32_t* d_cmin, const uint32_t* d_sufmin, gg_pair* d_out,
+                     uint64_t cap, uint64_t* d_count, uint64_t work, hipStream_t st) {
+  constexpr uint32_t kGateXcdRun = 64;  // ~ workgroups resident per XCD (32 CUs x 2)
+  const GateParams gp = gate_params(c->s);
+  std::vector<PairSeg> items;
+  uint32_t I0 = UINT32_MAX, I1 = 0;
+  {
+    uint64_t t = 0;
+    for (uint64_t I = 0; I < nb && t < te; ++I) {
+      const uint64_t first = t, last = t + (nb - I);
+      const uint64_t lo = std::max(first, tb), hi = std::min(last, te);
+      t = last;
+      if (lo >= hi) continue;
+      I0 = std::min<uint32_t>(I0, (uint32_t)I);
+      I1 = std::max<uint32_t>(I1, (uint32_t)I);
+      uint64_t J = I + (lo - first);
+      const uint64_t Jend = I + (hi - first);
+      while (J < Jend) {
+        const uint64_t Jn = std::min<uint64_t>(Jend, (J / kGateSegTiles + 1) * kGateSegTiles);
+        for (uint32_t rb = 0; rb < gp.G; ++rb)
+          if (I * GG_PAIR_TILE + rb * gp.R < n)
+            items.push_back(PairSeg{(uint32_t)I, (uint32_t)J, (uint32_t)Jn, rb});
+        J = Jn;
+      }
+    }
+  }
+  if (items.empty()) return GG_OK;
+  std::stable_sort(items.begin(), items.end(), [](const PairSeg& x, const PairSeg& y) {
+    return x.J0 / kGateSegTiles < y.J0 / kGateSegTiles;
+  });
+  const uint64_t per = 8ull * kGateXcdRun;
+  const uint64_t n_blocks = (items.size() + per - 1) / per * per;
+  if (n_blocks > 0x7fffffffull) return fail(c, GG_ERR_INVALID_ARG, "too many pair work items");
+  c->seg_host.assign(n_blocks, PairSeg{UINT32_MAX, 0, 0, 0});
+  for (uint64_t k = 0; k < items.size(); ++k) {
+    const uint64_t run = k / kGateXcdRun;
+    const uint64_t b = (run / 8) * per + (k % kGateXcdRun) * 8 + run % 8;
+    c->seg_host[b] = items[k];
+  }
+  PairSeg* d_items;
+  GG_HIP(c, scratch_t(c, "pair_segs", c->seg_host.size(), &d_items));
+  GG_HIP(c, hipMemcpyAsync(d_items, c->seg_host.data(), c->seg_host.size() * sizeof(PairSeg),
+                           hipMemcpyHostToDevice, st));
+  GateBuildLaunch bl;
+  bl.sketches = d_sk;
+  bl.lens = d_lens;
+  bl.n = n;
+  bl.stride = c->s;
+  bl.tile_row0 = I0;
+  bl.n_blocks = (I1 - I0 + 1) * gp.G;
+  bl.p = gp;
+  GG_HIP(c, scratch_t(c, "gate_tables", (size_t)bl.n_blocks * gp.block_bytes, &bl.tables));
+  GG_HIP(c, scratch_t(c, "gate_lo32", (size_t)n * c->s, &bl.lo32));
+  GateLaunch g;
+  g.sketches = d_sk;
+  g.lens = d_lens;
+  g.n = n;
+  g.stride = c->s;
+  g.items = d_items;
+  g.n_items = (uint32_t)n_blocks;
+  g.tile_row0 = I0;
+  g.p = gp;
+  g.tables = bl.tables;
+  g.lo32 = bl.lo32;
+  g.cmin = d_cmin;
+  g.sufmin = d_sufmin;
+  g.tmax = 2 * c->s;
+  g.zero_passes = c->sufmin_host[0] == 0;
+  g.out = d_out;
+  g.out_cap = cap;
+  g.count = (unsigned long long*)d_count;
+  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] {
+    hipError_t e = launch_gate_build(bl, st);
+    return e != hipSuccess ? e : launch_pairs_gate(g, st);
+  }));
+  return GG_OK;
+}
+
 gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
                      uint64_t tb, uint64_t te, float min_ani, gg_pair* d_out, uint64_t cap,
                      uint64_t* d_count, hipStream_t st) {
@@ -431,7 +517,8 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs(a, st); }));
     return GG_OK;
   }
-  build_segments(c->seg_host, nb, tb, te, kern == 0 ? kGateSegTiles : kSegTiles);
+  if (kern == 0) return pairs_gate(c, d_sk, d_lens, n, nb, tb, te, d_cmin, d_sufmin, d_out, cap, d_count, work, st);
+  build_segments(c->seg_host, nb, tb, te, kSegTiles);
   if (c->seg_host.empty()) return GG_OK;
   PairSeg* d_segs;
   GG_HIP(c, scratch_t(c, "pair_segs", c->seg_host.size(), &d_segs));
@@ -453,39 +540,6 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs_table(b, st); }));
     return GG_OK;
   }
-  // gate kernel: tables for the tile rows this range touches, then the stream
-  const GateParams gp = gate_params(c->s);
-  const uint32_t I0 = c->seg_host.front().I, I1 = c->seg_host.back().I;
-  GateBuildLaunch bl;
-  bl.sketches = d_sk;
-  bl.lens = d_lens;
-  bl.n = n;
-  bl.stride = c->s;
-  bl.tile_row0 = I0;
-  bl.n_blocks = (I1 - I0 + 1) * gp.G;
-  bl.p = gp;
-  GG_HIP(c, scratch_t(c, "gate_tables", (size_t)bl.n_blocks * gp.block_bytes, &bl.tables));
-  GateLaunch g;
-  g.sketches = d_sk;
-  g.lens = d_lens;
-  g.n = n;
-  g.stride = c->s;
-  g.segs = d_segs;
-  g.n_segs = (uint32_t)c->seg_host.size();
-  g.tile_row0 = I0;
-  g.p = gp;
-  g.tables = bl.tables;
-  g.cmin = d_cmin;
-  g.sufmin = d_sufmin;
-  g.tmax = 2 * c->s;
-  g.zero_passes = c->sufmin_host[0] == 0;
-  g.out = d_out;
-  g.out_cap = cap;
-  g.count = (unsigned long long*)d_count;
-  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] {
-    hipError_t e = launch_gate_build(bl, st);
-    return e != hipSuccess ? e : launch_pairs_gate(g, st);
-  }));
   return GG_OK;
 }
 

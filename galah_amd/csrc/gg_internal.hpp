@@ -118,17 +118,19 @@ struct GateBuildLaunch {
   uint32_t n_blocks;   // tables to build
   GateParams p;
   uint8_t* tables;
+  uint32_t* lo32;      // [n * stride]: low words of rows >= tile_row0 * GG_PAIR_TILE
 };
 struct GateLaunch {
   const uint64_t* sketches;
   const uint32_t* lens;
   uint32_t n;
   uint32_t stride;
-  const PairSeg* segs;
-  uint32_t n_segs;
+  const PairSeg* items;  // per blockIdx: {tile row, J0, J1, row block}; I = ~0: idle
+  uint32_t n_items;
   uint32_t tile_row0;
   GateParams p;
   const uint8_t* tables;
+  const uint32_t* lo32;
   const uint32_t* cmin;    // [tmax + 1]
   const uint32_t* sufmin;  // [tmax + 1] min(cmin[t..tmax])
   uint32_t tmax;

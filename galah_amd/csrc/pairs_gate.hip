@@ -6,17 +6,25 @@
 // VALU instructions instead of a merge:
 //
 //  * Row blocks.  The R (<= 32) rows of a row block share one table, built
-//    once per launch by gate_build_kernel into HBM: the block's distinct
-//    keys in value buckets (dir = start | count << 16), a 32-bit row mask
-//    per key, and a gate bitmap with bit (key mod 2^b) set for every key.
-//    R * s <= 32768 keys, so at s = 1000 a row block holds 32 rows.
+//    once per launch by gate_build_kernel into HBM: the block's keys in
+//    value buckets (dir = start | count << 16; a key shared by several
+//    rows appears once per row, buckets unsorted), the row of each entry
+//    as a one-bit mask, and a gate bitmap with bit (key mod 2^b) set for
+//    every key.  R * s <= 32768 keys, so at s = 1000 a row block holds 32
+//    rows.
 //  * Gate.  pairs_gate_kernel copies the row block's bitmap (64 KiB at
-//    s = 1000) into LDS and streams column sketches through it: per column
-//    hash one LDS read and a bit test.  With 32k keys in 2^19 bits ~6% of
-//    the hashes of an unrelated column pass the gate.  Passing hashes are
-//    queued per wave (LDS ring of column positions) and resolved 64 at a
-//    time by a walk of the bucket in HBM/L2.  One column hash therefore
-//    serves all R rows, and the table walk runs only for gate hits.
+//    s = 1000) into LDS and streams the low words of column sketches (a
+//    compact copy made per launch) through it: per column hash one LDS read
+//    and a bit test.  With 32k keys in 2^19 bits ~6% of the hashes of an
+//    unrelated column pass the gate.  Passing hashes are queued per wave
+//    (LDS ring of column positions) and resolved 64 at a time by a walk of
+//    the bucket in HBM/L2 that ORs the masks of the equal keys.  One column
+//    hash therefore serves all R rows, and the table walk runs only for
+//    gate hits.
+//  * Work order.  Work items (row block x column segment) are dealt to
+//    blockIdx column-segment-major in runs of 64 per XCD (the host does
+//    it: pairs_gate in api.cpp), so the workgroups resident on an XCD
+//    stream the same columns through its L2.
 //  * Totals.  A pair can pass only if common >= min(cmin[t], t >= min(|A|,
 //    |B|)) (the first exhaustion leaves total >= |A| or >= |B|), so the
 //    ranks that finch's total needs are computed (binary searches) only for
@@ -174,39 +182,26 @@ __global__ __launch_bounds__(kThreads) void gate_build_kernel(GateBuildLaunch a)
     v.masks[slot] = 1u << r;
   }
   __syncthreads();
-  // pass 3: sort each bucket, merge keys shared by several rows
+  // buckets stay unsorted: a lookup compares every entry of its bucket
+  // (~2 at R * s = 32k keys in 16k buckets) and ORs the masks of equal keys
   for (uint32_t b = tid; b < p.nb; b += kThreads) {
     const uint32_t s0 = b ? cnt[b - 1] : 0u, s1 = cnt[b];
-    for (uint32_t i = s0 + 1; i < s1; ++i) {
-      const uint64_t k = v.keys[i];
-      const uint32_t m = v.masks[i];
-      uint32_t j = i;
-      while (j > s0 && v.keys[j - 1] > k) {
-        v.keys[j] = v.keys[j - 1];
-        v.masks[j] = v.masks[j - 1];
-        --j;
-      }
-      v.keys[j] = k;
-      v.masks[j] = m;
-    }
-    uint32_t w = s0;
-    for (uint32_t i = s0; i < s1; ++i) {
-      if (w > s0 && v.keys[i] == v.keys[w - 1]) {
-        v.masks[w - 1] |= v.masks[i];
-      } else {
-        v.keys[w] = v.keys[i];
-        v.masks[w] = v.masks[i];
-        ++w;
-      }
-    }
-    v.dir[b] = s0 | ((w - s0) << 16);
+    v.dir[b] = s0 | ((s1 - s0) << 16);
   }
   for (uint32_t i = tid; i < p.bm_words; i += kThreads) v.bm[i] = bm[i];
   if (tid == 0) *const_cast<GateMeta*>(v.meta) = meta;
 }
 
+// Low 32 bits of every hash of rows [row0, n): the gate reads 4 B per
+// column hash instead of 8.
+__global__ __launch_bounds__(256) void gate_lo32_kernel(const uint64_t* __restrict__ sk, uint32_t* __restrict__ lo,
+                                                        uint64_t begin, uint64_t end) {
+  for (uint64_t i = begin + (uint64_t)blockIdx.x * 256 + threadIdx.x; i < end; i += (uint64_t)gridDim.x * 256)
+    lo[i] = (uint32_t)sk[i];
+}
+
 // ---------------------------------------------------------------------------
-// Column streaming: one workgroup per (work item, row block).
+// Column streaming: one workgroup per (row block, column segment).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kThreads, 8) void pairs_gate_kernel(GateLaunch a) {
   extern __shared__ __align__(16) uint32_t sm[];
@@ -215,14 +210,11 @@ __global__ __launch_bounds__(kThreads, 8) void pairs_gate_kernel(GateLaunch a) {
   uint32_t* rings = sm + p.bm_words;  // [kWaves][kRing]
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  // The G row blocks of a work item are 8 apart in blockIdx, so they land
-  // on one XCD (round-robin dispatch) and stream the same columns through
-  // one L2.
-  const uint32_t b = blockIdx.x, q = b >> 3;
-  const uint32_t rb = q % p.G;
-  const uint32_t seg_id = (q / p.G) * 8 + (b & 7);
-  if (seg_id >= a.n_segs) return;
-  const PairSeg sg = a.segs[seg_id];
+  // work item of this workgroup (the host orders items so that the
+  // workgroups resident on one XCD share a column segment)
+  const PairSeg sg = a.items[blockIdx.x];
+  if (sg.I == UINT32_MAX) return;
+  const uint32_t rb = sg.pad;
   const uint32_t row0 = sg.I * GG_PAIR_TILE + rb * p.R;
   if (row0 >= a.n || rb * p.R >= GG_PAIR_TILE) return;
   const uint32_t c0 = max(sg.J0 * GG_PAIR_TILE, row0 + 1);
@@ -261,13 +253,8 @@ __global__ __launch_bounds__(kThreads, 8) void pairs_gate_kernel(GateLaunch a) {
         if (bv <= maxkey) {
           const uint32_t d = v.dir[bucket_of(bv, sr, sl, scale)];
           const uint32_t st = d & 0xFFFFu, n = d >> 16;
-          for (uint32_t k = 0; k < n; ++k) {
-            const uint64_t key = v.keys[st + k];
-            if (key >= bv) {
-              if (key == bv) m = v.masks[st + k];
-              break;
-            }
-          }
+          for (uint32_t k = 0; k < n; ++k)
+            if (v.keys[st + k] == bv) m |= v.masks[st + k];
         }
       }
       if (__ballot(m != 0)) {
@@ -279,8 +266,8 @@ __global__ __launch_bounds__(kThreads, 8) void pairs_gate_kernel(GateLaunch a) {
       head += count;
     };
 
-    // the gate needs the low 32 bits of each hash only (little-endian u64)
-    const uint32_t* B32 = reinterpret_cast<const uint32_t*>(B);
+    // the gate needs the low 32 bits of each hash only
+    const uint32_t* B32 = a.lo32 + (uint64_t)j * a.stride;
     // One chunk of kRounds x 64 column hashes: all loads, then all bitmap
     // reads, then the tests, so the latencies overlap.  TAIL: the chunk
     // reaches past the column end; those lanes re-read its last hash and
@@ -288,10 +275,10 @@ __global__ __launch_bounds__(kThreads, 8) void pairs_gate_kernel(GateLaunch a) {
     auto chunk = [&](uint32_t cb, auto tail_tag) {
       constexpr bool TAIL = decltype(tail_tag)::value;
       uint32_t lo[kRounds], w[kRounds];
-      const uint32_t* src = B32 + 2 * (cb + lane);
+      const uint32_t* src = B32 + cb + lane;
 #pragma unroll
       for (int t = 0; t < kRounds; ++t)
-        lo[t] = TAIL ? B32[2 * min(cb + t * 64 + lane, lb - 1)] : src[2 * 64 * t];
+        lo[t] = TAIL ? B32[min(cb + t * 64 + lane, lb - 1)] : src[64 * t];
 #pragma unroll
       for (int t = 0; t < kRounds; ++t) w[t] = bm[(lo[t] & bmask) >> 5];
 #pragma unroll
@@ -384,6 +371,13 @@ GateParams gate_params(uint32_t s) {
 
 hipError_t launch_gate_build(const GateBuildLaunch& a, hipStream_t st) {
   if (a.n_blocks == 0) return hipSuccess;
+  {
+    const uint64_t begin = (uint64_t)a.tile_row0 * GG_PAIR_TILE * a.stride, end = (uint64_t)a.n * a.stride;
+    if (begin < end) {
+      const uint64_t blocks = std::min<uint64_t>(8192, (end - begin + 255) / 256);
+      hipLaunchKernelGGL(gate_lo32_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, a.sketches, a.lo32, begin, end);
+    }
+  }
   const size_t lds = 4ull * (a.p.nb + a.p.bm_words);
   hipError_t e = hipFuncSetAttribute((const void*)gate_build_kernel,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -393,14 +387,12 @@ hipError_t launch_gate_build(const GateBuildLaunch& a, hipStream_t st) {
 }
 
 hipError_t launch_pairs_gate(const GateLaunch& a, hipStream_t st) {
-  if (a.n_segs == 0) return hipSuccess;
+  if (a.n_items == 0) return hipSuccess;
   const size_t lds = 4ull * (a.p.bm_words + (uint64_t)kWaves * kRing);
   hipError_t e = hipFuncSetAttribute((const void*)pairs_gate_kernel,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  const uint64_t blocks = (uint64_t)((a.n_segs + 7) / 8) * 8 * a.p.G;
-  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pairs_gate_kernel, dim3((uint32_t)blocks), dim3(kThreads), lds, st, a);
+  hipLaunchKernelGGL(pairs_gate_kernel, dim3(a.n_items), dim3(kThreads), lds, st, a);
   return hipGetLastError();
 }
 
