@@ -44,8 +44,15 @@ N_SIMD = 256 * 4       # 256 CUs x 4 SIMDs
 K1_CYCLES_PER_VALU = 4
 K1_VALU_PER_KMER = 3.667e10 / (29999800000 / 64)
 K1_PEAK_GKMER = N_SIMD * CLK_GHZ * 64 / (K1_CYCLES_PER_VALU * K1_VALU_PER_KMER)  # Gkmer/s
-# K2 (pairs): SURVEY 8(d) prices a pair at the reference merge's bytes,
-# 8 B x (|A| + |B|), against LDS bandwidth: 256 B/clk/CU for 64-bit reads.
+# K2 (pairs: gate_lo32 + gate_build + pairs_gate kernels) is also priced
+# against VALU issue: SQ_INSTS_VALU of the three kernels per evaluated pair
+# from the PMC pass over the C3 launch (profiles/r01_pmc_k1_k2gate.txt).  It
+# runs well under that ceiling: the queued table walks wait on L2/HBM.
+K2_VALU_PER_PAIR = (5.706e8 + 3.114e7 + 7.888e5) / 49995000
+K2_PEAK_GPAIR = N_SIMD * CLK_GHZ / (K1_CYCLES_PER_VALU * K2_VALU_PER_PAIR)  # Gpair/s
+K2_PMC_HBM_BYTES_C3 = (5.617e6 + 7.658e4 + 3.907e4) * 1024 * 2
+# SURVEY 8(d)'s merge pricing (8 B x (|A| + |B|) per pair against 256 B/clk/CU
+# of LDS), reported for reference: the gate kernel does not merge.
 LDS_PEAK_GBS = 256 * 256 * CLK_GHZ
 # HBM bytes per K1 launch on this workload from the PMC pass (FETCH_SIZE x 2,
 # the gfx950 correction of MI355X_MICROARCH.md), profiles/r01_pmc_sketch.txt
@@ -241,16 +248,39 @@ def main():
           "note": ("VALU-issue ceiling: %.1f VALU per wave64 k-mer (PMC) x %d cycles each, 1024 SIMDs at "
                    "%.1f GHz; input is 0.25 B/k-mer, so the HBM fraction is small by design"
                    % (K1_VALU_PER_KMER, K1_CYCLES_PER_VALU, CLK_GHZ))}
-    k2 = {"kernel": "pairs_table_kernel<8>", "bound": "lds", "unit": "GB/s",
-          "achieved": pairs_per_launch * 16.0 * s / (pr_ms * 1e-3) / 1e9, "peak": LDS_PEAK_GBS,
-          "avg_ms": pr_ms, "work_per_launch": pairs_per_launch, "traffic": None,
-          "note": "SURVEY 8(d) pricing: 8 B x (|A|+|B|) = 16 KB per pair at s=1000 vs 256 B/clk/CU LDS"}
+    c3 = N == 10000 and glen == 3000000 and world == 1
+    k2 = {"kernel": "pairs_gate_kernel (+ gate_build_kernel, gate_lo32_kernel)", "bound": "valu", "unit": "Gpair/s",
+          "achieved": pairs_per_launch / (pr_ms * 1e-3) / 1e9, "peak": K2_PEAK_GPAIR,
+          "avg_ms": pr_ms, "work_per_launch": pairs_per_launch,
+          "traffic": (K2_PMC_HBM_BYTES_C3 if c3 else None), "valu_per_pair": K2_VALU_PER_PAIR,
+          "merge_priced_GBps": pairs_per_launch * 16.0 * s / (pr_ms * 1e-3) / 1e9, "lds_peak_GBps": LDS_PEAK_GBS,
+          "note": ("VALU-issue ceiling: %.2f VALU per pair (PMC, all three kernels) x %d cycles, 1024 SIMDs at %.1f GHz; "
+                   "latency of the queued table walks keeps it below; merge_priced_GBps = SURVEY 8(d) pricing "
+                   "(16 KB per pair at s=1000) for reference" % (K2_VALU_PER_PAIR, K1_CYCLES_PER_VALU, CLK_GHZ))}
     dom = k1 if sk_ms * kst["sketch"]["launches"] >= pr_ms * kst["pairs"]["launches"] else k2
     roof = {"bound": dom["bound"], "achieved": round(dom["achieved"], 3), "peak": round(dom["peak"], 3),
             "unit": dom["unit"], "frac": round(dom["achieved"] / dom["peak"], 4), "traffic": dom["traffic"],
             "kernel": dom["kernel"], "avg_launch_ms": round(dom["avg_ms"], 4), "note": dom["note"],
             "kernels": [{kk: (round(v, 5) if isinstance(v, float) else v) for kk, v in x.items()}
                         for x in (k1, k2)]}
+
+    # SURVEY 8(f) row 1, downstream of the timed step: single-linkage
+    # preclusters of the passing pairs (host C++, union-find), and
+    # transform_ids for every precluster at once
+    downstream = None
+    if rank == 0 and world == 1:
+        pairs_h = _host.numpy().view(np.uint32).reshape(-1, 4)
+        pa = np.zeros(len(pairs_h), dtype=ga.PAIR_DTYPE)
+        for k_, f_ in enumerate(("i", "j", "common", "total")):
+            pa[f_] = pairs_h[:, k_]
+        t0 = time.perf_counter()
+        members, offsets = ga.partition_preclusters(N, pa)
+        t_part = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        ga.precluster_pairs(N, pa, members, offsets)
+        t_tr = time.perf_counter() - t0
+        downstream = {"partition_preclusters_ms": round(t_part * 1e3, 3), "precluster_pairs_ms": round(t_tr * 1e3, 3),
+                      "preclusters": int(len(offsets) - 1), "largest": int(np.diff(offsets).max()) if N else 0}
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -276,6 +306,7 @@ def main():
             "pairs_found": int(tsum[4]) if world > 1 else found,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "downstream": downstream,
         }
         print(json.dumps(line), flush=True)
     ctx.close()
