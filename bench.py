@@ -64,19 +64,27 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--genomes", type=int, default=10000)
-    ap.add_argument("--genome-len", type=int, default=3000000)
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"],
+                    help="c3 (default, the headline): 10k x 3 Mbp, s=1000; c2: 1k x 3 Mbp; "
+                         "c5: 10k genomes of 0.5-12 Mbp (log-uniform) with N runs, s=10000")
+    ap.add_argument("--genomes", type=int, default=None)
+    ap.add_argument("--genome-len", type=int, default=3000000, help="c2/c3 genome length")
     ap.add_argument("--cluster", type=int, default=10)
     ap.add_argument("--max-sub", type=float, default=0.07)
     ap.add_argument("--min-ani", type=float, default=95.0, help="--precluster-ani (percent)")
-    ap.add_argument("--sketch", type=int, default=1000)
+    ap.add_argument("--sketch", type=int, default=None)
     ap.add_argument("--k", type=int, default=21)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=20.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo stages collectives through host memory (testing ranks that share one GPU)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.genomes is None:
+        a.genomes = 1000 if a.config == "c2" else 10000
+    if a.sketch is None:
+        a.sketch = 10000 if a.config == "c5" else 1000
+    return a
 
 
 def cpu_baseline(words_dev, runs, glen, sk_all, lens_all, k, s, min_ani, n_total, budget_s):
@@ -151,8 +159,15 @@ def main():
     sh = stream.cuda_stream
 
     # inputs resident in HBM: this rank's genome shard, 2-bit packed
-    d_words = torch.empty(n_loc * glen // 16, dtype=torch.int32, device="cuda")
-    runs = ctx.synth_device(n_loc, glen, a.cluster, a.max_sub, a.seed, d_words, stream=sh, first_genome=g0)
+    if a.config == "c5":
+        lens_bp = ga.synth_mixed_lengths(n_loc, 500000, 12000000, a.cluster, 7, first_genome=g0)
+        d_words = torch.empty(int(lens_bp.sum()) // 16, dtype=torch.int32, device="cuda")
+        runs = ctx.synth_mixed_device(lens_bp, a.cluster, a.max_sub, 1e-4, 8, d_words, stream=sh, first_genome=g0)
+        bases_loc = int(lens_bp.sum())
+    else:
+        d_words = torch.empty(n_loc * glen // 16, dtype=torch.int32, device="cuda")
+        runs = ctx.synth_device(n_loc, glen, a.cluster, a.max_sub, a.seed, d_words, stream=sh, first_genome=g0)
+        bases_loc = n_loc * glen
     d_sk_loc = torch.empty((n_loc, s), dtype=torch.int64, device="cuda")
     d_len_loc = torch.empty(n_loc, dtype=torch.int32, device="cuda")
     if world > 1:
@@ -217,7 +232,7 @@ def main():
     kst = {name: ctx.timing_read(kid) for name, kid in
            (("sketch", ga.KERNEL_SKETCH), ("finalize", ga.KERNEL_FINALIZE), ("pairs", ga.KERNEL_PAIRS))}
     ctx.timing_enable(False)
-    t = torch.tensor([elapsed, phase["sketch"], phase["pairs"], phase["gather"], float(found)],
+    t = torch.tensor([elapsed, phase["sketch"], phase["pairs"], phase["gather"], float(found), float(bases_loc)],
                      dtype=torch.float64, device="cuda")
     if world > 1:
         if gloo:
@@ -232,7 +247,7 @@ def main():
     ms_step = elapsed_max / a.steps * 1e3
     npairs = N * (N - 1) // 2
     value = npairs / (elapsed_max / a.steps)
-    total_bases = N * glen
+    total_bases = float(tsum[5])
 
     # roofline of the dominant kernel, from this rank's per-launch events
     sk_ms = kst["sketch"]["ms"] / max(1, kst["sketch"]["launches"])
@@ -243,12 +258,13 @@ def main():
     k1 = {"kernel": "sketch_candidates_kernel<21>", "bound": "valu", "unit": "Gkmer/s",
           "achieved": k1_gkmer, "peak": K1_PEAK_GKMER, "avg_ms": sk_ms, "work_per_launch": kmers_per_launch,
           "hbm_achieved_GBps": kmers_per_launch * 0.25 / (sk_ms * 1e-3) / 1e9, "hbm_peak_GBps": HBM_PEAK_GBS,
-          "traffic": (K1_PMC_HBM_BYTES_C3 if (N == 10000 and glen == 3000000 and world == 1) else None),
+          "traffic": (K1_PMC_HBM_BYTES_C3 if (a.config == "c3" and N == 10000 and glen == 3000000 and world == 1)
+                      else None),
           "valu_per_kmer": K1_VALU_PER_KMER,
           "note": ("VALU-issue ceiling: %.1f VALU per wave64 k-mer (PMC) x %d cycles each, 1024 SIMDs at "
                    "%.1f GHz; input is 0.25 B/k-mer, so the HBM fraction is small by design"
                    % (K1_VALU_PER_KMER, K1_CYCLES_PER_VALU, CLK_GHZ))}
-    c3 = N == 10000 and glen == 3000000 and world == 1
+    c3 = a.config == "c3" and N == 10000 and glen == 3000000 and world == 1 and s == 1000
     k2 = {"kernel": "pairs_gate_kernel (+ gate_build_kernel, gate_lo32_kernel)", "bound": "valu", "unit": "Gpair/s",
           "achieved": pairs_per_launch / (pr_ms * 1e-3) / 1e9, "peak": K2_PEAK_GPAIR,
           "avg_ms": pr_ms, "work_per_launch": pairs_per_launch,
@@ -283,7 +299,7 @@ def main():
                       "preclusters": int(len(offsets) - 1), "largest": int(np.diff(offsets).max()) if N else 0}
 
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.config != "c5":
         sk_h = d_sk.cpu().numpy().view(np.uint64)
         ln_h = d_len.cpu().numpy().view(np.uint32)
         cpu = cpu_baseline(d_words, runs, glen, sk_h, ln_h, a.k, s, min_ani, N, a.cpu_budget_s)
@@ -295,9 +311,12 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "u64",
             "data": "synthetic clustered genomes generated on device (no network)",
-            "config": {"workload": "C3: %d synthetic genomes x %d bp, clusters of %d, sub rate U(0,%.2f), "
-                                   "k=%d, s=%d, min_ani=%s" % (N, glen, a.cluster, a.max_sub, a.k, s, min_ani),
-                       "genomes": N, "genome_len": glen, "sketch_size": s, "k": a.k,
+            "config": {"workload": (("C5: %d synthetic genomes of 0.5-12 Mbp (log-uniform, %.0f bp total) with N runs"
+                                     % (N, total_bases)) if a.config == "c5" else
+                                    ("%s: %d synthetic genomes x %d bp" % (a.config.upper(), N, glen)))
+                                   + ", clusters of %d, sub rate U(0,%.2f), k=%d, s=%d, min_ani=%s"
+                                   % (a.cluster, a.max_sub, a.k, s, min_ani),
+                       "genomes": N, "genome_len": (None if a.config == "c5" else glen), "sketch_size": s, "k": a.k,
                        "min_ani": float(min_ani), "parallelism": "dp%d" % world},
             "sketch_gbases_per_s": round(total_bases / (float(tmax[1]) / a.steps * 1e-3) / 1e9, 3),
             "pairs_kernel_pairs_per_s": round(npairs / (float(tmax[2]) / a.steps * 1e-3), 1),

@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "gg_pair_tiles", "gg_pair_partition", "gg_pairs", "gg_pairs_device",
     "gg_precluster_files", "gg_ani_f64", "gg_ani_f32", "gg_parse_percentage",
     "gg_free", "gg_synth_clustered_device", "gg_timing_enable", "gg_timing_read",
-    "gg_partition_preclusters", "gg_precluster_pairs",
+    "gg_partition_preclusters", "gg_precluster_pairs", "gg_synth_mixed_lengths", "gg_synth_mixed_device",
 )
 
 GG_OK = 0
@@ -116,6 +116,9 @@ _sig("gg_ani_f32", ctypes.c_float, [_u32, _u32, _i32])
 _sig("gg_parse_percentage", _i32, [ctypes.c_float, ctypes.POINTER(ctypes.c_float)])
 _sig("gg_free", None, [_vp])
 _sig("gg_synth_clustered_device", _i32, [_vp, _u32, _u32, _u32, _u32, ctypes.c_float, _u64, _vp, _vp, _vp])
+_sig("gg_synth_mixed_lengths", _i32, [_u32, _u32, _u32, _u32, _u32, _u64, _vp])
+_sig("gg_synth_mixed_device", _i32, [_vp, _u32, _u32, _vp, _u32, ctypes.c_float, ctypes.c_double, _u64, _vp, _vp,
+                                     _u64, ctypes.POINTER(_u64), _vp])
 _sig("gg_partition_preclusters", _i32, [_u32, _vp, _u64, _vp, _vp, ctypes.POINTER(_u32)])
 _sig("gg_precluster_pairs", _i32, [_u32, _vp, _u64, _vp, _vp, _u32, _vp, _vp])
 
@@ -187,6 +190,15 @@ def _as_pairs(pairs):
         if pairs.dtype.names and f in pairs.dtype.names:
             p[f] = pairs[f]
     return p
+
+
+def synth_mixed_lengths(n_genomes, min_len, max_len, cluster_size, seed, first_genome=0):
+    """Config C5 genome lengths: log-uniform in [min_len, max_len] per cluster."""
+    lens = np.zeros(max(n_genomes, 1), np.uint32)
+    st = _L.gg_synth_mixed_lengths(first_genome, n_genomes, min_len, max_len, cluster_size, seed, _ptr(lens))
+    if st != GG_OK:
+        raise _thread_err(st)
+    return lens[:n_genomes]
 
 
 def partition_preclusters(n_genomes, pairs):
@@ -395,6 +407,26 @@ class Context:
                                 None if stream is None else stream)
         if st != GG_OK:
             raise self._err(st)
+
+    def synth_mixed_device(self, lens, cluster_size, max_sub_rate, n_run_rate, seed, d_words, stream=None,
+                           first_genome=0):
+        """Config C5: genomes of lengths `lens` (see synth_mixed_lengths) with
+        N runs; -> the host run table (RUN_DTYPE)."""
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        cap = max(1024, int(lens.sum() * max(n_run_rate, 1e-6) * 2) + 4 * len(lens))
+        for _ in range(2):
+            runs = np.zeros(cap, dtype=RUN_DTYPE)
+            nr = _u64()
+            st = _L.gg_synth_mixed_device(self._c, first_genome, len(lens), _ptr(lens), cluster_size,
+                                          ctypes.c_float(max_sub_rate), ctypes.c_double(n_run_rate), seed,
+                                          _dev_ptr(d_words), _ptr(runs), cap, ctypes.byref(nr),
+                                          None if stream is None else stream)
+            if st == GG_OK:
+                return runs[:nr.value]
+            if st != 8:
+                raise self._err(st)
+            cap = nr.value
+        raise self._err(st)
 
     def synth_device(self, n_genomes, genome_len, cluster_size, max_sub_rate, seed, d_words, stream=None,
                      first_genome=0):

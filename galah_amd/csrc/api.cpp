@@ -944,4 +944,72 @@ gg_status gg_synth_clustered_device(gg_ctx* ctx, uint32_t first_genome, uint32_t
   return GG_OK;
 }
 
+static uint64_t splitmix_host(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+gg_status gg_synth_mixed_lengths(uint32_t first_genome, uint32_t n_genomes, uint32_t min_len, uint32_t max_len,
+                                 uint32_t cluster_size, uint64_t seed, uint32_t* lens) {
+  if ((n_genomes && !lens) || cluster_size == 0 || min_len < 64 || max_len < min_len)
+    return fail(nullptr, GG_ERR_INVALID_ARG, "gg_synth_mixed_lengths: bad arguments");
+  const double lo = std::log((double)min_len), hi = std::log((double)max_len);
+  for (uint32_t i = 0; i < n_genomes; ++i) {
+    const uint32_t cl = (first_genome + i) / cluster_size;
+    const double u = (double)(splitmix_host(seed * 0x9E3779B97F4A7C15ull + cl) >> 11) * (1.0 / 9007199254740992.0);
+    const uint32_t L = (uint32_t)std::exp(lo + u * (hi - lo));
+    lens[i] = std::max<uint32_t>(64, std::min(max_len, L)) / 16 * 16;
+  }
+  return GG_OK;
+}
+
+gg_status gg_synth_mixed_device(gg_ctx* ctx, uint32_t first_genome, uint32_t n_genomes, const uint32_t* lens,
+                                uint32_t cluster_size, float max_sub_rate, double n_run_rate, uint64_t seed,
+                                uint32_t* d_words, gg_run* runs, uint64_t runs_cap, uint64_t* n_runs, void* stream) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (!d_words || !lens || !n_runs || cluster_size == 0 || !(n_run_rate >= 0.0 && n_run_rate < 1.0))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_synth_mixed_device: bad arguments");
+  for (uint32_t g = 0; g < n_genomes; ++g)
+    if (lens[g] % 16 || lens[g] == 0) return fail(ctx, GG_ERR_INVALID_ARG, "genome lengths must be positive multiples of 16");
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<uint64_t> woff(n_genomes + 1, 0);
+  uint64_t max_words = 0;
+  for (uint32_t g = 0; g < n_genomes; ++g) {
+    woff[g + 1] = woff[g] + lens[g] / 16;
+    max_words = std::max<uint64_t>(max_words, lens[g] / 16);
+  }
+  uint64_t* d_woff;
+  GG_HIP(ctx, scratch_t(ctx, "synth_woff", n_genomes + 1, &d_woff));
+  GG_HIP(ctx, hipMemcpyAsync(d_woff, woff.data(), (n_genomes + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  GG_HIP(ctx, launch_synth_mixed(first_genome, n_genomes, d_woff, max_words, cluster_size, max_sub_rate, seed, d_words, st));
+  // N runs: geometric gaps (start probability n_run_rate per base), 1-64 bases
+  uint64_t nr = 0;
+  const uint32_t k = (uint32_t)ctx->k;
+  for (uint32_t g = 0; g < n_genomes; ++g) {
+    uint64_t state = splitmix_host(seed ^ 0x4E4E4E4Eull ^ ((uint64_t)(first_genome + g) << 20));
+    auto next = [&]() { state = splitmix_host(state); return state; };
+    const uint64_t L = lens[g], base0 = woff[g] * 16;
+    uint64_t pos = 0;
+    while (pos < L) {
+      uint64_t run_end = L;
+      if (n_run_rate > 0.0) {
+        const double u = ((double)(next() >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+        const double gap = std::floor(std::log(u) / std::log1p(-n_run_rate));
+        if (gap < (double)(L - pos)) run_end = pos + (uint64_t)gap;
+      }
+      if (run_end - pos >= k) {
+        if (nr < runs_cap && runs) runs[nr] = gg_run{g, (uint32_t)(run_end - pos), base0 + pos};
+        ++nr;
+      }
+      pos = run_end + (run_end < L ? 1 + next() % 64 : 0);
+    }
+  }
+  *n_runs = nr;
+  if (nr > runs_cap) return fail(ctx, GG_ERR_OUTPUT_FULL, "run buffer too small");
+  return GG_OK;
+}
+
 }  // extern "C"

@@ -147,6 +147,10 @@ hipError_t launch_synth(uint32_t first_genome, uint32_t n_genomes, uint32_t geno
                         uint32_t cluster_size, float max_sub_rate,
                         uint64_t seed, uint32_t* words, hipStream_t st);
 
+hipError_t launch_synth_mixed(uint32_t first_genome, uint32_t n_genomes, const uint64_t* d_woff,
+                              uint64_t max_words, uint32_t cluster_size, float max_sub_rate, uint64_t seed,
+                              uint32_t* words, hipStream_t st);
+
 // api.cpp helpers used by pack.cpp
 void set_thread_error(const std::string& msg);
 

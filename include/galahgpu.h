@@ -241,6 +241,24 @@ gg_status gg_synth_clustered_device(gg_ctx* ctx, uint32_t first_genome, uint32_t
                                     uint32_t* d_words, gg_run* runs,
                                     void* stream);
 
+/* Config C5: mixed genome lengths and N runs.  Host side,
+ * deterministic in the arguments: lens[g] for genomes [first_genome,
+ * first_genome + n_genomes) -- log-uniform in [min_len, max_len], rounded
+ * down to a multiple of 16, shared by the members of a cluster. */
+gg_status gg_synth_mixed_lengths(uint32_t first_genome, uint32_t n_genomes, uint32_t min_len,
+                                 uint32_t max_len, uint32_t cluster_size, uint64_t seed,
+                                 uint32_t* lens);
+/* Writes the genomes (local genome g at word offset sum(lens[<g])/16) and
+ * the ACGT runs between N runs: an N run starts at a base with probability
+ * n_run_rate and is 1-64 bases long (those bases are excluded from every
+ * run, as needletail's non-ACGT bytes break k-mers); runs shorter than k are
+ * dropped.  runs has room for runs_cap entries; *n_runs receives the count
+ * (GG_ERR_OUTPUT_FULL when it exceeds runs_cap). */
+gg_status gg_synth_mixed_device(gg_ctx* ctx, uint32_t first_genome, uint32_t n_genomes,
+                                const uint32_t* lens, uint32_t cluster_size, float max_sub_rate,
+                                double n_run_rate, uint64_t seed, uint32_t* d_words, gg_run* runs,
+                                uint64_t runs_cap, uint64_t* n_runs, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

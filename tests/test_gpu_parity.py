@@ -283,3 +283,55 @@ def test_gate_table_and_merge_kernels_match_oracle(monkeypatch, s, min_ani):
     assert got["merge"] == exp
     assert got["table"] == exp
     assert got["gate"] == exp
+
+
+def test_c5_mixed_sizes_s10000(gpu_ctx, monkeypatch):
+    """Config C5 shape: s = 10000, genome lengths log-uniform in
+    0.5-12 Mbp, N runs breaking k-mers.  Oracle spot checks on sketches (the
+    smallest and largest genome and one more) and on 150 pairs; the gate,
+    table-free merge and oracle agree on a 200-genome subset; pairs stay
+    inside clusters."""
+    torch = torch_dev()
+    n, s, cl = 3000, 10000, 10
+    lens_bp = ga.synth_mixed_lengths(n, 500000, 12000000, cl, 7)
+    assert lens_bp.min() >= 500000 - 16 and lens_bp.max() <= 12000000
+    d_words = torch.empty(int(lens_bp.sum()) // 16, dtype=torch.int32, device="cuda")
+    with ga.Context(k=21, sketch_size=s) as ctx:
+        runs = ctx.synth_mixed_device(lens_bp, cl, 0.07, 1e-4, 8, d_words)
+        torch.cuda.synchronize()
+        assert len(runs) > n  # N runs split the genomes
+        d_sk = torch.zeros((n, s), dtype=torch.int64, device="cuda")
+        d_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ctx.sketch_device(d_words, runs, n, d_sk, d_len)
+        torch.cuda.synchronize()
+        sk = d_sk.cpu().numpy().view(np.uint64)
+        ln = d_len.cpu().numpy().view(np.uint32)
+        assert (ln == s).all()
+        assert (np.diff(sk, axis=1) > 0).all()
+        words = d_words.cpu().numpy().view(np.uint32)
+        for g in (int(np.argmin(lens_bp)), int(np.argmax(lens_bp)), 1234):
+            recs = [unpack_run(words, int(r["base"]), int(r["len"])) for r in runs[runs["genome"] == g]]
+            exp = oracle.sketch_records(recs, s=s)
+            assert (sk[g] == exp).all(), g
+        thr = np.float32(0.95)
+        p = ctx.pairs(sk, ln, thr)
+        assert len(p) > 0 and all(r["i"] // cl == r["j"] // cl for r in p)
+        passing = {(int(r["i"]), int(r["j"])): (int(r["common"]), int(r["total"])) for r in p}
+        rng = np.random.default_rng(1)
+        for _ in range(150):
+            i = int(rng.integers(0, n - 1))
+            j = min(n - 1, (i // cl) * cl + int(rng.integers(0, cl))) if rng.random() < 0.7 else int(rng.integers(0, n))
+            if i == j:
+                continue
+            i, j = min(i, j), max(i, j)
+            c, t = oracle.raw_distance(sk[i], sk[j])
+            assert ((i, j) in passing) == (oracle.ani(c, t) >= np.float64(thr))
+            if (i, j) in passing:
+                assert passing[(i, j)] == (c, t)
+    sub = 200
+    o = oracle.pairs(sk[:sub], ln[:sub].astype(np.int32), thr)
+    exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+    assert [x for x in as_tuples(p) if x[1] < sub] == exp
+    monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "merge")
+    with ga.Context(k=21, sketch_size=s) as ctx:
+        assert as_tuples(ctx.pairs(sk[:sub], ln[:sub], thr)) == exp
