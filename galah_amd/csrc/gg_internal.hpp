@@ -104,8 +104,11 @@ struct GateParams {
   uint32_t R;         // rows per row block
   uint32_t G;         // row blocks per tile row (ceil(GG_PAIR_TILE / R))
   uint32_t cap;       // R * s
-  uint32_t nb;        // value buckets (power of two)
+  uint32_t nb;        // buckets (power of two, ~8 keys each)
   uint32_t bm_words;  // gate bitmap words (power of two)
+  uint32_t nb_log2;
+  uint32_t bm_log2;   // log2 of the gate's bits
+  uint32_t wide;      // two-bit gate + directory in LDS (large sketches)
   uint64_t block_bytes;
 };
 GateParams gate_params(uint32_t s);  // requires s <= kGateCap

@@ -7,20 +7,24 @@
 //
 //  * Row blocks.  The R (<= 32) rows of a row block share one table, built
 //    once per launch by gate_build_kernel into HBM: the block's keys in
-//    value buckets (dir = start | count << 16; a key shared by several
-//    rows appears once per row, buckets unsorted), the row of each entry
-//    as a one-bit mask, and a gate bitmap with bit (key mod 2^b) set for
-//    every key.  R * s <= 32768 keys, so at s = 1000 a row block holds 32
-//    rows.
-//  * Gate.  pairs_gate_kernel copies the row block's bitmap (64 KiB at
-//    s = 1000) into LDS and streams the low words of column sketches (a
-//    compact copy made per launch) through it: per column hash one LDS read
-//    and a bit test.  With 32k keys in 2^19 bits ~6% of the hashes of an
-//    unrelated column pass the gate.  Passing hashes are queued per wave
-//    (LDS ring of column positions) and resolved 64 at a time by a walk of
-//    the bucket in HBM/L2 that ORs the masks of the equal keys.  One column
-//    hash therefore serves all R rows, and the table walk runs only for
-//    gate hits.
+//    buckets chosen by a hash of the key's low word (dir = start | count <<
+//    16, ~8 entries per bucket; a key shared by several rows appears once
+//    per row, buckets unsorted), the row of each entry as a one-bit mask,
+//    and a gate: a Bloom filter over the low words.  R * s <= 32768 keys,
+//    so at s = 1000 a row block holds 32 rows.
+//  * Gate.  pairs_gate_kernel copies the row block's gate into LDS and
+//    streams the low words of column sketches (a compact copy made per
+//    launch) through it.  For s < 2048: one gate bit in 2^19 bits (64 KiB;
+//    one LDS read per column hash; ~6% of an unrelated column's hashes pass
+//    at 32k keys) and ~2-key buckets whose directory stays in HBM.  For
+//    s >= 2048 ("wide": few rows per block, thousands of hashes per column
+//    visit): two gate bits in 2^18 bits (2-5% pass) and ~8-key buckets whose
+//    directory (16 KiB) is copied to LDS too.  Passing hashes are queued
+//    per wave (LDS ring of low words and positions) and resolved 64 at a
+//    time: directory, then the bucket's keys read 8 at a time; only a
+//    low-word match reads the column's high word.  The masks of the equal
+//    keys are ORed into per-lane byte counters.  One column hash serves all
+//    R rows.
 //  * Work order.  Work items (row block x column segment) are dealt to
 //    blockIdx column-segment-major in runs of 64 per XCD (the host does
 //    it: pairs_gate in api.cpp), so the workgroups resident on an XCD
@@ -43,19 +47,18 @@ namespace {
 
 constexpr int kThreads = 1024;
 constexpr int kWaves = kThreads / 64;
-constexpr uint32_t kRing = 128;      // per-wave queue of column positions (<= 63 + 64 pending)
+constexpr uint32_t kRing = 128;      // per-wave queue (<= 63 + 64 pending)
 constexpr int kRounds = 8;           // 64-hash rounds per register chunk
 constexpr uint32_t kMetaBytes = 512;
 
 struct GateMeta {
   uint64_t last[kGateRowsMax];  // largest hash of each row
   uint32_t len[kGateRowsMax];
-  uint64_t maxkey;
-  uint32_t shift_r, shift_l, scale, nrows;
+  uint32_t nrows;
 };
 static_assert(sizeof(GateMeta) <= kMetaBytes, "meta");
 
-// One row block's table in HBM: meta | dir[nb] | bitmap[bm_words] | keys[cap] | masks[cap]
+// One row block's table in HBM: meta | gate[bm_words] | dir[nb] | keys[cap] | masks[cap]
 struct BlockView {
   const GateMeta* meta;
   uint32_t* dir;
@@ -68,11 +71,22 @@ __device__ __forceinline__ BlockView block_view(const uint8_t* base, const GateP
   uint8_t* b = const_cast<uint8_t*>(base);
   BlockView v;
   v.meta = reinterpret_cast<const GateMeta*>(b);
-  v.dir = reinterpret_cast<uint32_t*>(b + kMetaBytes);
-  v.bm = v.dir + p.nb;
-  v.keys = reinterpret_cast<uint64_t*>(v.bm + p.bm_words);
+  v.bm = reinterpret_cast<uint32_t*>(b + kMetaBytes);
+  v.dir = v.bm + p.bm_words;
+  v.keys = reinterpret_cast<uint64_t*>(v.dir + p.nb);
   v.masks = reinterpret_cast<uint32_t*>(v.keys + p.cap);
   return v;
+}
+
+// Bucket of a key from its low word (multiplicative hash, independent of
+// the gate bits).
+__device__ __forceinline__ uint32_t bucket_lo(uint32_t lo, uint32_t nb_log2) {
+  return (lo * 0x9E3779B1u) >> (32 - nb_log2);
+}
+// The two gate bits of a key: a two-hash Bloom filter over the low word.
+__device__ __forceinline__ uint32_t gate_bit1(uint32_t lo, uint32_t bm_log2) { return lo & ((1u << bm_log2) - 1); }
+__device__ __forceinline__ uint32_t gate_bit2(uint32_t lo, uint32_t bm_log2) {
+  return (lo * 0x85EBCA6Bu) >> (32 - bm_log2);
 }
 
 // #{ e < n : a[e] <= x }, a ascending
@@ -106,7 +120,6 @@ __global__ __launch_bounds__(kThreads) void gate_build_kernel(GateBuildLaunch a)
 
   if (tid == 0) {
     const uint32_t nrows = row0 < row_end ? row_end - row0 : 0;
-    uint64_t mx = 0;
     uint32_t acc = 0;
     for (uint32_t r = 0; r < kGateRowsMax; ++r) {
       uint32_t l = 0;
@@ -119,22 +132,13 @@ __global__ __launch_bounds__(kThreads) void gate_build_kernel(GateBuildLaunch a)
       meta.last[r] = last;
       pre[r] = acc;
       acc += l;
-      if (l && last > mx) mx = last;
     }
     pre[kGateRowsMax] = acc;
-    meta.maxkey = mx;
-    const uint32_t L = mx ? 64 - __builtin_clzll(mx) : 1;
-    meta.shift_r = L > 32 ? L - 32 : 0;
-    meta.shift_l = L > 32 ? 0 : 32 - L;
-    const uint64_t t = (uint64_t)top32(mx, meta.shift_r, meta.shift_l) + 1;  // in (2^31, 2^32]
-    meta.scale = (uint32_t)(((uint64_t)p.nb << 32) / t);
     meta.nrows = nrows;
   }
   for (uint32_t i = tid; i < p.nb + p.bm_words; i += kThreads) sm[i] = 0;
   __syncthreads();
   const uint32_t E = pre[kGateRowsMax];
-  const uint32_t sr = meta.shift_r, sl = meta.shift_l, scale = meta.scale;
-  const uint32_t bmask = p.bm_words * 32 - 1;
   auto entry = [&](uint32_t e, uint32_t& r) {
     r = 0;
     for (uint32_t x = 1; x < p.R; ++x) r += (e >= pre[x]) ? 1u : 0u;
@@ -145,9 +149,11 @@ __global__ __launch_bounds__(kThreads) void gate_build_kernel(GateBuildLaunch a)
   for (uint32_t e = tid; e < E; e += kThreads) {
     uint32_t r;
     const uint64_t key = entry(e, r);
-    atomicAdd(&cnt[bucket_of(key, sr, sl, scale)], 1u);
-    const uint32_t bit = (uint32_t)key & bmask;
-    atomicOr(&bm[bit >> 5], 1u << (bit & 31));
+    const uint32_t lo = (uint32_t)key;
+    atomicAdd(&cnt[bucket_lo(lo, p.nb_log2)], 1u);
+    const uint32_t b1 = gate_bit1(lo, p.bm_log2), b2 = gate_bit2(lo, p.bm_log2);
+    atomicOr(&bm[b1 >> 5], 1u << (b1 & 31));
+    if (p.wide) atomicOr(&bm[b2 >> 5], 1u << (b2 & 31));
   }
   __syncthreads();
   // exclusive scan of the counts -> bucket starts
@@ -177,13 +183,13 @@ __global__ __launch_bounds__(kThreads) void gate_build_kernel(GateBuildLaunch a)
   for (uint32_t e = tid; e < E; e += kThreads) {
     uint32_t r;
     const uint64_t key = entry(e, r);
-    const uint32_t slot = atomicAdd(&cnt[bucket_of(key, sr, sl, scale)], 1u);
+    const uint32_t slot = atomicAdd(&cnt[bucket_lo((uint32_t)key, p.nb_log2)], 1u);
     v.keys[slot] = key;
     v.masks[slot] = 1u << r;
   }
   __syncthreads();
   // buckets stay unsorted: a lookup compares every entry of its bucket
-  // (~2 at R * s = 32k keys in 16k buckets) and ORs the masks of equal keys
+  // (~8 at R * s = 32k keys in 4k buckets) and ORs the masks of equal keys
   for (uint32_t b = tid; b < p.nb; b += kThreads) {
     const uint32_t s0 = b ? cnt[b - 1] : 0u, s1 = cnt[b];
     v.dir[b] = s0 | ((s1 - s0) << 16);
@@ -203,11 +209,14 @@ __global__ __launch_bounds__(256) void gate_lo32_kernel(const uint64_t* __restri
 // ---------------------------------------------------------------------------
 // Column streaming: one workgroup per (row block, column segment).
 // ---------------------------------------------------------------------------
+template <bool WIDE>
 __global__ __launch_bounds__(kThreads, 8) void pairs_gate_kernel(GateLaunch a) {
   extern __shared__ __align__(16) uint32_t sm[];
   const GateParams p = a.p;
-  uint32_t* bm = sm;                  // [bm_words]
-  uint32_t* rings = sm + p.bm_words;  // [kWaves][kRing]
+  uint32_t* bm = sm;                                 // [bm_words] gate
+  uint32_t* dir = bm + p.bm_words;                   // WIDE: [nb] bucket directory
+  uint32_t* rings_lo = dir + (WIDE ? p.nb : 0u);     // [kWaves][kRing] queued low words
+  uint16_t* rings_e = reinterpret_cast<uint16_t*>(rings_lo + kWaves * kRing);  // their column positions
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
   // work item of this workgroup (the host orders items so that the
@@ -224,19 +233,19 @@ __global__ __launch_bounds__(kThreads, 8) void pairs_gate_kernel(GateLaunch a) {
   const BlockView v = block_view(a.tables + (size_t)blk * p.block_bytes, p);
 
   {
+    // gate and directory are adjacent in both places
     const uint4* src = reinterpret_cast<const uint4*>(v.bm);
     uint4* dst = reinterpret_cast<uint4*>(bm);
-    for (uint32_t i = tid; i < p.bm_words / 4; i += kThreads) dst[i] = src[i];
+    for (uint32_t i = tid; i < (p.bm_words + (WIDE ? p.nb : 0u)) / 4; i += kThreads) dst[i] = src[i];
   }
   const GateMeta& gm = *v.meta;
-  const uint64_t maxkey = gm.maxkey;
-  const uint32_t sr = gm.shift_r, sl = gm.shift_l, scale = gm.scale, nrows = gm.nrows;
+  const uint32_t nrows = gm.nrows;
   // lane r < R holds row r
   const uint32_t la = lane < kGateRowsMax ? gm.len[lane] : 0u;
   const uint64_t xa = lane < kGateRowsMax ? gm.last[lane] : 0ull;
-  const uint32_t bmask = p.bm_words * 32 - 1;
   const uint32_t nacc = (p.R + 3) / 4;
-  uint32_t* ring = rings + wave * kRing;
+  uint32_t* ring_lo = rings_lo + wave * kRing;
+  uint16_t* ring_e = rings_e + wave * kRing;
   __syncthreads();
 
   for (uint32_t j = c0 + wave; j < c1; j += kWaves) {
@@ -245,16 +254,37 @@ __global__ __launch_bounds__(kThreads, 8) void pairs_gate_kernel(GateLaunch a) {
     uint32_t head = 0, tail = 0;  // wave-uniform
     uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // byte counters, rows 4q..4q+3
     bool hits = false;
-    // table walk for up to 64 queued column positions
+    const uint32_t* Bw = reinterpret_cast<const uint32_t*>(B);  // [2e] low, [2e+1] high word
+    // table walk for up to 64 queued hashes: directory in LDS, one read of
+    // the bucket's keys; the column's high word only for low-word matches
     auto drain = [&](uint32_t count) {
       uint32_t m = 0;
       if (lane < count) {
-        const uint64_t bv = B[ring[(head + lane) & (kRing - 1)]];
-        if (bv <= maxkey) {
-          const uint32_t d = v.dir[bucket_of(bv, sr, sl, scale)];
-          const uint32_t st = d & 0xFFFFu, n = d >> 16;
-          for (uint32_t k = 0; k < n; ++k)
-            if (v.keys[st + k] == bv) m |= v.masks[st + k];
+        const uint32_t q = (head + lane) & (kRing - 1);
+        const uint32_t lo = ring_lo[q];
+        const uint32_t d = (WIDE ? dir : v.dir)[bucket_lo(lo, p.nb_log2)];
+        const uint32_t st = d & 0xFFFFu, n = d >> 16;
+        // the bucket's keys, 8 loads in flight at a time; low-word matches
+        // collected as a bit set
+        const uint32_t* kw = reinterpret_cast<const uint32_t*>(v.keys + st);
+        uint32_t hi = 0;
+        bool have_hi = false;
+        for (uint32_t k0 = 0; k0 < n; k0 += 8) {
+          uint32_t kl[8];
+#pragma unroll
+          for (uint32_t t = 0; t < 8; ++t) kl[t] = kw[2 * min(k0 + t, n - 1)];
+          uint32_t match = 0;
+#pragma unroll
+          for (uint32_t t = 0; t < 8; ++t) match |= (kl[t] == lo && k0 + t < n) ? (1u << t) : 0u;
+          while (match) {
+            const uint32_t k = k0 + __builtin_ctz(match);
+            match &= match - 1;
+            if (!have_hi) {
+              hi = Bw[2 * (uint32_t)ring_e[q] + 1];
+              have_hi = true;
+            }
+            if (kw[2 * k + 1] == hi) m |= v.masks[st + k];
+          }
         }
       }
       if (__ballot(m != 0)) {
@@ -274,22 +304,30 @@ __global__ __launch_bounds__(kThreads, 8) void pairs_gate_kernel(GateLaunch a) {
     // are masked out of the hit test (branch-free).
     auto chunk = [&](uint32_t cb, auto tail_tag) {
       constexpr bool TAIL = decltype(tail_tag)::value;
-      uint32_t lo[kRounds], w[kRounds];
+      uint32_t lo[kRounds], w1[kRounds], w2[kRounds];
       const uint32_t* src = B32 + cb + lane;
 #pragma unroll
       for (int t = 0; t < kRounds; ++t)
         lo[t] = TAIL ? B32[min(cb + t * 64 + lane, lb - 1)] : src[64 * t];
 #pragma unroll
-      for (int t = 0; t < kRounds; ++t) w[t] = bm[(lo[t] & bmask) >> 5];
+      for (int t = 0; t < kRounds; ++t) {
+        w1[t] = bm[gate_bit1(lo[t], p.bm_log2) >> 5];
+        if (WIDE) w2[t] = bm[gate_bit2(lo[t], p.bm_log2) >> 5];
+      }
 #pragma unroll
       for (int t = 0; t < kRounds; ++t) {
         if (TAIL && cb + t * 64 >= lb) break;  // wave-uniform
         const uint32_t e = cb + t * 64 + lane;
-        uint32_t hit = (w[t] >> (lo[t] & 31)) & 1u;
+        uint32_t hit = (w1[t] >> (lo[t] & 31)) & 1u;
+        if (WIDE) hit &= w2[t] >> (gate_bit2(lo[t], p.bm_log2) & 31);
         if (TAIL) hit &= (e < lb) ? 1u : 0u;
         const uint64_t mm = __ballot(hit);
         if (mm) {
-          if (hit) ring[(tail + lanes_below(mm)) & (kRing - 1)] = e;
+          if (hit) {
+            const uint32_t q = (tail + lanes_below(mm)) & (kRing - 1);
+            ring_lo[q] = lo[t];
+            ring_e[q] = (uint16_t)e;
+          }
           tail += __popcll(mm);
           if (tail - head >= 64) drain(64);
         }
@@ -362,8 +400,21 @@ GateParams gate_params(uint32_t s) {
   g.R = std::min<uint32_t>(kGateRowsMax, std::max<uint32_t>(1, kGateCap / std::max<uint32_t>(s, 1)));
   g.G = (GG_PAIR_TILE + g.R - 1) / g.R;
   g.cap = g.R * s;
-  g.nb = std::min<uint32_t>(16384, std::max<uint32_t>(64, pow2_at_least((g.cap + 1) / 2)));
-  g.bm_words = std::min<uint32_t>(1u << 14, std::max<uint32_t>(128, pow2_at_least((uint64_t)g.cap * 16) / 32));
+  // Wide sketches (few rows per block, s hashes per column visit): a
+  // two-hash gate in 2^18 bits and the directory (~8 keys per bucket) in
+  // LDS, so gate misses are rarer and a table walk is one L2 round trip.
+  // Small sketches: a one-bit gate in 2^19 bits (cheaper per hash) and a
+  // directory of ~2-key buckets in HBM.
+  g.wide = s >= 2048;
+  if (g.wide) {
+    g.nb = std::min<uint32_t>(4096, std::max<uint32_t>(64, pow2_at_least((g.cap + 7) / 8)));
+    g.bm_words = std::min<uint32_t>(1u << 13, std::max<uint32_t>(128, pow2_at_least((uint64_t)g.cap * 8) / 32));
+  } else {
+    g.nb = std::min<uint32_t>(16384, std::max<uint32_t>(64, pow2_at_least((g.cap + 1) / 2)));
+    g.bm_words = std::min<uint32_t>(1u << 14, std::max<uint32_t>(128, pow2_at_least((uint64_t)g.cap * 16) / 32));
+  }
+  g.nb_log2 = __builtin_ctz(g.nb);
+  g.bm_log2 = __builtin_ctz(g.bm_words * 32);
   const uint64_t bytes = kMetaBytes + 4ull * g.nb + 4ull * g.bm_words + 12ull * g.cap;
   g.block_bytes = (bytes + 255) & ~255ull;
   return g;
@@ -388,11 +439,12 @@ hipError_t launch_gate_build(const GateBuildLaunch& a, hipStream_t st) {
 
 hipError_t launch_pairs_gate(const GateLaunch& a, hipStream_t st) {
   if (a.n_items == 0) return hipSuccess;
-  const size_t lds = 4ull * (a.p.bm_words + (uint64_t)kWaves * kRing);
-  hipError_t e = hipFuncSetAttribute((const void*)pairs_gate_kernel,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const size_t lds = 4ull * (a.p.bm_words + (a.p.wide ? a.p.nb : 0u)) + 6ull * kWaves * kRing;
+  const void* fn = a.p.wide ? (const void*)pairs_gate_kernel<true> : (const void*)pairs_gate_kernel<false>;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(pairs_gate_kernel, dim3(a.n_items), dim3(kThreads), lds, st, a);
+  if (a.p.wide) hipLaunchKernelGGL(pairs_gate_kernel<true>, dim3(a.n_items), dim3(kThreads), lds, st, a);
+  else hipLaunchKernelGGL(pairs_gate_kernel<false>, dim3(a.n_items), dim3(kThreads), lds, st, a);
   return hipGetLastError();
 }
 
