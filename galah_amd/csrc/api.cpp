@@ -35,6 +35,7 @@ struct gg_ctx {
     uint64_t work;
   };
   std::vector<gg::PairSeg> seg_host;
+  std::vector<uint64_t> kstart_host;
   int pairs_kernel = 0;  // GALAHGPU_PAIRS_KERNEL: 0 gate (default), 1 table, 2 merge
   std::vector<uint32_t> sufmin_host;
   bool timing = false;
@@ -285,30 +286,33 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
     std::vector<uint32_t> active = h_slot_list;
     for (int pass = 0; !active.empty(); ++pass) {
       if (pass > 200) return fail(c, GG_ERR_INTERNAL, "bottom-s threshold search did not converge");
-      // run table for the active genomes
-      std::vector<uint64_t> rb, rk;
-      std::vector<uint32_t> rs;
+      // run table for the active genomes: on the first pass the caller's
+      // runs of the batch as they are (one copy), on retries the subset
+      const bool all = active.size() == nb;
+      const gg_run* run_src = runs + gr[g0];
+      uint64_t nr = gr[g0 + nb] - gr[g0];
+      std::vector<gg_run> sub;
+      if (!all) {
+        sub.clear();
+        for (uint32_t slot : active)
+          for (uint64_t r = gr[g0 + slot]; r < gr[g0 + slot + 1]; ++r) sub.push_back(runs[r]);
+        run_src = sub.data();
+        nr = sub.size();
+      }
+      std::vector<uint64_t>& rk = c->kstart_host;
+      rk.resize(nr + 1);
       uint64_t kacc = 0;
-      for (uint32_t slot : active) {
-        const uint32_t g = g0 + slot;
-        for (uint64_t r = gr[g]; r < gr[g + 1]; ++r) {
-          rb.push_back(runs[r].base);
-          rk.push_back(kacc);
-          rs.push_back(slot);
-          kacc += runs[r].len - c->k + 1;
-        }
+      const uint32_t kk = (uint32_t)c->k;
+      for (uint64_t r = 0; r < nr; ++r) {
+        rk[r] = kacc;
+        kacc += run_src[r].len - kk + 1;
       }
-      rk.push_back(kacc);
-      const uint32_t nr = (uint32_t)rs.size();
-      uint64_t *d_rb, *d_rk;
-      uint32_t* d_rs;
-      GG_HIP(c, scratch_t(c, "run_base", std::max<size_t>(nr, 1), &d_rb));
+      rk[nr] = kacc;
+      gg_run* d_runs;
+      uint64_t* d_rk;
+      GG_HIP(c, scratch_t(c, "runs", std::max<size_t>(nr, 1), &d_runs));
       GG_HIP(c, scratch_t(c, "run_kstart", nr + 1, &d_rk));
-      GG_HIP(c, scratch_t(c, "run_slot", std::max<size_t>(nr, 1), &d_rs));
-      if (nr) {
-        GG_HIP(c, hipMemcpyAsync(d_rb, rb.data(), nr * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-        GG_HIP(c, hipMemcpyAsync(d_rs, rs.data(), nr * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-      }
+      if (nr) GG_HIP(c, hipMemcpyAsync(d_runs, run_src, nr * sizeof(gg_run), hipMemcpyHostToDevice, st));
       GG_HIP(c, hipMemcpyAsync(d_rk, rk.data(), (nr + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
       GG_HIP(c, hipMemcpyAsync(d_tau, h_tau.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
       GG_HIP(c, hipMemcpyAsync(d_slot_list, active.data(), active.size() * sizeof(uint32_t),
@@ -327,10 +331,10 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       SketchLaunch a;
       a.words = d_words;
       a.n_words = n_words;
-      a.run_base = d_rb;
+      a.runs = d_runs;
       a.run_kstart = d_rk;
-      a.run_slot = d_rs;
-      a.n_runs = nr;
+      a.slot_genome0 = g0;
+      a.n_runs = (uint32_t)nr;
       a.n_kmers = kacc;
       a.tau = d_tau;
       a.table = d_table;

@@ -31,9 +31,9 @@ constexpr uint32_t kSortCap = 16384;
 struct SketchLaunch {
   const uint32_t* words;
   uint64_t n_words;
-  const uint64_t* run_base;    // [n_runs]
+  const gg_run* runs;          // [n_runs] (genome - slot_genome0 = slot within the batch)
   const uint64_t* run_kstart;  // [n_runs + 1] exclusive prefix of k-mer counts
-  const uint32_t* run_slot;    // [n_runs] genome slot within the batch
+  uint32_t slot_genome0;       // genome of batch slot 0
   uint32_t n_runs;
   uint64_t n_kmers;
   const uint64_t* tau;         // [slots]

@@ -283,10 +283,11 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
       const uint64_t rk0 = a.run_kstart[r];
       const uint64_t stop = min(pend, a.run_kstart[r + 1]);
       const uint32_t cnt = (uint32_t)(stop - p);
-      const uint32_t slot = a.run_slot[r];
+      const gg_run run = a.runs[r];
+      const uint32_t slot = run.genome - a.slot_genome0;
       const uint64_t tau = a.tau[slot];
       uint64_t* gset = a.table + ((uint64_t)slot << a.cap_log2);
-      const uint64_t b = a.run_base[r] + (p - rk0);  // first base of k-mer p
+      const uint64_t b = run.base + (p - rk0);  // first base of k-mer p
 
       const uint64_t wi = b >> 4;
       const uint32_t off = (uint32_t)b & 15u;
