@@ -16,7 +16,7 @@
 //     The reverse complement needs no separate state:
 //       rc MSB-first = ~fl, rc LSB-first = ~fm   (within 2k bits).
 //   * The first multiply of each murmur3 input word and the ASCII byte
-//     assembly are folded into LDS tables (see hash_code).
+//     assembly are folded into LDS tables (see hash_parts).
 //   * Bottom-s selection is a threshold prefilter: a k-mer survives iff
 //     h <= tau[g] where tau[g] ~ C*s/nk_g * 2^64, so only ~C*s of the
 //     ~nk_g hashes per genome reach a per-genome open-addressing set in HBM
@@ -56,14 +56,16 @@ __device__ __forceinline__ uint64_t rotl64(uint64_t x) {
   return ((uint64_t)nh << 32) | nl;
 }
 
-__device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+// fmix64 without its final k ^= k >> 33, which leaves the high word alone
+// (see the tau prefilter in sketch_candidates_kernel).
+__device__ __forceinline__ uint64_t fmix64_pre(uint64_t k) {
   k ^= k >> 33;
   k *= 0xff51afd7ed558ccdull;
   k ^= k >> 33;
   k *= 0xc4ceb9fe1a85ec53ull;
-  k ^= k >> 33;
   return k;
 }
+__device__ __forceinline__ uint64_t fmix_last(uint64_t k) { return k ^ (k >> 33); }
 
 // h * 5 + c with one v_lshl_add_u64 (hipcc otherwise lowers the multiply by
 // 5 to v_mad_u64_u32 sequences).
@@ -95,7 +97,8 @@ __device__ __forceinline__ uint32_t group_byte(uint32_t hi, uint32_t lo, int q) 
   return (w >> (8 * (3 - (q & 3)))) & 0xFFu;
 }
 
-// murmurhash3_x64_128(bytes, seed).0 where byte p = ASCII of base p of the
+// murmurhash3_x64_128(bytes, seed).0 = fmix_last(f1) + fmix_last(f2) with
+// (f1, f2) from hash_parts, where byte p = ASCII of base p of the
 // k-mer whose MSB-first 2-bit code is top-aligned in `code` (base 0 in bits
 // 63..62; bits below 64-2K are ignored, K <= 32).
 //
@@ -110,9 +113,8 @@ __device__ __forceinline__ uint32_t group_byte(uint32_t hi, uint32_t lo, int q) 
 // final h1 ^= len, is one table entry.  Tables live in LDS
 // (HashShape<K>::TAB_U64 entries).
 template <int K>
-__device__ __forceinline__ uint64_t hash_code(uint64_t code,
-                                              const uint64_t* __restrict__ tab,
-                                              uint64_t seed) {
+__device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __restrict__ tab,
+                                           uint64_t seed, uint64_t& f1, uint64_t& f2) {
   using S = HashShape<K>;
   const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
   const uint32_t hi = (uint32_t)(code >> 32), lo = (uint32_t)code;
@@ -148,9 +150,8 @@ __device__ __forceinline__ uint64_t hash_code(uint64_t code,
   h2 ^= (uint64_t)K;
   h1 += h2;
   h2 += h1;
-  h1 = fmix64(h1);
-  h2 = fmix64(h2);
-  return h1 + h2;
+  f1 = fmix64_pre(h1);
+  f2 = fmix64_pre(h2);
 }
 
 // ASCII bytes of `nbases` bases of an MSB-first code of `width` bases
@@ -265,7 +266,7 @@ __device__ __forceinline__ uint32_t window32(const uint32_t (&w)[4], int t) {
 template <int K, bool SEED0>
 __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_kernel(SketchLaunch a) {
   static_assert(K >= 1 && K <= 32 && kSeg + K - 1 <= 64, "window");
-  __shared__ uint64_t mtab[HashShape<K>::TAB_U64];  // murmur word tables (hash_code)
+  __shared__ uint64_t mtab[HashShape<K>::TAB_U64];  // murmur word tables (hash_parts)
   build_tables<K>(mtab);
   __syncthreads();
 
@@ -286,6 +287,12 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
       const gg_run run = a.runs[r];
       const uint32_t slot = run.genome - a.slot_genome0;
       const uint64_t tau = a.tau[slot];
+      // prefilter on the high words: h = fmix_last(f1) + fmix_last(f2)
+      // has high word S or S + 1 (carry), S = hi(f1) + hi(f2), so h <= tau
+      // needs S <= hi(tau) or S = 2^32 - 1, i.e. S + 1 <= hi(tau) + 1 (mod
+      // 2^32; every S passes when hi(tau) = 2^32 - 1)
+      const uint32_t tau_hi = (uint32_t)(tau >> 32);
+      const uint32_t thr = tau_hi == 0xFFFFFFFFu ? 0xFFFFFFFFu : tau_hi + 1u;
       uint64_t* gset = a.table + ((uint64_t)slot << a.cap_log2);
       const uint64_t b = run.base + (p - rk0);  // first base of k-mer p
 
@@ -303,23 +310,27 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
 
 #pragma unroll
       for (int g = 0; g < kSeg / kGroup; ++g) {
-        uint64_t h[kGroup];
+        uint64_t f1[kGroup], f2[kGroup];
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
           const int i = g * kGroup + j;
           const uint64_t fwd = ((uint64_t)window32(F, i) << 32) | window32(F, i + 16);
           const int t0 = 64 - K - i;  // reverse complement of k-mer i starts here
           const uint64_t rev = ((uint64_t)window32(R, t0) << 32) | window32(R, t0 + 16);
-          h[j] = hash_code<K>(fwd < rev ? fwd : rev, mtab, seed);
+          hash_parts<K>(fwd < rev ? fwd : rev, mtab, seed, f1[j], f2[j]);
         }
         bool any = false;
 #pragma unroll
-        for (int j = 0; j < kGroup; ++j) any |= h[j] <= tau;
+        for (int j = 0; j < kGroup; ++j)
+          any |= (uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr;
         if (any) {
+          uint64_t h[kGroup];
           uint32_t pending = 0;
 #pragma unroll
-          for (int j = 0; j < kGroup; ++j)
+          for (int j = 0; j < kGroup; ++j) {
+            h[j] = fmix_last(f1[j]) + fmix_last(f2[j]);
             pending |= ((h[j] <= tau) & ((uint32_t)(g * kGroup + j) < cnt)) ? (1u << j) : 0u;
+          }
           while (pending) {
             const int j = __builtin_ctz(pending);
             pending &= pending - 1;
