@@ -255,10 +255,9 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   const int grid = std::max(1, n_cu) * 8;
 
   uint64_t* d_table;
-  uint32_t *d_count, *d_flags, *d_status, *d_slot_list, *d_slot_genome;
+  uint32_t *d_flags, *d_status, *d_slot_list, *d_slot_genome;
   uint64_t* d_tau;
   GG_HIP(c, scratch_t(c, "table", (size_t)max_batch * cap, &d_table));
-  GG_HIP(c, scratch_t(c, "count", max_batch, &d_count));
   GG_HIP(c, scratch_t(c, "flags", max_batch, &d_flags));
   GG_HIP(c, scratch_t(c, "status", max_batch, &d_status));
   GG_HIP(c, scratch_t(c, "slot_list", max_batch, &d_slot_list));
@@ -319,12 +318,10 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
                                hipMemcpyHostToDevice, st));
       if (pass == 0) {
         GG_HIP(c, hipMemsetAsync(d_table, 0xFF, (size_t)nb * cap * sizeof(uint64_t), st));
-        GG_HIP(c, hipMemsetAsync(d_count, 0, nb * sizeof(uint32_t), st));
         GG_HIP(c, hipMemsetAsync(d_flags, 0, nb * sizeof(uint32_t), st));
       } else {
         for (uint32_t slot : active) {
           GG_HIP(c, hipMemsetAsync(d_table + (uint64_t)slot * cap, 0xFF, cap * sizeof(uint64_t), st));
-          GG_HIP(c, hipMemsetAsync(d_count + slot, 0, sizeof(uint32_t), st));
           GG_HIP(c, hipMemsetAsync(d_flags + slot, 0, sizeof(uint32_t), st));
         }
       }
@@ -339,8 +336,6 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       a.tau = d_tau;
       a.table = d_table;
       a.cap_log2 = geom.cap_log2;
-      a.count = d_count;
-      a.limit = geom.limit;
       a.flags = d_flags;
       a.seed = c->seed;
       const uint64_t segs = (kacc + 31) / 32;
@@ -349,7 +344,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
                              [&] { return launch_sketch_candidates(c->k, a, g, st); }));
       GG_HIP(c, timed_launch(c, GG_KERNEL_FINALIZE, active.size(), st, [&] {
         return launch_sketch_finalize(d_slot_list, (uint32_t)active.size(), d_slot_genome, d_tau,
-                                      d_table, geom.cap_log2, d_count, d_flags, c->s,
+                                      d_table, geom.cap_log2, d_flags, c->s,
                                       geom.sort_pow2, d_out, d_lens, d_status, st);
       }));
       std::vector<uint32_t> status(nb);

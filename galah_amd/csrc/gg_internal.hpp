@@ -39,8 +39,6 @@ struct SketchLaunch {
   const uint64_t* tau;         // [slots]
   uint64_t* table;             // [slots << cap_log2]
   uint32_t cap_log2;
-  uint32_t* count;             // [slots]
-  uint32_t limit;
   uint32_t* flags;             // [slots]
   uint64_t seed;
 };
@@ -51,7 +49,7 @@ hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,
 hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   const uint32_t* slot_genome,
                                   const uint64_t* tau, const uint64_t* table,
-                                  uint32_t cap_log2, const uint32_t* count,
+                                  uint32_t cap_log2,
                                   const uint32_t* flags, uint32_t s,
                                   uint32_t sort_pow2, uint64_t* out,
                                   uint32_t* lens, uint32_t* status,

@@ -184,32 +184,26 @@ __device__ __forceinline__ void build_tables(uint64_t* tab) {
   }
 }
 
-// Insert h into genome slot's open-addressing set.
+// Insert h into genome slot's open-addressing set (linear probing; one
+// atomicCAS per probe, no per-genome counter: the finalize kernel counts the
+// set when it gathers it).
 __device__ __forceinline__ void insert_candidate(uint64_t* __restrict__ tab,
                                                  uint32_t mask,
-                                                 uint32_t* __restrict__ count,
-                                                 uint32_t limit,
                                                  uint32_t* __restrict__ flags,
                                                  uint64_t h) {
   if (h == kEmpty) {  // only reachable when tau == 2^64-1
     atomicOr(flags, kFlagSawMax);
     return;
   }
-  if (__hip_atomic_load(flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & kFlagOverflow) return;
   uint32_t i = (uint32_t)h & mask;
   for (uint32_t probe = 0; probe <= mask; ++probe) {
     const unsigned long long old =
         atomicCAS((unsigned long long*)&tab[i], (unsigned long long)kEmpty,
                   (unsigned long long)h);
-    if (old == kEmpty) {
-      const uint32_t c = atomicAdd(count, 1u);
-      if (c + 1 >= limit) atomicOr(flags, kFlagOverflow);
-      return;
-    }
-    if (old == h) return;
+    if (old == kEmpty || old == h) return;
     i = (i + 1) & mask;
   }
-  atomicOr(flags, kFlagOverflow);
+  atomicOr(flags, kFlagOverflow);  // table full
 }
 
 // Largest r with run_kstart[r] <= p, searching forward from `from`
@@ -337,7 +331,7 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
             uint64_t hv = h[0];
 #pragma unroll
             for (int q = 1; q < kGroup; ++q) hv = (j == q) ? h[q] : hv;
-            insert_candidate(gset, cap_mask, a.count + slot, a.limit, a.flags + slot, hv);
+            insert_candidate(gset, cap_mask, a.flags + slot, hv);
           }
         }
       }
@@ -352,7 +346,7 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
 __global__ __launch_bounds__(kBlock) void sketch_finalize_kernel(
     const uint32_t* __restrict__ slot_list, const uint32_t* __restrict__ slot_genome,
     const uint64_t* __restrict__ tau, const uint64_t* __restrict__ table,
-    uint32_t cap_log2, const uint32_t* __restrict__ count,
+    uint32_t cap_log2,
     const uint32_t* __restrict__ flags, uint32_t s, uint32_t sort_pow2,
     uint64_t* __restrict__ out, uint32_t* __restrict__ lens,
     uint32_t* __restrict__ status) {
@@ -361,14 +355,9 @@ __global__ __launch_bounds__(kBlock) void sketch_finalize_kernel(
   const uint32_t slot = slot_list[blockIdx.x];
   const uint32_t g = slot_genome[slot];
   const uint32_t f = flags[slot];
-  const uint32_t cnt = count[slot];
-  uint32_t st = kSketchOk;
-  if (f & kFlagOverflow) st = kSketchRetrySmaller;
-  else if (cnt < s && tau[slot] != kEmpty) st = kSketchRetryLarger;
-  else if (cnt > sort_pow2) st = kSketchRetrySmaller;  // cannot sort in LDS
-  if (st != kSketchOk) {
+  if (f & kFlagOverflow) {
     if (threadIdx.x == 0) {
-      status[slot] = st;
+      status[slot] = kSketchRetrySmaller;
       lens[g] = 0;
     }
     return;
@@ -379,10 +368,23 @@ __global__ __launch_bounds__(kBlock) void sketch_finalize_kernel(
   const uint32_t cap = 1u << cap_log2;
   for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
     const uint64_t v = tab[i];
-    if (v != kEmpty) buf[atomicAdd(&fill, 1u)] = v;
+    if (v != kEmpty) {
+      const uint32_t at = atomicAdd(&fill, 1u);
+      if (at < sort_pow2) buf[at] = v;
+    }
   }
   __syncthreads();
-  const uint32_t n = fill;  // == cnt
+  const uint32_t n = fill;  // distinct candidates <= tau
+  uint32_t st = kSketchOk;
+  if (n > sort_pow2) st = kSketchRetrySmaller;  // cannot sort in LDS
+  else if (n < s && tau[slot] != kEmpty) st = kSketchRetryLarger;
+  if (st != kSketchOk) {
+    if (threadIdx.x == 0) {
+      status[slot] = st;
+      lens[g] = 0;
+    }
+    return;
+  }
   uint32_t P = 1;
   while (P < n) P <<= 1;
   for (uint32_t i = n + threadIdx.x; i < P; i += blockDim.x) buf[i] = kEmpty;
@@ -445,7 +447,7 @@ hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,
 hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   const uint32_t* slot_genome,
                                   const uint64_t* tau, const uint64_t* table,
-                                  uint32_t cap_log2, const uint32_t* count,
+                                  uint32_t cap_log2,
                                   const uint32_t* flags, uint32_t s,
                                   uint32_t sort_pow2, uint64_t* out,
                                   uint32_t* lens, uint32_t* status,
@@ -458,7 +460,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
     if (e != hipSuccess) return e;
   }
   hipLaunchKernelGGL(sketch_finalize_kernel, dim3(n_slots), dim3(kBlock), lds, st,
-                     slot_list, slot_genome, tau, table, cap_log2, count, flags, s,
+                     slot_list, slot_genome, tau, table, cap_log2, flags, s,
                      sort_pow2, out, lens, status);
   return hipGetLastError();
 }
