@@ -335,3 +335,40 @@ def test_c5_mixed_sizes_s10000(gpu_ctx, monkeypatch):
     monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "merge")
     with ga.Context(k=21, sketch_size=s) as ctx:
         assert as_tuples(ctx.pairs(sk[:sub], ln[:sub], thr)) == exp
+
+
+@pytest.mark.parametrize("s", [200, 3000])
+def test_gate_kernel_low_word_collisions(monkeypatch, s):
+    """Keys that share their low 32 bits all land in one bucket of the gate
+    kernel's table and set a single gate bit: the walks degenerate into
+    full-bucket scans but must still count exactly (narrow and wide)."""
+    rng = np.random.default_rng(s)
+    n = 70
+    lo = np.uint64(0x9E3779B9)
+    his = np.unique(rng.integers(1, 2**31, 3 * s, dtype=np.uint64))
+    sk = np.zeros((n, s), np.uint64)
+    lens = np.zeros(n, np.uint32)
+    for i in range(n):
+        m = s if i % 5 else s // 3
+        pick = np.sort(rng.choice(len(his) // (1 + i % 3), m, replace=False))
+        v = (his[pick] << np.uint64(32)) | lo
+        if i % 7 == 0:  # a few keys with their own low words
+            v = np.unique(np.concatenate([v[: m - 5], rng.integers(0, 2**63, 5, dtype=np.uint64)]))[:m]
+        sk[i, :len(v)] = v
+        lens[i] = len(v)
+    for thr in (0.0, 0.5, 0.9):
+        o = oracle.pairs(sk, lens.astype(np.int32), np.float32(thr))
+        exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+        monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "gate")
+        with ga.Context(k=21, sketch_size=s) as ctx:
+            assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, thr
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 31, 33, 65, 129])
+def test_gate_kernel_small_and_ragged_n(gpu_ctx, n):
+    rng = np.random.default_rng(n)
+    sk, lens = random_sketch_set(rng, n, 1000, 3)
+    for thr in (0.0, 0.9):
+        p = gpu_ctx.pairs(sk, lens, np.float32(thr))
+        o = oracle.pairs(sk, lens.astype(np.int32), np.float32(thr))
+        assert as_tuples(p) == [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
