@@ -109,7 +109,10 @@ int gg_device(const gg_ctx* ctx);
 /* ---- host-side ingest: FASTA/FASTQ (plain or gz) -> 2-bit runs --------- */
 /* Replaces needletail parse_fastx_file + normalize(false) + the ACGT
  * window test of canonical_kmers inside finch::sketch_files
- * (src/finch.rs:47).  n_threads <= 0 means all hardware threads. */
+ * (src/finch.rs:47).  Files are read on n_threads threads (<= 0: the
+ * GALAHGPU_THREADS or OMP_NUM_THREADS environment variable, else the CPUs
+ * in the process's affinity mask); gzip is decoded with libdeflate when the
+ * system library is present, zlib otherwise. */
 gg_status gg_pack_files(const char* const* paths, uint32_t n_paths,
                         int kmer_length, int n_threads, gg_packed** out);
 /* In-memory records: record r (bytes seqs[r][0..lens[r]) , no header, may

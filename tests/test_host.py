@@ -245,3 +245,24 @@ def test_cache_key_normalisation():
 
 def test_finch_preclusterer_method_name():
     assert ga.FinchPreclusterer(0.9, 1000, 21).method_name() == "finch"
+
+
+def test_packer_multi_member_gzip_and_decoders(tmp_path, monkeypatch):
+    # bgzip-style concatenated gzip members decode to the whole file, with
+    # libdeflate (when installed) and with the zlib fallback alike
+    recs = [b">a\n" + b"ACGTTGCAAC" * 500 + b"\n", b">b\n" + b"ggcatTTACU" * 700 + b"\nNNNN\nACGT" * 30 + b"\n"]
+    gz = tmp_path / "m.fa.gz"
+    gz.write_bytes(gzip.compress(recs[0]) + gzip.compress(recs[1]))
+    plain = tmp_path / "m.fa"
+    plain.write_bytes(recs[0] + recs[1])
+    a = ga.pack_files([str(plain)])
+    b = ga.pack_files([str(gz)])
+    assert (a.words == b.words).all() and (a.runs == b.runs).all()
+    assert (oracle.sketch_records(packed_records(a)[0]) == oracle.sketch_file(str(plain))).all()
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import galah_amd as ga, numpy as np; "
+            "a = ga.pack_files([%r]); b = ga.pack_files([%r]); "
+            "assert (a.words == b.words).all() and (a.runs == b.runs).all()" % (ROOT, str(plain), str(gz)))
+    env = dict(os.environ, GALAHGPU_NO_LIBDEFLATE="1")
+    subprocess.run([sys.executable, "-c", code], check=True, env=env)
