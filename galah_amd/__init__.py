@@ -27,6 +27,7 @@ __all__ = [
     "SortedPairGenomeDistanceCache", "PreclusterDistanceFinder",
     "FinchPreclusterer", "distances", "PAIR_DTYPE", "LIB_PATH", "EXPORTED_SYMBOLS",
     "partition_preclusters", "precluster_pairs", "preclusters", "LOCAL_PAIR_DTYPE",
+    "sketch_cache_load", "sketch_cache_store",
 ]
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -45,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "gg_precluster_files", "gg_ani_f64", "gg_ani_f32", "gg_parse_percentage",
     "gg_free", "gg_synth_clustered_device", "gg_timing_enable", "gg_timing_read",
     "gg_partition_preclusters", "gg_precluster_pairs", "gg_synth_mixed_lengths", "gg_synth_mixed_device",
+    "gg_sketch_cache_load", "gg_sketch_cache_store", "gg_sketch_files", "gg_precluster_files_cached",
 )
 
 GG_OK = 0
@@ -111,6 +113,14 @@ _sig("gg_pairs", _i32, [_vp, _vp, _vp, _u32, ctypes.c_float, ctypes.POINTER(_vp)
 _sig("gg_pairs_device", _i32, [_vp, _vp, _vp, _u32, _u64, _u64, ctypes.c_float, _vp, _u64, _vp, _vp])
 _sig("gg_precluster_files", _i32, [_vp, ctypes.POINTER(ctypes.c_char_p), _u32, ctypes.c_float,
                                    ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_u64)])
+_sig("gg_precluster_files_cached", _i32, [_vp, ctypes.POINTER(ctypes.c_char_p), _u32, ctypes.c_float,
+                                          ctypes.c_char_p, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                          ctypes.POINTER(_u64), ctypes.POINTER(_u32)])
+_sig("gg_sketch_files", _i32, [_vp, ctypes.POINTER(ctypes.c_char_p), _u32, ctypes.c_char_p, _vp, _vp,
+                               ctypes.POINTER(_u32)])
+_sig("gg_sketch_cache_load", _i32, [ctypes.c_char_p, ctypes.c_char_p, _i32, _u32, _u64, _vp,
+                                    ctypes.POINTER(_u32), ctypes.POINTER(_i32)])
+_sig("gg_sketch_cache_store", _i32, [ctypes.c_char_p, ctypes.c_char_p, _i32, _u32, _u64, _vp, _u32])
 _sig("gg_ani_f64", ctypes.c_double, [_u32, _u32, _i32])
 _sig("gg_ani_f32", ctypes.c_float, [_u32, _u32, _i32])
 _sig("gg_parse_percentage", _i32, [ctypes.c_float, ctypes.POINTER(ctypes.c_float)])
@@ -238,6 +248,27 @@ def preclusters(n_genomes, pairs):
     a list of ascending index lists, largest first."""
     members, offsets = partition_preclusters(n_genomes, pairs)
     return [members[offsets[s]:offsets[s + 1]].tolist() for s in range(len(offsets) - 1)]
+
+
+def sketch_cache_load(cache_dir, path, k=21, s=1000, seed=0):
+    """the cached bottom-s sketch of a genome file
+    (ascending u64 array), or None when there is no valid entry.  Host only."""
+    out = np.zeros(max(int(s), 1), dtype=np.uint64)
+    n, hit = _u32(), _i32()
+    st = _L.gg_sketch_cache_load(os.fsencode(cache_dir), os.fsencode(path), int(k), int(s), int(seed),
+                                 _ptr(out), ctypes.byref(n), ctypes.byref(hit))
+    if st != GG_OK:
+        raise _thread_err(st)
+    return out[:n.value].copy() if hit.value else None
+
+
+def sketch_cache_store(cache_dir, path, hashes, k=21, s=1000, seed=0):
+    """Store the sketch of a genome file (strictly ascending, len <= s).  Host only."""
+    h = np.ascontiguousarray(hashes, dtype=np.uint64)
+    st = _L.gg_sketch_cache_store(os.fsencode(cache_dir), os.fsencode(path), int(k), int(s), int(seed),
+                                  _ptr(h), len(h))
+    if st != GG_OK:
+        raise _thread_err(st)
 
 
 class Packed:
@@ -375,12 +406,31 @@ class Context:
             raise self._err(st)
         return _take_pairs(outp, cnt.value)
 
-    def precluster_files(self, paths, min_ani):
-        """-> (pairs structured array sorted by (i, j), ani f32 array)."""
+    def sketch_files(self, paths, cache_dir=None):
+        """finch sketch_files (src/finch.rs:47) for files -> (sketches [n, s] u64
+        padded with 0, lens [n] u32, number of genomes served by cache_dir)."""
+        n = len(paths)
+        arr = (ctypes.c_char_p * max(n, 1))(*[os.fsencode(p) for p in paths])
+        out = np.zeros((max(n, 1), self.s), dtype=np.uint64)
+        lens = np.zeros(max(n, 1), dtype=np.uint32)
+        hits = _u32()
+        st = _L.gg_sketch_files(self._c, arr, n, None if cache_dir is None else os.fsencode(cache_dir),
+                                _ptr(out), _ptr(lens), ctypes.byref(hits))
+        if st != GG_OK:
+            raise self._err(st)
+        return out[:n], lens[:n], hits.value
+
+    def precluster_files(self, paths, min_ani, cache_dir=None):
+        """-> (pairs structured array sorted by (i, j), ani f32 array).  With
+        cache_dir, genomes sketched by an earlier call are read from the
+        sketch cache (self.last_cached counts them)."""
         arr = (ctypes.c_char_p * max(len(paths), 1))(*[os.fsencode(p) for p in paths])
-        pp, ap, cnt = _vp(), _vp(), _u64()
-        st = _L.gg_precluster_files(self._c, arr, len(paths), ctypes.c_float(min_ani), ctypes.byref(pp),
-                                    ctypes.byref(ap), ctypes.byref(cnt))
+        pp, ap, cnt, hits = _vp(), _vp(), _u64(), _u32()
+        st = _L.gg_precluster_files_cached(self._c, arr, len(paths), ctypes.c_float(min_ani),
+                                           None if cache_dir is None else os.fsencode(cache_dir),
+                                           ctypes.byref(pp), ctypes.byref(ap), ctypes.byref(cnt),
+                                           ctypes.byref(hits))
+        self.last_cached = hits.value
         if st != GG_OK:
             raise self._err(st)
         n = cnt.value
@@ -530,11 +580,14 @@ def _context(k, s, seed=0):
     return c
 
 
-def distances(genome_fasta_paths, min_ani, num_kmers, kmer_length):
-    """src/finch.rs:26-75 -> SortedPairGenomeDistanceCache, computed on the GPU."""
+def distances(genome_fasta_paths, min_ani, num_kmers, kmer_length, sketch_cache_dir=None):
+    """src/finch.rs:26-75 -> SortedPairGenomeDistanceCache, computed on the GPU.
+    sketch_cache_dir (not in galah) reuses sketches of
+    unchanged genome files from earlier runs; the result is the same."""
     try:
         ctx = _context(int(kmer_length), int(num_kmers))
-        pairs, ani = ctx.precluster_files(list(genome_fasta_paths), float(np.float32(min_ani)))
+        pairs, ani = ctx.precluster_files(list(genome_fasta_paths), float(np.float32(min_ani)),
+                                          cache_dir=sketch_cache_dir)
     except GalahGpuError as e:
         # src/finch.rs:50
         raise RuntimeError("Failed to sketch genomes with finch: %s" % e) from e
@@ -547,13 +600,15 @@ def distances(genome_fasta_paths, min_ani, num_kmers, kmer_length):
 class FinchPreclusterer(PreclusterDistanceFinder):
     """src/finch.rs:4-24: min_ani is a fraction (f32), num_kmers = s, kmer_length = k."""
 
-    def __init__(self, min_ani, num_kmers=1000, kmer_length=21):
+    def __init__(self, min_ani, num_kmers=1000, kmer_length=21, sketch_cache_dir=None):
         self.min_ani = np.float32(min_ani)
         self.num_kmers = int(num_kmers)
         self.kmer_length = int(kmer_length)
+        self.sketch_cache_dir = sketch_cache_dir
 
     def distances(self, genome_fasta_paths):
-        return distances(genome_fasta_paths, self.min_ani, self.num_kmers, self.kmer_length)
+        return distances(genome_fasta_paths, self.min_ani, self.num_kmers, self.kmer_length,
+                         sketch_cache_dir=self.sketch_cache_dir)
 
     def method_name(self):
         return "finch"

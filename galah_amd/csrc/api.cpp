@@ -582,6 +582,93 @@ T* copy_out(const std::vector<T>& v) {
   return p;
 }
 
+// Sketches of the genome files paths[0..n) in device rows d_out [n x s],
+// d_lens [n] (ctx scratch "sk_out", "sk_lens"), the body of finch's
+// sketch_files (src/finch.rs:47).  With a cache directory (SURVEY.md 8(f)
+// row 4, sketch_cache.cpp) genomes with a valid entry skip ingest and K1;
+// the others are packed, sketched and stored.  host_out / host_lens, when
+// given, receive the rows as well.  Cache writes that fail (read-only
+// directory, full disk) do not fail the call: the sketches are still exact.
+gg_status sketch_paths(gg_ctx* c, const char* const* paths, uint32_t n, const char* cache_dir,
+                       hipStream_t st, uint64_t** d_out_p, uint32_t** d_lens_p, uint64_t* host_out,
+                       uint32_t* host_lens, uint32_t* n_cached) {
+  const uint32_t s = c->s;
+  uint64_t* d_out;
+  uint32_t* d_lens;
+  GG_HIP(c, scratch_t(c, "sk_out", (size_t)std::max(n, 1u) * s, &d_out));
+  GG_HIP(c, scratch_t(c, "sk_lens", std::max(n, 1u), &d_lens));
+  *d_out_p = d_out;
+  *d_lens_p = d_lens;
+  if (n_cached) *n_cached = 0;
+  if (n == 0) return GG_OK;
+  std::vector<uint8_t> hit(n, 0);
+  std::vector<uint64_t> rows_own;
+  std::vector<uint32_t> lens_own;
+  uint64_t* rows = host_out;
+  uint32_t* lens = host_lens;
+  if (cache_dir) {
+    if (!rows) {
+      rows_own.assign((size_t)n * s, 0);
+      rows = rows_own.data();
+    }
+    if (!lens) {
+      lens_own.assign(n, 0);
+      lens = lens_own.data();
+    }
+    memset(rows, 0, (size_t)n * s * sizeof(uint64_t));
+    cache_load_many(cache_dir, paths, n, c->k, s, c->seed, rows, lens, hit.data());
+  }
+  std::vector<const char*> miss;
+  std::vector<uint32_t> miss_at;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!hit[i]) {
+      miss.push_back(paths[i]);
+      miss_at.push_back(i);
+    }
+  if (n_cached) *n_cached = n - (uint32_t)miss.size();
+  if (!miss.empty()) {
+    gg_packed* pk = nullptr;
+    gg_status s_ = gg_pack_files(miss.data(), (uint32_t)miss.size(), c->k, 0, &pk);
+    if (s_ != GG_OK) return fail(c, s_, g_thread_err);
+    struct Free {
+      gg_packed* p;
+      ~Free() { gg_packed_free(p); }
+    } guard{pk};
+    uint32_t* d_words;
+    GG_HIP(c, scratch_t(c, "in_words", std::max<uint64_t>(pk->n_words, 1), &d_words));
+    if (pk->n_words)
+      GG_HIP(c, hipMemcpyAsync(d_words, pk->words, pk->n_words * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, st));
+    // all genomes missed: sketch straight into the output rows
+    uint64_t* d_m = d_out;
+    uint32_t* d_ml = d_lens;
+    if (miss.size() != n) {
+      GG_HIP(c, scratch_t(c, "sk_miss", miss.size() * s, &d_m));
+      GG_HIP(c, scratch_t(c, "sk_miss_lens", miss.size(), &d_ml));
+    }
+    GG_HIP(c, hipMemsetAsync(d_m, 0, miss.size() * s * sizeof(uint64_t), st));
+    s_ = sketch_core(c, d_words, pk->n_words, pk->runs, pk->n_runs, pk->n_genomes, d_m, d_ml, st);
+    if (s_ != GG_OK) return s_;
+    if (rows) {
+      std::vector<uint64_t> mrows(miss.size() * s);
+      std::vector<uint32_t> mlens(miss.size());
+      GG_HIP(c, hipMemcpyAsync(mrows.data(), d_m, mrows.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+      GG_HIP(c, hipMemcpyAsync(mlens.data(), d_ml, mlens.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      GG_HIP(c, hipStreamSynchronize(st));
+      for (size_t m = 0; m < miss.size(); ++m) {
+        memcpy(rows + (size_t)miss_at[m] * s, &mrows[m * s], s * sizeof(uint64_t));
+        lens[miss_at[m]] = mlens[m];
+        if (cache_dir) (void)cache_store(cache_dir, miss[m], c->k, s, c->seed, &mrows[m * s], mlens[m]);
+      }
+    }
+    if (miss.size() == n) return GG_OK;  // rows already on the device
+  }
+  GG_HIP(c, hipMemcpyAsync(d_out, rows, (size_t)n * s * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  GG_HIP(c, hipMemcpyAsync(d_lens, lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  GG_HIP(c, hipStreamSynchronize(st));
+  return GG_OK;
+}
+
 }  // namespace
 
 double ani_f64(uint32_t common, uint32_t total, int k) {
@@ -826,8 +913,24 @@ gg_status gg_pairs(gg_ctx* ctx, const uint64_t* sketches, const uint32_t* lens, 
   return GG_OK;
 }
 
-gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
-                              float min_ani, gg_pair** pairs, float** ani, uint64_t* n_out) {
+gg_status gg_sketch_files(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
+                          const char* cache_dir, uint64_t* out_hashes, uint32_t* out_lens,
+                          uint32_t* n_cached) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (n_paths && (!paths || !out_hashes || !out_lens))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_sketch_files: null argument");
+  if (n_cached) *n_cached = 0;
+  if (n_paths == 0) return GG_OK;
+  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
+  uint64_t* d_out;
+  uint32_t* d_lens;
+  return sketch_paths(ctx, paths, n_paths, cache_dir, ctx->stream, &d_out, &d_lens, out_hashes, out_lens,
+                      n_cached);
+}
+
+gg_status gg_precluster_files_cached(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
+                                     float min_ani, const char* cache_dir, gg_pair** pairs,
+                                     float** ani, uint64_t* n_out, uint32_t* n_cached) {
   if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
   if (!pairs || !ani || !n_out || (n_paths && !paths))
     return fail(ctx, GG_ERR_INVALID_ARG, "gg_precluster_files: null argument");
@@ -835,32 +938,26 @@ gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths, uint32_t n_
   *pairs = nullptr;
   *ani = nullptr;
   *n_out = 0;
-  gg_packed* pk = nullptr;
-  gg_status s = gg_pack_files(paths, n_paths, ctx->k, 0, &pk);
-  if (s != GG_OK) return fail(ctx, s, g_thread_err);
-  struct Free {
-    gg_packed* p;
-    ~Free() { gg_packed_free(p); }
-  } guard{pk};
+  if (n_cached) *n_cached = 0;
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
   hipStream_t st = ctx->stream;
-  const uint32_t ng = pk->n_genomes;
   std::vector<gg_pair> res;
-  if (ng >= 2) {
-    uint32_t* d_words;
+  if (n_paths >= 2 || cache_dir) {
     uint64_t* d_out;
     uint32_t* d_lens;
-    GG_HIP(ctx, scratch_t(ctx, "in_words", std::max<uint64_t>(pk->n_words, 1), &d_words));
-    GG_HIP(ctx, scratch_t(ctx, "sk_out", (size_t)ng * ctx->s, &d_out));
-    GG_HIP(ctx, scratch_t(ctx, "sk_lens", ng, &d_lens));
-    if (pk->n_words)
-      GG_HIP(ctx, hipMemcpyAsync(d_words, pk->words, pk->n_words * sizeof(uint32_t),
-                                 hipMemcpyHostToDevice, st));
-    GG_HIP(ctx, hipMemsetAsync(d_out, 0, (size_t)ng * ctx->s * sizeof(uint64_t), st));
-    s = sketch_core(ctx, d_words, pk->n_words, pk->runs, pk->n_runs, ng, d_out, d_lens, st);
+    gg_status s = sketch_paths(ctx, paths, n_paths, cache_dir, st, &d_out, &d_lens, nullptr, nullptr,
+                               n_cached);
     if (s != GG_OK) return s;
-    s = pairs_to_host(ctx, d_out, d_lens, ng, min_ani, res, st);
-    if (s != GG_OK) return s;
+    if (n_paths >= 2) {
+      s = pairs_to_host(ctx, d_out, d_lens, n_paths, min_ani, res, st);
+      if (s != GG_OK) return s;
+    }
+  } else {
+    // one genome: no pairs, but the file must still parse (src/finch.rs:50)
+    gg_packed* pk = nullptr;
+    gg_status s = gg_pack_files(paths, n_paths, ctx->k, 0, &pk);
+    if (s != GG_OK) return fail(ctx, s, g_thread_err);
+    gg_packed_free(pk);
   }
   std::vector<float> a(res.size());
   for (size_t i = 0; i < res.size(); ++i) a[i] = gg_ani_f32(res[i].common, res[i].total, ctx->k);
@@ -875,6 +972,11 @@ gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths, uint32_t n_
   }
   *n_out = res.size();
   return GG_OK;
+}
+
+gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
+                              float min_ani, gg_pair** pairs, float** ani, uint64_t* n_out) {
+  return gg_precluster_files_cached(ctx, paths, n_paths, min_ani, nullptr, pairs, ani, n_out, nullptr);
 }
 
 double gg_ani_f64(uint32_t common, uint32_t total, int kmer_length) {

@@ -155,6 +155,12 @@ hipError_t launch_synth_mixed(uint32_t first_genome, uint32_t n_genomes, const u
 // api.cpp helpers used by pack.cpp
 void set_thread_error(const std::string& msg);
 
+// sketch_cache.cpp
+void cache_load_many(const char* dir, const char* const* paths, uint32_t n, int k, uint32_t s,
+                     uint64_t seed, uint64_t* rows, uint32_t* lens, uint8_t* hit);
+gg_status cache_store(const char* dir, const char* path, int k, uint32_t s, uint64_t seed,
+                      const uint64_t* hashes, uint32_t len);
+
 // host arithmetic (api.cpp)
 double ani_f64(uint32_t common, uint32_t total, int k);
 std::vector<uint32_t> build_cmin(uint32_t s, int k, float min_ani);

@@ -169,6 +169,38 @@ gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths,
                               uint32_t n_paths, float min_ani, gg_pair** pairs,
                               float** ani, uint64_t* n_out);
 
+/* ---- sketch cache --------------------------------- */
+/* galah sketches every genome on every run (src/finch.rs:47); these entry
+ * points keep per-genome sketches on disk so a repeated run over the same
+ * files skips ingest and K1 for them.  One entry per (genome file, k) in
+ * cache_dir, valid while the file's resolved path, size and mtime and the
+ * hash seed are unchanged; an entry computed with sketch size S serves any
+ * s <= S (bottom-s is a prefix of bottom-S).  Results are identical with and
+ * without the cache.  Format: galah_amd/csrc/sketch_cache.cpp. */
+
+/* *hit = 1 and out_hashes[0..*out_len) filled when a valid entry exists,
+ * else *hit = 0 (absent, stale, other parameters or corrupt).  Host only. */
+gg_status gg_sketch_cache_load(const char* cache_dir, const char* path, int kmer_length,
+                               uint32_t sketch_size, uint64_t hash_seed, uint64_t* out_hashes,
+                               uint32_t* out_len, int* hit);
+/* Writes (atomically replaces) the entry of path; hashes strictly ascending,
+ * len <= sketch_size.  Creates cache_dir when missing.  Host only. */
+gg_status gg_sketch_cache_store(const char* cache_dir, const char* path, int kmer_length,
+                                uint32_t sketch_size, uint64_t hash_seed, const uint64_t* hashes,
+                                uint32_t len);
+/* finch::sketch_files (src/finch.rs:47) for files: out_hashes is
+ * n_paths * sketch_size (row padded with 0 after out_lens[g]).  cache_dir
+ * may be NULL (no cache); otherwise cached genomes are read from it and
+ * the rest sketched on the device and stored (a failed store does not fail
+ * the call).  *n_cached (may be NULL) receives the number of cache hits. */
+gg_status gg_sketch_files(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
+                          const char* cache_dir, uint64_t* out_hashes, uint32_t* out_lens,
+                          uint32_t* n_cached);
+/* gg_precluster_files with a sketch cache directory (NULL = none). */
+gg_status gg_precluster_files_cached(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
+                                     float min_ani, const char* cache_dir, gg_pair** pairs,
+                                     float** ani, uint64_t* n_out, uint32_t* n_cached);
+
 /* ---- after distances(): preclusters -------- */
 /* src/clusterer.rs:409-431 partition_sketches (single linkage over the
  * pairs the cache contains) + :45-57 (each set sorted ascending, sets
