@@ -30,8 +30,11 @@
 namespace gg {
 namespace {
 
-constexpr int kSeg = 32;        // k-mer positions per lane per segment
 constexpr int kGroup = 4;       // k-mers per tau-check branch
+// k-mer positions per lane per segment: as many as one 64-base window holds
+// (k = 21: 44), capped to bound the unrolled code
+template <int K>
+constexpr int seg_len() { return ((65 - K) / kGroup) * kGroup < 48 ? ((65 - K) / kGroup) * kGroup : 48; }
 constexpr int kBlock = 256;
 // min waves per SIMD forced on the register allocator (8 = 64 VGPRs; the
 // k = 21 body then spills a few dwords and runs ~1% slower than at 66 VGPRs)
@@ -54,6 +57,21 @@ __device__ __forceinline__ uint64_t rotl64(uint64_t x) {
   const uint32_t nh = __builtin_amdgcn_alignbit(hi, lo, 32 - r);
   const uint32_t nl = __builtin_amdgcn_alignbit(lo, hi, 32 - r);
   return ((uint64_t)nh << 32) | nl;
+}
+
+// rotl(x, 31) + y: the two v_alignbit_b32 halves feed a 32-bit add/addc
+// pair directly (hipcc otherwise splits the rotate into two 64-bit adds and
+// a move to re-pair the halves).
+__device__ __forceinline__ uint64_t add_rotl31(uint64_t x, uint64_t y) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  const uint32_t nh = __builtin_amdgcn_alignbit(hi, lo, 1);
+  const uint32_t nl = __builtin_amdgcn_alignbit(lo, hi, 1);
+  uint32_t rl, rh;
+  asm("v_add_co_u32 %0, vcc, %2, %4\n\tv_addc_co_u32 %1, vcc, %3, %5, vcc"
+      : "=&v"(rl), "=v"(rh)
+      : "v"(nl), "v"(nh), "v"((uint32_t)y), "v"((uint32_t)(y >> 32))
+      : "vcc");
+  return ((uint64_t)rh << 32) | rl;
 }
 
 // fmix64 without its final k ^= k >> 33, which leaves the high word alone
@@ -128,7 +146,7 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
     k1 = rotl64<31>(k1); k1 *= c2; h1 ^= k1;
     h1 = rotl64<27>(h1); h1 += h2; h1 = times5_plus(h1, 0x52dce729);
     k2 = rotl64<33>(k2); k2 *= c1; h2 ^= k2;
-    h2 = rotl64<31>(h2); h2 += h1; h2 = times5_plus(h2, 0x38495ab5);
+    h2 = add_rotl31(h2, h1); h2 = times5_plus(h2, 0x38495ab5);
   }
   if (S::TAIL_TAB) {
     const uint32_t w = S::NBLK ? lo : hi;
@@ -259,7 +277,8 @@ __device__ __forceinline__ uint32_t window32(const uint32_t (&w)[4], int t) {
 // piece (i >= cnt) are hashed but never inserted.
 template <int K, bool SEED0>
 __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_kernel(SketchLaunch a) {
-  static_assert(K >= 1 && K <= 32 && kSeg + K - 1 <= 64, "window");
+  constexpr int kSeg = seg_len<K>();
+  static_assert(K >= 1 && K <= 32 && kSeg + K - 1 <= 64 && kSeg % kGroup == 0, "window");
   __shared__ uint64_t mtab[HashShape<K>::TAB_U64];  // murmur word tables (hash_parts)
   build_tables<K>(mtab);
   __syncthreads();
@@ -318,20 +337,24 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
         for (int j = 0; j < kGroup; ++j)
           any |= (uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr;
         if (any) {
-          uint64_t h[kGroup];
+          // rare (a lane of the wave has a k-mer whose high-word sum can
+          // reach tau): finish the exact test per candidate k-mer only
           uint32_t pending = 0;
 #pragma unroll
-          for (int j = 0; j < kGroup; ++j) {
-            h[j] = fmix_last(f1[j]) + fmix_last(f2[j]);
-            pending |= ((h[j] <= tau) & ((uint32_t)(g * kGroup + j) < cnt)) ? (1u << j) : 0u;
-          }
+          for (int j = 0; j < kGroup; ++j)
+            pending |= (((uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr) &
+                        ((uint32_t)(g * kGroup + j) < cnt)) ? (1u << j) : 0u;
           while (pending) {
             const int j = __builtin_ctz(pending);
             pending &= pending - 1;
-            uint64_t hv = h[0];
+            uint64_t a1 = f1[0], a2 = f2[0];
 #pragma unroll
-            for (int q = 1; q < kGroup; ++q) hv = (j == q) ? h[q] : hv;
-            insert_candidate(gset, cap_mask, a.flags + slot, hv);
+            for (int q = 1; q < kGroup; ++q) {
+              a1 = (j == q) ? f1[q] : a1;
+              a2 = (j == q) ? f2[q] : a2;
+            }
+            const uint64_t hv = fmix_last(a1) + fmix_last(a2);
+            if (hv <= tau) insert_candidate(gset, cap_mask, a.flags + slot, hv);
           }
         }
       }
