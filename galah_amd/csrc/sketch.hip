@@ -102,10 +102,14 @@ struct HashShape {
   static constexpr int NBLK = K / 16;             // full 16-byte blocks
   static constexpr int TAIL = K % 16;             // tail bytes
   static constexpr bool TAIL_TAB = TAIL >= 1 && TAIL <= kTailMaxBases;
-  // groups that need a group table (all but the tail word's when TAIL_TAB)
-  static constexpr int NG = TAIL_TAB ? 4 * NBLK : NW;
+  // per full block: two k1 group tables of 16-byte entries, two k2 group
+  // tables of 8-byte entries (u64 units)
+  static constexpr int BLK_U64 = 2 * 512 + 2 * 256;
+  // tail: a whole-word table, or one 8-byte group table per tail group
+  static constexpr int TAIL_GROUPS = TAIL_TAB ? 0 : NW - 4 * NBLK;
   static constexpr int TAIL_ENTRIES = TAIL_TAB ? (1 << (2 * TAIL)) : 0;
-  static constexpr int TAB_U64 = NG * 256 + TAIL_ENTRIES;
+  static constexpr int TAIL_BASE = NBLK * BLK_U64;
+  static constexpr int TAB_U64 = TAIL_BASE + TAIL_GROUPS * 256 + TAIL_ENTRIES;
 };
 
 // 8-bit code of bases 4q..4q+3 of a top-aligned MSB-first k-mer code
@@ -126,6 +130,15 @@ __device__ __forceinline__ uint32_t group_byte(uint32_t hi, uint32_t lo, int q) 
 //   w * c = T[2i][g_2i] + T[2i+1][g_2i+1]      (mod 2^64)
 // with g_q the 8-bit code of bases 4q..4q+3 and
 //   T[q][g] = ascii4(g) * (c << 32*(q & 1))  (bytes past K masked out).
+// T[odd q] has a zero low word, so hi(w * c) = hi(T[2i]) + hi(T[2i+1]).
+//
+// A block's k1 word continues as rotl(x, 31) * c2 with x = k1 * c1.  The
+// rotate's halves x << 31 and x >> 33 have disjoint bits, so
+//   rotl(x, 31) * c2 = x * (c2 << 31) + (hi(x) >> 1) * c2     (mod 2^64)
+// and x * (c2 << 31) is again a sum of two table entries: the k1 group
+// tables hold {T[q][g] * (c2 << 31), hi(T[q][g])} (16 bytes), and the
+// rotate + full multiply become one 32 x 64-bit multiply-add.
+//
 // A tail k1 word of <= 5 bases (k = 21: bases 16..20) is a function of at
 // most 10 bits, so its whole contribution rotl(w * c1, 31) * c2, and the
 // final h1 ^= len, is one table entry.  Tables live in LDS
@@ -139,28 +152,34 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
   uint64_t h1 = seed, h2 = seed;
 #pragma unroll
   for (int b = 0; b < S::NBLK; ++b) {
-    uint64_t k1 = tab[(4 * b) * 256 + group_byte(hi, lo, 4 * b)] +
-                  tab[(4 * b + 1) * 256 + group_byte(hi, lo, 4 * b + 1)];  // = k1 * c1
-    uint64_t k2 = tab[(4 * b + 2) * 256 + group_byte(hi, lo, 4 * b + 2)] +
-                  tab[(4 * b + 3) * 256 + group_byte(hi, lo, 4 * b + 3)];  // = k2 * c2
-    k1 = rotl64<31>(k1); k1 *= c2; h1 ^= k1;
+    const uint64_t* bt = tab + b * S::BLK_U64;
+    const ulonglong2 e0 = *(const ulonglong2*)(bt + 2 * group_byte(hi, lo, 4 * b));
+    const ulonglong2 e1 = *(const ulonglong2*)(bt + 512 + 2 * group_byte(hi, lo, 4 * b + 1));
+    uint64_t k2 = bt[1024 + group_byte(hi, lo, 4 * b + 2)] +
+                  bt[1280 + group_byte(hi, lo, 4 * b + 3)];  // = k2 * c2
+    // rotl(k1 * c1, 31) * c2
+    const uint32_t v = ((uint32_t)e0.y + (uint32_t)e1.y) >> 1;
+    uint64_t k1 = (uint64_t)v * (uint32_t)c2 + (e0.x + e1.x);
+    k1 += (uint64_t)(v * (uint32_t)(c2 >> 32)) << 32;
+    h1 ^= k1;
     h1 = rotl64<27>(h1); h1 += h2; h1 = times5_plus(h1, 0x52dce729);
     k2 = rotl64<33>(k2); k2 *= c1; h2 ^= k2;
     h2 = add_rotl31(h2, h1); h2 = times5_plus(h2, 0x38495ab5);
   }
+  const uint64_t* tt = tab + S::TAIL_BASE;
   if (S::TAIL_TAB) {
     const uint32_t w = S::NBLK ? lo : hi;
-    h1 ^= tab[S::NG * 256 + (w >> (32 - 2 * S::TAIL))];  // includes ^= len
+    h1 ^= tt[w >> (32 - 2 * S::TAIL)];  // includes ^= len
   } else {
     constexpr int q0 = 4 * S::NBLK;  // first group of the tail
     if (S::TAIL > 8) {
-      uint64_t k2 = tab[(q0 + 2) * 256 + group_byte(hi, lo, q0 + 2)];
-      if (q0 + 3 < S::NW) k2 += tab[(q0 + 3) * 256 + group_byte(hi, lo, q0 + 3)];
+      uint64_t k2 = tt[2 * 256 + group_byte(hi, lo, q0 + 2)];
+      if (q0 + 3 < S::NW) k2 += tt[3 * 256 + group_byte(hi, lo, q0 + 3)];
       k2 = rotl64<33>(k2); k2 *= c1; h2 ^= k2;
     }
     if (S::TAIL > 0) {
-      uint64_t k1 = tab[q0 * 256 + group_byte(hi, lo, q0)];
-      if (q0 + 1 < S::NW) k1 += tab[(q0 + 1) * 256 + group_byte(hi, lo, q0 + 1)];
+      uint64_t k1 = tt[group_byte(hi, lo, q0)];
+      if (q0 + 1 < S::NW) k1 += tt[256 + group_byte(hi, lo, q0 + 1)];
       k1 = rotl64<31>(k1); k1 *= c2; h1 ^= k1;
     }
     h1 ^= (uint64_t)K;
@@ -183,19 +202,38 @@ __device__ __forceinline__ uint64_t ascii_msb(uint32_t codes, int width, int nba
   return v;
 }
 
+// T[q][g] of hash_parts: group q (bases 4q..4q+3, those past K masked out)
+// as its word's bytes times the word's first multiplier
+template <int K>
+__device__ __forceinline__ uint64_t group_term(int q, uint32_t g) {
+  const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  const int nb = min(4, K - 4 * q);                  // valid bases of the group
+  const uint64_t cw = ((q >> 1) & 1) ? c2 : c1;      // k1 words: c1, k2 words: c2
+  return (ascii_msb(g, 4, nb) << (32 * (q & 1))) * cw;
+}
+
 template <int K>
 __device__ __forceinline__ void build_tables(uint64_t* tab) {
   using S = HashShape<K>;
   const uint64_t c1 = 0x87c37b91114253d5ull, c2 = 0x4cf5ad432745937full;
+  const uint64_t c2r = c2 << 31;
   for (uint32_t i = threadIdx.x; i < (uint32_t)S::TAB_U64; i += blockDim.x) {
-    if (i < (uint32_t)S::NG * 256) {
-      const uint32_t q = i >> 8, g = i & 255u;
-      const int nb = min(4, K - 4 * (int)q);                // valid bases of the group
-      const uint64_t cw = ((q >> 1) & 1u) ? c2 : c1;      // k1 words: c1, k2 words: c2
-      tab[i] = (ascii_msb(g, 4, nb) << (32 * (q & 1u))) * cw;
+    if (i < (uint32_t)S::TAIL_BASE) {
+      const uint32_t b = i / S::BLK_U64, r = i % S::BLK_U64;
+      if (r < 1024) {  // k1 groups: {T * (c2 << 31), hi(T)}
+        const uint32_t q = 4 * b + (r >> 9), g = (r & 511u) >> 1;
+        const uint64_t t = group_term<K>((int)q, g);
+        tab[i] = (r & 1u) ? (t >> 32) : t * c2r;
+      } else {  // k2 groups: T
+        const uint32_t q = 4 * b + 2 + ((r - 1024) >> 8), g = (r - 1024) & 255u;
+        tab[i] = group_term<K>((int)q, g);
+      }
+    } else if (!S::TAIL_TAB) {
+      const uint32_t r = i - (uint32_t)S::TAIL_BASE;
+      tab[i] = group_term<K>(4 * S::NBLK + (int)(r >> 8), r & 255u);
     } else {
       // whole tail k1 word: bases 16*NBLK .. +TAIL-1 -> rotl(w * c1, 31) * c2 ^ len
-      const uint32_t x = i - (uint32_t)S::NG * 256;
+      const uint32_t x = i - (uint32_t)S::TAIL_BASE;
       const uint64_t w = ascii_msb(x, S::TAIL, S::TAIL);
       tab[i] = (rotl64<31>(w * c1) * c2) ^ (uint64_t)K;
     }
@@ -279,7 +317,7 @@ template <int K, bool SEED0>
 __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_kernel(SketchLaunch a) {
   constexpr int kSeg = seg_len<K>();
   static_assert(K >= 1 && K <= 32 && kSeg + K - 1 <= 64 && kSeg % kGroup == 0, "window");
-  __shared__ uint64_t mtab[HashShape<K>::TAB_U64];  // murmur word tables (hash_parts)
+  __shared__ __attribute__((aligned(16))) uint64_t mtab[HashShape<K>::TAB_U64];  // murmur word tables (hash_parts)
   build_tables<K>(mtab);
   __syncthreads();
 
