@@ -305,6 +305,22 @@ __device__ __forceinline__ uint32_t window32(const uint32_t (&w)[4], int t) {
   return __builtin_amdgcn_alignbit(x, y, 32 - 2 * sh);
 }
 
+// 64 bits of the base stream starting at base t, top-aligned, of which the
+// top 2K bits are exact (the k-mer starting at t).  pair[a] = w[a]:w[a+1].
+// When the k-mer lies inside one pair (2 * (t % 16) + 2K <= 64) that is one
+// full-rate v_lshlrev_b64 (or nothing); otherwise two v_alignbit_b32.
+template <int K>
+__device__ __forceinline__ uint64_t window64(const uint32_t (&w)[4], const uint64_t (&pair)[4], int t) {
+  const int a = t >> 4, sh = t & 15;
+  if (sh == 0) return pair[a];
+  if (sh <= 32 - K) {
+    uint64_t r;
+    asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "i"(2 * sh), "v"(pair[a]));
+    return r;
+  }
+  return ((uint64_t)window32(w, t) << 32) | window32(w, t + 16);
+}
+
 // Each lane owns kSeg consecutive k-mer positions.  For every maximal piece
 // of the segment inside one run it loads the 64-base window starting at the
 // piece's first base (5 words, funnel-shifted to the base offset) and its
@@ -358,6 +374,12 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
         F[j] = off ? __builtin_amdgcn_alignbit(w[j], w[j + 1], 32 - 2 * off) : w[j];
 #pragma unroll
       for (int m = 0; m < 4; ++m) R[m] = revcomp16(F[3 - m]);
+      uint64_t FP[4], RP[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        FP[m] = ((uint64_t)F[m] << 32) | (m + 1 < 4 ? F[m + 1] : 0u);
+        RP[m] = ((uint64_t)R[m] << 32) | (m + 1 < 4 ? R[m + 1] : 0u);
+      }
 
 #pragma unroll
       for (int g = 0; g < kSeg / kGroup; ++g) {
@@ -365,9 +387,9 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
           const int i = g * kGroup + j;
-          const uint64_t fwd = ((uint64_t)window32(F, i) << 32) | window32(F, i + 16);
+          const uint64_t fwd = window64<K>(F, FP, i);
           const int t0 = 64 - K - i;  // reverse complement of k-mer i starts here
-          const uint64_t rev = ((uint64_t)window32(R, t0) << 32) | window32(R, t0 + 16);
+          const uint64_t rev = window64<K>(R, RP, t0);
           hash_parts<K>(fwd < rev ? fwd : rev, mtab, seed, f1[j], f2[j]);
         }
         bool any = false;

@@ -87,6 +87,17 @@ __global__ __launch_bounds__(256) void ubench(uint32_t* out, uint32_t seed) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) x ^= b[q];
       a1 ^= x;
+    } else if (OP == 8) {  // v_lshlrev_b64 x8
+      asm volatile(
+          "v_lshlrev_b64 %0, 3, %0\n v_lshlrev_b64 %1, 3, %1\n v_lshlrev_b64 %2, 3, %2\n v_lshlrev_b64 %3, 3, %3\n"
+          "v_lshlrev_b64 %0, 5, %0\n v_lshlrev_b64 %1, 5, %1\n v_lshlrev_b64 %2, 5, %2\n v_lshlrev_b64 %3, 5, %3\n"
+          : "+v"(w0), "+v"(w1), "+v"(w2), "+v"(w3));
+    } else if (OP == 9) {  // v_cndmask_b32 x8 (vcc mask)
+      asm volatile(
+          "v_cndmask_b32 %0, %0, %1, vcc\n v_cndmask_b32 %1, %1, %2, vcc\n v_cndmask_b32 %2, %2, %3, vcc\n"
+          "v_cndmask_b32 %3, %3, %4, vcc\n v_cndmask_b32 %4, %4, %5, vcc\n v_cndmask_b32 %5, %5, %6, vcc\n"
+          "v_cndmask_b32 %6, %6, %7, vcc\n v_cndmask_b32 %7, %7, %0, vcc\n"
+          : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
     } else if (OP == 5) {  // v_mul_hi_u32 x8
       asm volatile(
           "v_mul_hi_u32 %0, %0, %8\n v_mul_hi_u32 %1, %1, %8\n v_mul_hi_u32 %2, %2, %8\n v_mul_hi_u32 %3, %3, %8\n"
@@ -132,6 +143,8 @@ int main() {
   run<2>("v_mad_u64_u32", d_out, n_cu);
   run<3>("v_lshl_add_u64", d_out, n_cu);
   run<4>("v_alignbit_b32", d_out, n_cu);
+  run<8>("v_lshlrev_b64", d_out, n_cu);
+  run<9>("v_cndmask_b32", d_out, n_cu);
   run<6>("v_add_u32 x16 chains", d_out, n_cu);
   run<7>("v_mul_lo_u32 x16 chains", d_out, n_cu);
   run<6>("v_add_u32 x16 chains", d_out, n_cu, 1);
