@@ -102,9 +102,11 @@ struct HashShape {
   static constexpr int NBLK = K / 16;             // full 16-byte blocks
   static constexpr int TAIL = K % 16;             // tail bytes
   static constexpr bool TAIL_TAB = TAIL >= 1 && TAIL <= kTailMaxBases;
-  // per full block: two k1 group tables of 16-byte entries, two k2 group
-  // tables of 8-byte entries (u64 units)
-  static constexpr int BLK_U64 = 2 * 512 + 2 * 256;
+  // per full block (u64 units): k1 group tables of 16-byte {T * (c2 << 31),
+  // hi(T)} and 8-byte {hi(T * (c2 << 31)), hi(T)} entries (the second group's
+  // T has a zero low word, so has its product), k2 group tables of 8-byte T
+  // and 4-byte hi(T) entries
+  static constexpr int BLK_U64 = 512 + 256 + 256 + 128;
   // tail: a whole-word table, or one 8-byte group table per tail group
   static constexpr int TAIL_GROUPS = TAIL_TAB ? 0 : NW - 4 * NBLK;
   static constexpr int TAIL_ENTRIES = TAIL_TAB ? (1 << (2 * TAIL)) : 0;
@@ -136,8 +138,10 @@ __device__ __forceinline__ uint32_t group_byte(uint32_t hi, uint32_t lo, int q) 
 // rotate's halves x << 31 and x >> 33 have disjoint bits, so
 //   rotl(x, 31) * c2 = x * (c2 << 31) + (hi(x) >> 1) * c2     (mod 2^64)
 // and x * (c2 << 31) is again a sum of two table entries: the k1 group
-// tables hold {T[q][g] * (c2 << 31), hi(T[q][g])} (16 bytes), and the
-// rotate + full multiply become one 32 x 64-bit multiply-add.
+// tables hold {T[q][g] * (c2 << 31), hi(T[q][g])}, and the rotate + full
+// multiply become one 32 x 64-bit multiply-add.  Entries of odd groups have
+// zero low words and are stored as their high words only (4 bytes less LDS
+// traffic each; the LDS pipe runs at ~40% in this kernel).
 //
 // A tail k1 word of <= 5 bases (k = 21: bases 16..20) is a function of at
 // most 10 bits, so its whole contribution rotl(w * c1, 31) * c2, and the
@@ -154,12 +158,13 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
   for (int b = 0; b < S::NBLK; ++b) {
     const uint64_t* bt = tab + b * S::BLK_U64;
     const ulonglong2 e0 = *(const ulonglong2*)(bt + 2 * group_byte(hi, lo, 4 * b));
-    const ulonglong2 e1 = *(const ulonglong2*)(bt + 512 + 2 * group_byte(hi, lo, 4 * b + 1));
-    uint64_t k2 = bt[1024 + group_byte(hi, lo, 4 * b + 2)] +
-                  bt[1280 + group_byte(hi, lo, 4 * b + 3)];  // = k2 * c2
+    const uint2 e1 = *(const uint2*)(bt + 512 + group_byte(hi, lo, 4 * b + 1));
+    const uint64_t t2 = bt[768 + group_byte(hi, lo, 4 * b + 2)];
+    const uint32_t t3 = ((const uint32_t*)(bt + 1024))[group_byte(hi, lo, 4 * b + 3)];
+    uint64_t k2 = t2 + ((uint64_t)t3 << 32);  // = k2 * c2
     // rotl(k1 * c1, 31) * c2
-    const uint32_t v = ((uint32_t)e0.y + (uint32_t)e1.y) >> 1;
-    uint64_t k1 = (uint64_t)v * (uint32_t)c2 + (e0.x + e1.x);
+    const uint32_t v = ((uint32_t)e0.y + e1.y) >> 1;
+    uint64_t k1 = (uint64_t)v * (uint32_t)c2 + (e0.x + ((uint64_t)e1.x << 32));
     k1 += (uint64_t)(v * (uint32_t)(c2 >> 32)) << 32;
     h1 ^= k1;
     h1 = rotl64<27>(h1); h1 += h2; h1 = times5_plus(h1, 0x52dce729);
@@ -220,13 +225,18 @@ __device__ __forceinline__ void build_tables(uint64_t* tab) {
   for (uint32_t i = threadIdx.x; i < (uint32_t)S::TAB_U64; i += blockDim.x) {
     if (i < (uint32_t)S::TAIL_BASE) {
       const uint32_t b = i / S::BLK_U64, r = i % S::BLK_U64;
-      if (r < 1024) {  // k1 groups: {T * (c2 << 31), hi(T)}
-        const uint32_t q = 4 * b + (r >> 9), g = (r & 511u) >> 1;
-        const uint64_t t = group_term<K>((int)q, g);
+      if (r < 512) {  // k1 group 4b: {T * (c2 << 31), hi(T)}
+        const uint64_t t = group_term<K>((int)(4 * b), r >> 1);
         tab[i] = (r & 1u) ? (t >> 32) : t * c2r;
-      } else {  // k2 groups: T
-        const uint32_t q = 4 * b + 2 + ((r - 1024) >> 8), g = (r - 1024) & 255u;
-        tab[i] = group_term<K>((int)q, g);
+      } else if (r < 768) {  // k1 group 4b+1: {hi(T * (c2 << 31)), hi(T)}
+        const uint64_t t = group_term<K>((int)(4 * b + 1), r - 512);
+        tab[i] = ((t * c2r) >> 32) | (t & 0xFFFFFFFF00000000ull);
+      } else if (r < 1024) {  // k2 group 4b+2: T
+        tab[i] = group_term<K>((int)(4 * b + 2), r - 768);
+      } else {  // k2 group 4b+3: hi(T), two entries per u64
+        const uint32_t g = 2 * (r - 1024);
+        tab[i] = (group_term<K>((int)(4 * b + 3), g) >> 32) |
+                 (group_term<K>((int)(4 * b + 3), g + 1) & 0xFFFFFFFF00000000ull);
       }
     } else if (!S::TAIL_TAB) {
       const uint32_t r = i - (uint32_t)S::TAIL_BASE;
