@@ -42,7 +42,7 @@ N_SIMD = 256 * 4       # 256 CUs x 4 SIMDs
 # launch (profiles/r01_pmc_k1_k2gate.txt).  Ceiling = 1024 SIMDs x 2.4 GHz x 64
 # lanes / (4 cycles x VALU per k-mer).
 K1_CYCLES_PER_VALU = 4
-K1_VALU_PER_KMER = 3.294e10 / (29999800000 / 64)
+K1_VALU_PER_KMER = 3.247e10 / (29999800000 / 64)
 K1_PEAK_GKMER = N_SIMD * CLK_GHZ * 64 / (K1_CYCLES_PER_VALU * K1_VALU_PER_KMER)  # Gkmer/s
 # K2 (pairs: gate_lo32 + gate_build + pairs_gate kernels) is also priced
 # against VALU issue: SQ_INSTS_VALU of the three kernels per evaluated pair
@@ -56,7 +56,7 @@ K2_PMC_HBM_BYTES_C3 = (5.586e6 + 7.706e4 + 3.907e4) * 1024 * 2
 LDS_PEAK_GBS = 256 * 256 * CLK_GHZ
 # HBM bytes per K1 launch on this workload from the PMC pass (FETCH_SIZE x 2,
 # the gfx950 correction of MI355X_MICROARCH.md), profiles/r01_pmc_k1_k2gate.txt
-K1_PMC_HBM_BYTES_C3 = 3.849e6 * 1024 * 2
+K1_PMC_HBM_BYTES_C3 = 3.85e6 * 1024 * 2
 
 
 def parse():
