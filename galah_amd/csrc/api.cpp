@@ -164,7 +164,9 @@ struct SketchGeom {
 
 SketchGeom sketch_geom(uint32_t s) {
   SketchGeom g;
-  g.limit = std::min<uint32_t>(kSortCap, std::max<uint32_t>(4 * s, 64));
+  // ~1.6 s candidates expected at s = 1000 (sd ~ 40): the set never reaches
+  // the limit and the LDS sort never exceeds 2048 entries
+  g.limit = std::min<uint32_t>(kSortCap, std::max<uint32_t>(2 * s, 64));
   g.sort_pow2 = 1;
   while (g.sort_pow2 < g.limit) g.sort_pow2 <<= 1;
   g.cap_log2 = 1;
