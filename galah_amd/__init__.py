@@ -347,10 +347,13 @@ class Context:
         if not self._c:
             raise _thread_err(st.value)
         self.k, self.s, self.seed = k, sketch_size, seed
+        # held by the instance: module globals may already be None when a
+        # Context is collected at interpreter shutdown
+        self._destroy = _L.gg_destroy
 
     def close(self):
         if getattr(self, "_c", None):
-            _L.gg_destroy(self._c)
+            self._destroy(self._c)
             self._c = None
 
     def __del__(self):

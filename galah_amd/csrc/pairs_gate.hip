@@ -37,6 +37,7 @@
 // Bound: VALU issue of the gate loop (~10 instructions per 64 column
 // hashes, shared by R rows) and L2 bandwidth for the streamed columns.
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "device_util.hpp"
@@ -405,7 +406,13 @@ GateParams gate_params(uint32_t s) {
   // LDS, so gate misses are rarer and a table walk is one L2 round trip.
   // Small sketches: a one-bit gate in 2^19 bits (cheaper per hash) and a
   // directory of ~2-key buckets in HBM.
-  g.wide = s >= 2048;
+  // GALAHGPU_GATE_WIDE_MIN_S: sketch size from which the wide regime is
+  // used (default 2048; for A/B runs only, results do not depend on it)
+  static const uint32_t wide_min = [] {
+    const char* e = getenv("GALAHGPU_GATE_WIDE_MIN_S");
+    return e && *e ? (uint32_t)strtoul(e, nullptr, 10) : 2048u;
+  }();
+  g.wide = s >= wide_min;
   if (g.wide) {
     g.nb = std::min<uint32_t>(4096, std::max<uint32_t>(64, pow2_at_least((g.cap + 7) / 8)));
     g.bm_words = std::min<uint32_t>(1u << 13, std::max<uint32_t>(128, pow2_at_least((uint64_t)g.cap * 8) / 32));
