@@ -39,10 +39,13 @@ N_SIMD = 256 * 4       # 256 CUs x 4 SIMDs
 # scripts/ubench_valu.hip, profiles/r01_ubench_valu.txt).  K1's VALU count per
 # k-mer (all of the kernel: hashing, windows, segment setup, candidate
 # inserts) is SQ_INSTS_VALU / (k-mers / 64) from the PMC pass over the C3
-# launch (profiles/r01_pmc_k1_k2gate.txt).  Ceiling = 1024 SIMDs x 2.4 GHz x 64
-# lanes / (4 cycles x VALU per k-mer).
+# launch (profiles/r01_pmc_k1_grid112.txt).  Ceiling = 1024 SIMDs x 2.4 GHz x 64
+# lanes / (4 cycles x VALU per k-mer).  Since the K1 grid went to 112
+# workgroups per CU the kernel reads at ~1.0 of this ceiling (52.1 ms against
+# 53.4 ms): it is at the VALU issue limit to within the accuracy of this
+# model (PMC instruction count, nominal clock, 4 cycles for every VALU op).
 K1_CYCLES_PER_VALU = 4
-K1_VALU_PER_KMER = 3.247e10 / (29999800000 / 64)
+K1_VALU_PER_KMER = 3.282e10 / (29999800000 / 64)
 K1_PEAK_GKMER = N_SIMD * CLK_GHZ * 64 / (K1_CYCLES_PER_VALU * K1_VALU_PER_KMER)  # Gkmer/s
 # K2 (pairs: gate_lo32 + gate_build + pairs_gate kernels) is also priced
 # against VALU issue: SQ_INSTS_VALU of the three kernels per evaluated pair
@@ -55,8 +58,8 @@ K2_PMC_HBM_BYTES_C3 = (5.586e6 + 7.706e4 + 3.907e4) * 1024 * 2
 # of LDS), reported for reference: the gate kernel does not merge.
 LDS_PEAK_GBS = 256 * 256 * CLK_GHZ
 # HBM bytes per K1 launch on this workload from the PMC pass (FETCH_SIZE x 2,
-# the gfx950 correction of MI355X_MICROARCH.md), profiles/r01_pmc_k1_k2gate.txt
-K1_PMC_HBM_BYTES_C3 = 3.85e6 * 1024 * 2
+# the gfx950 correction of MI355X_MICROARCH.md), profiles/r01_pmc_k1_grid112.txt
+K1_PMC_HBM_BYTES_C3 = 3.871e6 * 1024 * 2
 
 
 def parse():

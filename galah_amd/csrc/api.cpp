@@ -254,7 +254,17 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
 
   int n_cu = 256;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
-  const int grid = std::max(1, n_cu) * 8;
+  // K1 grid: many small workgroups per CU (112; each thread then owns ~60
+  // segments at C3) so the dispatcher balances the tail.  At 8 per CU the
+  // grid was 8 waves per SIMD against an occupancy of 7 (68 VGPRs) and the
+  // last eighth of the work ran as a second, thin round (C3 K1: 56.7 ms at
+  // 8, 54.4 at 14, 52.5 at 56, 52.2 at 112, 52.5 at 448).
+  // GALAHGPU_K1_WG_PER_CU overrides it for A/B runs.
+  static const int wg_per_cu = [] {
+    const char* e = getenv("GALAHGPU_K1_WG_PER_CU");
+    return e && *e ? std::max(1, atoi(e)) : 112;
+  }();
+  const int grid = std::max(1, n_cu) * wg_per_cu;
 
   uint64_t* d_table;
   uint32_t *d_flags, *d_status, *d_slot_list, *d_slot_genome;
