@@ -265,7 +265,9 @@ def main():
                       else None),
           "valu_per_kmer": K1_VALU_PER_KMER,
           "note": ("VALU-issue ceiling: %.1f VALU per wave64 k-mer (PMC) x %d cycles each, 1024 SIMDs at "
-                   "%.1f GHz; input is 0.25 B/k-mer, so the HBM fraction is small by design"
+                   "%.1f GHz; input is 0.25 B/k-mer, so the HBM fraction is small by design; a frac of ~1.0 or "
+                   "slightly above means the kernel is at the issue limit and the PMC count or the 4-cycle/nominal-"
+                   "clock model is a few percent off, not that the limit is exceeded"
                    % (K1_VALU_PER_KMER, K1_CYCLES_PER_VALU, CLK_GHZ))}
     c3 = a.config == "c3" and N == 10000 and glen == 3000000 and world == 1 and s == 1000
     k2 = {"kernel": "pairs_gate_kernel (+ gate_build_kernel, gate_lo32_kernel)", "bound": "valu", "unit": "Gpair/s",
