@@ -119,25 +119,28 @@ __global__ __launch_bounds__(kThreads) void gate_build_kernel(GateBuildLaunch a)
   const uint32_t row_end = min(min(row0 + p.R, (I + 1) * GG_PAIR_TILE), a.n);
   BlockView v = block_view(a.tables + (size_t)blk * p.block_bytes, p);
 
+  const uint32_t nrows = row0 < row_end ? row_end - row0 : 0;
+  if (tid < kGateRowsMax) {  // one thread per row: the loads overlap
+    uint32_t l = 0;
+    uint64_t last = 0;
+    if (tid < nrows) {
+      l = a.lens[row0 + tid];
+      if (l) last = a.sketches[(uint64_t)(row0 + tid) * a.stride + l - 1];
+    }
+    meta.len[tid] = l;
+    meta.last[tid] = last;
+  }
+  for (uint32_t i = tid; i < p.nb + p.bm_words; i += kThreads) sm[i] = 0;
+  __syncthreads();
   if (tid == 0) {
-    const uint32_t nrows = row0 < row_end ? row_end - row0 : 0;
     uint32_t acc = 0;
     for (uint32_t r = 0; r < kGateRowsMax; ++r) {
-      uint32_t l = 0;
-      uint64_t last = 0;
-      if (r < nrows) {
-        l = a.lens[row0 + r];
-        if (l) last = a.sketches[(uint64_t)(row0 + r) * a.stride + l - 1];
-      }
-      meta.len[r] = l;
-      meta.last[r] = last;
       pre[r] = acc;
-      acc += l;
+      acc += meta.len[r];
     }
     pre[kGateRowsMax] = acc;
     meta.nrows = nrows;
   }
-  for (uint32_t i = tid; i < p.nb + p.bm_words; i += kThreads) sm[i] = 0;
   __syncthreads();
   const uint32_t E = pre[kGateRowsMax];
   auto entry = [&](uint32_t e, uint32_t& r) {
