@@ -417,8 +417,23 @@ GateParams gate_params(uint32_t s) {
   }();
   g.wide = s >= wide_min;
   if (g.wide) {
-    g.nb = std::min<uint32_t>(4096, std::max<uint32_t>(64, pow2_at_least((g.cap + 7) / 8)));
-    g.bm_words = std::min<uint32_t>(1u << 13, std::max<uint32_t>(128, pow2_at_least((uint64_t)g.cap * 8) / 32));
+    // Keys per wide row block: up to 65535 (the 16-bit bucket starts), twice
+    // kGateCap.  More keys = more rows per block = fewer passes over each
+    // column's hashes, with a gate (2^19 bits) and directory twice as large
+    // (C5, s = 10000: R = 6 instead of 3, pairs 193.8 -> 95.5 ms).
+    // GALAHGPU_GATE_WIDE_CAP overrides it for A/B runs (results do not
+    // depend on it).
+    static const uint32_t wide_cap = [] {
+      const char* e = getenv("GALAHGPU_GATE_WIDE_CAP");
+      const uint32_t v = e && *e ? (uint32_t)strtoul(e, nullptr, 10) : 65535u;
+      return std::min<uint32_t>(65535u, std::max<uint32_t>(kGateCap, v));
+    }();
+    g.R = std::min<uint32_t>(kGateRowsMax, std::max<uint32_t>(1, wide_cap / std::max<uint32_t>(s, 1)));
+    g.G = (GG_PAIR_TILE + g.R - 1) / g.R;
+    g.cap = g.R * s;
+    const uint32_t big = g.cap > kGateCap ? 1u : 0u;
+    g.nb = std::min<uint32_t>(4096u << big, std::max<uint32_t>(64, pow2_at_least((g.cap + 7) / 8)));
+    g.bm_words = std::min<uint32_t>(1u << (13 + big), std::max<uint32_t>(128, pow2_at_least((uint64_t)g.cap * 8) / 32));
   } else {
     g.nb = std::min<uint32_t>(16384, std::max<uint32_t>(64, pow2_at_least((g.cap + 1) / 2)));
     g.bm_words = std::min<uint32_t>(1u << 14, std::max<uint32_t>(128, pow2_at_least((uint64_t)g.cap * 16) / 32));
