@@ -34,6 +34,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # GALAHGPU_LIB points at an alternate build (A/B kernel experiments)
 LIB_PATH = os.environ.get("GALAHGPU_LIB") or os.path.join(HERE, "lib", "libgalahgpu.so")
 
+GG_PAIR_TILE = 64  # include/galahgpu.h: pair tiles are 64 x 64
 PAIR_DTYPE = np.dtype([("i", np.uint32), ("j", np.uint32), ("common", np.uint32), ("total", np.uint32)])
 
 # every function include/galahgpu.h declares

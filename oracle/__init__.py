@@ -53,6 +53,10 @@ def lib():
         L.oracle_pairs_parallel.restype = ctypes.c_uint64
         L.oracle_pairs_parallel.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32,
                                             ctypes.c_int, ctypes.c_float, ctypes.c_int, u64p]
+        L.oracle_pair_list.restype = None
+        L.oracle_pair_list.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int]
         _lib = L
     return _lib
 
@@ -147,6 +151,25 @@ def pairs(sketches: np.ndarray, lens: np.ndarray, min_ani: float, k: int = 21, c
                              ("total", np.uint32), ("ani", np.float32)])
     out["i"], out["j"], out["common"], out["total"], out["ani"] = oi[:m], oj[:m], oc[:m], ot[:m], oa[:m]
     return out
+
+
+def pair_list(sketches, lens, pi, pj, threads=8):
+    """finch raw_distance (common, total) of the pairs (pi[x], pj[x])."""
+    sketches = np.ascontiguousarray(sketches, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens, dtype=np.int32)
+    pi = np.ascontiguousarray(pi, dtype=np.uint32)
+    pj = np.ascontiguousarray(pj, dtype=np.uint32)
+    oc = np.zeros(max(len(pi), 1), np.uint32)
+    ot = np.zeros(max(len(pi), 1), np.uint32)
+    lib().oracle_pair_list(_ptr(sketches), _ptr(lens), sketches.shape[1], _ptr(pi), _ptr(pj), len(pi),
+                           _ptr(oc), _ptr(ot), threads)
+    return oc[:len(pi)], ot[:len(pi)]
+
+
+def ani_array(common, total, k=21):
+    """oracle_ani over arrays (same f64 expression, element by element)."""
+    L = lib()
+    return np.array([L.oracle_ani(int(c), int(t), k) for c, t in zip(common, total)], dtype=np.float64)
 
 
 def pairs_parallel(sketches, lens, min_ani, k=21, threads=1):

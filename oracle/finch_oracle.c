@@ -575,6 +575,45 @@ static void* pair_worker(void* arg) {
   return NULL;
 }
 
+/* (common, total) of an explicit list of pairs (pi[x], pj[x]), on n_threads
+ * threads: the full-size parity tests check thousands of chosen pairs. */
+typedef struct {
+  const uint64_t* sk;
+  const int32_t* lens;
+  uint32_t stride;
+  const uint32_t *pi, *pj;
+  uint64_t begin, end;
+  uint32_t *oc, *ot;
+} list_job_t;
+
+static void* list_worker(void* arg) {
+  list_job_t* p = (list_job_t*)arg;
+  for (uint64_t x = p->begin; x < p->end; ++x) {
+    const uint32_t i = p->pi[x], j = p->pj[x];
+    uint64_t c, t;
+    oracle_raw_distance(p->sk + (size_t)i * p->stride, (uint32_t)p->lens[i],
+                        p->sk + (size_t)j * p->stride, (uint32_t)p->lens[j], &c, &t);
+    p->oc[x] = (uint32_t)c;
+    p->ot[x] = (uint32_t)t;
+  }
+  return NULL;
+}
+
+void oracle_pair_list(const uint64_t* sketches, const int32_t* lens, uint32_t stride,
+                      const uint32_t* pi, const uint32_t* pj, uint64_t n_pairs,
+                      uint32_t* out_common, uint32_t* out_total, int n_threads) {
+  if (n_threads < 1) n_threads = 1;
+  if (n_threads > 256) n_threads = 256;
+  list_job_t jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < n_threads; ++t) {
+    jobs[t] = (list_job_t){sketches, lens, stride, pi, pj, n_pairs * t / n_threads,
+                           n_pairs * (t + 1) / n_threads, out_common, out_total};
+    pthread_create(&th[t], NULL, list_worker, &jobs[t]);
+  }
+  for (int t = 0; t < n_threads; ++t) pthread_join(th[t], NULL);
+}
+
 uint64_t oracle_pairs_parallel(const uint64_t* sketches, const int32_t* lens,
                                uint32_t n, uint32_t stride, int k,
                                float min_ani, int n_threads,
