@@ -48,6 +48,8 @@ EXPORTED_SYMBOLS = (
     "gg_free", "gg_synth_clustered_device", "gg_timing_enable", "gg_timing_read",
     "gg_partition_preclusters", "gg_precluster_pairs", "gg_synth_mixed_lengths", "gg_synth_mixed_device",
     "gg_sketch_cache_load", "gg_sketch_cache_store", "gg_sketch_files", "gg_precluster_files_cached",
+    "gg_create_multi", "gg_device_count", "gg_device_ctx", "gg_set_host_threads", "gg_phase_times",
+    "gg_precluster_shards",
 )
 
 GG_OK = 0
@@ -62,6 +64,11 @@ class GalahGpuError(RuntimeError):
 
 class _Run(ctypes.Structure):
     _fields_ = [("genome", ctypes.c_uint32), ("len", ctypes.c_uint32), ("base", ctypes.c_uint64)]
+
+
+class _Shard(ctypes.Structure):
+    _fields_ = [("d_words", ctypes.c_void_p), ("n_words", ctypes.c_uint64), ("runs", ctypes.c_void_p),
+                ("n_runs", ctypes.c_uint64), ("n_genomes", ctypes.c_uint32)]
 
 
 class _Packed(ctypes.Structure):
@@ -103,6 +110,13 @@ _sig("gg_thread_last_error", ctypes.c_char_p, [])
 _sig("gg_create", _vp, [_i32, _u32, _u64, _i32, ctypes.POINTER(_i32)])
 _sig("gg_destroy", None, [_vp])
 _sig("gg_device", _i32, [_vp])
+_sig("gg_create_multi", _vp, [_i32, _u32, _u64, _vp, _u32, ctypes.POINTER(_i32)])
+_sig("gg_device_count", _u32, [_vp])
+_sig("gg_device_ctx", _vp, [_vp, _u32])
+_sig("gg_set_host_threads", _i32, [_vp, _i32])
+_sig("gg_phase_times", _i32, [_vp, _vp])
+_sig("gg_precluster_shards", _i32, [_vp, _vp, ctypes.c_float, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                    ctypes.POINTER(_u64)])
 _sig("gg_pack_files", _i32, [ctypes.POINTER(ctypes.c_char_p), _u32, _i32, _i32, ctypes.POINTER(ctypes.POINTER(_Packed))])
 _sig("gg_pack_records", _i32, [ctypes.POINTER(_vp), _vp, _vp, _u64, _u32, _i32, ctypes.POINTER(ctypes.POINTER(_Packed))])
 _sig("gg_packed_free", None, [ctypes.POINTER(_Packed)])
@@ -339,18 +353,31 @@ def _dev_ptr(t):
     return t if isinstance(t, int) else t.data_ptr()
 
 
-class Context:
-    """A gg_ctx: one HIP device, fixed k / sketch size / seed."""
+PHASES = ("sketch", "replicate", "pairs", "merge")  # gg_phase_times order
 
-    def __init__(self, k=21, sketch_size=1000, seed=0, device=-1):
+
+class Context:
+    """A gg_ctx: fixed k / sketch size / seed on one HIP device (device=...),
+    or on several (devices=[...] ordinals, repeats allowed; devices="all":
+    every visible device, or GALAHGPU_DEVICES when set)."""
+
+    def __init__(self, k=21, sketch_size=1000, seed=0, device=-1, devices=None, host_threads=0):
         st = _i32()
-        self._c = _L.gg_create(k, sketch_size, seed, device, ctypes.byref(st))
+        if devices is None:
+            self._c = _L.gg_create(k, sketch_size, seed, device, ctypes.byref(st))
+        elif devices == "all":
+            self._c = _L.gg_create_multi(k, sketch_size, seed, None, 0, ctypes.byref(st))
+        else:
+            arr = (ctypes.c_int * max(len(devices), 1))(*devices)
+            self._c = _L.gg_create_multi(k, sketch_size, seed, arr, len(devices), ctypes.byref(st))
         if not self._c:
             raise _thread_err(st.value)
         self.k, self.s, self.seed = k, sketch_size, seed
         # held by the instance: module globals may already be None when a
         # Context is collected at interpreter shutdown
         self._destroy = _L.gg_destroy
+        if host_threads:
+            self.set_host_threads(host_threads)
 
     def close(self):
         if getattr(self, "_c", None):
@@ -372,6 +399,68 @@ class Context:
     @property
     def device(self):
         return _L.gg_device(self._c)
+
+    @property
+    def device_count(self):
+        return _L.gg_device_count(self._c)
+
+    def member(self, i):
+        """Member i as a borrowed single-device handle (device-resident calls
+        on that member's device); valid while this Context lives."""
+        p = _L.gg_device_ctx(self._c, i)
+        if not p:
+            raise IndexError(i)
+        m = Context.__new__(Context)
+        m._c, m.k, m.s, m.seed = p, self.k, self.s, self.seed
+        m._destroy = lambda _p: None  # owned by self
+        m._owner = self
+        return m
+
+    def set_host_threads(self, n):
+        """galah --threads (CAP:1327-1332): host threads for file ingest (<= 0: default)."""
+        st = _L.gg_set_host_threads(self._c, int(n))
+        if st != GG_OK:
+            raise self._err(st)
+
+    def phase_times(self):
+        """Wall-clock ms of the last fused call's phases (PHASES)."""
+        out = np.zeros(len(PHASES), np.float64)
+        st = _L.gg_phase_times(self._c, _ptr(out))
+        if st != GG_OK:
+            raise self._err(st)
+        return dict(zip(PHASES, out.tolist()))
+
+    def precluster_shards(self, shards, min_ani):
+        """shards: one (d_words tensor, runs RUN_DTYPE array, n_genomes) per
+        member, device-resident on that member's device -> (pairs sorted by
+        (i, j), ani f32), genomes numbered shard after shard."""
+        if len(shards) != self.device_count:
+            raise ValueError("one shard per device")
+        keep = []
+        arr = (_Shard * len(shards))()
+        for x, (d_words, runs, ng) in enumerate(shards):
+            runs = np.ascontiguousarray(runs, dtype=RUN_DTYPE)
+            keep.append(runs)
+            arr[x].d_words = _dev_ptr(d_words)
+            arr[x].n_words = d_words.numel()
+            arr[x].runs = runs.ctypes.data
+            arr[x].n_runs = len(runs)
+            arr[x].n_genomes = int(ng)
+        pp, ap, cnt = _vp(), _vp(), _u64()
+        st = _L.gg_precluster_shards(self._c, arr, ctypes.c_float(min_ani), ctypes.byref(pp), ctypes.byref(ap),
+                                     ctypes.byref(cnt))
+        if st != GG_OK:
+            raise self._err(st)
+        return self._pairs_ani(pp, ap, cnt.value)
+
+    @staticmethod
+    def _pairs_ani(pp, ap, n):
+        if n:
+            ani = np.ctypeslib.as_array(ctypes.cast(ap, ctypes.POINTER(ctypes.c_float)), shape=(n,)).copy()
+        else:
+            ani = np.zeros(0, np.float32)
+        _L.gg_free(ap)
+        return _take_pairs(pp, n), ani
 
     def timing_enable(self, on=True):
         st = _L.gg_timing_enable(self._c, 1 if on else 0)
@@ -437,13 +526,7 @@ class Context:
         self.last_cached = hits.value
         if st != GG_OK:
             raise self._err(st)
-        n = cnt.value
-        if n:
-            ani = np.ctypeslib.as_array(ctypes.cast(ap, ctypes.POINTER(ctypes.c_float)), shape=(n,)).copy()
-        else:
-            ani = np.zeros(0, np.float32)
-        _L.gg_free(ap)
-        return _take_pairs(pp, n), ani
+        return self._pairs_ani(pp, ap, cnt.value)
 
     # -- device-resident API (torch tensors on this context's device) ---------
     def sketch_device(self, d_words, runs, n_genomes, d_out, d_lens, stream=None):
@@ -576,10 +659,12 @@ _CTX_CACHE = {}
 
 
 def _context(k, s, seed=0):
+    """Every visible GPU (or GALAHGPU_DEVICES), as FinchPreclusterer::distances
+    uses them; host ingest threads from GALAHGPU_THREADS / the affinity mask."""
     key = (k, s, seed)
     c = _CTX_CACHE.get(key)
     if c is None:
-        c = Context(k, s, seed)
+        c = Context(k, s, seed, devices="all")
         _CTX_CACHE[key] = c
     return c
 

@@ -14,42 +14,14 @@
 #include <string>
 #include <vector>
 
-#include "gg_internal.hpp"
+#include "context.hpp"
 
-struct gg_ctx {
-  int k = 21;
-  uint32_t s = 1000;
-  uint64_t seed = 0;
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::string err;
-  // grow-only device scratch, keyed by purpose
-  std::map<std::string, std::pair<void*, size_t>> scratch;
-  // cached cmin table
-  float cmin_key = -1.0f;
-  std::vector<uint32_t> cmin_host;
-  // per-kernel timing (gg_timing_enable)
-  struct Timed {
-    int kernel;
-    hipEvent_t a, b;
-    uint64_t work;
-  };
-  std::vector<gg::PairSeg> seg_host;
-  std::vector<uint64_t> kstart_host;
-  int pairs_kernel = 0;  // GALAHGPU_PAIRS_KERNEL: 0 gate (default), 1 table, 2 merge
-  std::vector<uint32_t> sufmin_host;
-  bool timing = false;
-  std::vector<Timed> timed;
-  std::vector<hipEvent_t> spare_events;
-};
 
 namespace gg {
 
 thread_local std::string g_thread_err;
 
 void set_thread_error(const std::string& msg) { g_thread_err = msg; }
-
-namespace {
 
 gg_status fail(gg_ctx* c, gg_status st, const std::string& msg) {
   if (c) c->err = msg;
@@ -62,13 +34,6 @@ gg_status hip_fail(gg_ctx* c, hipError_t e, const char* what) {
               std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define GG_HIP(ctx, expr)                                   \
-  do {                                                      \
-    hipError_t _e = (expr);                                 \
-    if (_e != hipSuccess) return hip_fail((ctx), _e, #expr); \
-  } while (0)
-
-// Grow-only scratch buffer owned by the context.
 hipError_t scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
   auto& e = c->scratch[key];
   if (e.second < bytes) {
@@ -86,6 +51,25 @@ hipError_t scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
   *out = e.first;
   return hipSuccess;
 }
+
+hipError_t pinned(gg_ctx* c, size_t bytes, void** out) {
+  if (c->pinned_bytes < bytes) {
+    if (c->pinned) {
+      hipError_t err = hipHostFree(c->pinned);
+      if (err != hipSuccess) return err;
+      c->pinned = nullptr;
+      c->pinned_bytes = 0;
+    }
+    const size_t want = std::max<size_t>(bytes, 1 << 20);
+    hipError_t err = hipHostMalloc(&c->pinned, want, hipHostMallocDefault);
+    if (err != hipSuccess) return err;
+    c->pinned_bytes = want;
+  }
+  *out = c->pinned;
+  return hipSuccess;
+}
+
+namespace {
 
 hipEvent_t take_event(gg_ctx* c) {
   if (!c->spare_events.empty()) {
@@ -133,14 +117,6 @@ uint64_t pairs_in_tiles(uint32_t n, uint64_t tb, uint64_t te) {
     }
   }
   return acc;
-}
-
-template <typename T>
-hipError_t scratch_t(gg_ctx* c, const char* key, size_t count, T** out) {
-  void* p = nullptr;
-  hipError_t e = scratch(c, key, count * sizeof(T), &p);
-  *out = (T*)p;
-  return e;
 }
 
 inline double rust_min(double a, double b) {
@@ -228,10 +204,11 @@ gg_status validate_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t
   return GG_OK;
 }
 
-// Core of K1 over device-resident packed words; runs are host metadata.
+}  // namespace
+
 gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, const gg_run* runs,
                       uint64_t n_runs, uint32_t n_genomes, uint64_t* d_out, uint32_t* d_lens,
-                      hipStream_t st) {
+                      const uint32_t* d_row_of, hipStream_t st) {
   gg_status vs = validate_runs(c, runs, n_runs, n_genomes, n_words);
   if (vs != GG_OK) return vs;
   if (n_genomes == 0) return GG_OK;
@@ -357,7 +334,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       GG_HIP(c, timed_launch(c, GG_KERNEL_FINALIZE, active.size(), st, [&] {
         return launch_sketch_finalize(d_slot_list, (uint32_t)active.size(), d_slot_genome, d_tau,
                                       d_table, geom.cap_log2, d_flags, c->s,
-                                      geom.sort_pow2, d_out, d_lens, d_status, st);
+                                      geom.sort_pow2, d_row_of, d_out, d_lens, d_status, st);
       }));
       std::vector<uint32_t> status(nb);
       GG_HIP(c, hipMemcpyAsync(status.data(), d_status, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -375,6 +352,8 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   }
   return GG_OK;
 }
+
+namespace {
 
 gg_status ensure_cmin(gg_ctx* c, float min_ani, uint32_t** d_cmin, uint32_t** d_sufmin, hipStream_t st) {
   const uint32_t tmax = 2 * c->s;
@@ -501,6 +480,8 @@ gg_status pairs_gate(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
   return GG_OK;
 }
 
+}  // namespace
+
 gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
                      uint64_t tb, uint64_t te, float min_ani, gg_pair* d_out, uint64_t cap,
                      uint64_t* d_count, hipStream_t st) {
@@ -554,9 +535,10 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
   return GG_OK;
 }
 
-// Device sketches -> sorted host pairs.
-gg_status pairs_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
-                        float min_ani, std::vector<gg_pair>& res, hipStream_t st) {
+gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
+                              uint64_t tb, uint64_t te, float min_ani, std::vector<gg_pair>& res,
+                              hipStream_t st) {
+  if (n < 2 || tb >= te) return GG_OK;
   uint64_t* d_count;
   GG_HIP(c, scratch_t(c, "pair_count", 1, &d_count));
   uint64_t cap = std::max<uint64_t>(1 << 20, (uint64_t)n * 16);
@@ -566,122 +548,24 @@ gg_status pairs_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens,
     gg_pair* d_out;
     GG_HIP(c, scratch_t(c, "pair_out", cap, &d_out));
     GG_HIP(c, hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
-    gg_status ps = pairs_core(c, d_sk, d_lens, n, 0, gg_pair_tiles(n), min_ani, d_out, cap, d_count, st);
+    gg_status ps = pairs_core(c, d_sk, d_lens, n, tb, te, min_ani, d_out, cap, d_count, st);
     if (ps != GG_OK) return ps;
     uint64_t cnt = 0;
     GG_HIP(c, hipMemcpyAsync(&cnt, d_count, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(c, hipStreamSynchronize(st));
     if (cnt <= cap) {
-      res.resize(cnt);
+      const size_t at = res.size();
+      res.resize(at + cnt);
       if (cnt) {
-        GG_HIP(c, hipMemcpyAsync(res.data(), d_out, cnt * sizeof(gg_pair), hipMemcpyDeviceToHost, st));
+        GG_HIP(c, hipMemcpyAsync(res.data() + at, d_out, cnt * sizeof(gg_pair), hipMemcpyDeviceToHost, st));
         GG_HIP(c, hipStreamSynchronize(st));
       }
-      std::sort(res.begin(), res.end(), [](const gg_pair& x, const gg_pair& y) {
-        return x.i != y.i ? x.i < y.i : x.j < y.j;
-      });
       return GG_OK;
     }
     cap = cnt;
   }
   return fail(c, GG_ERR_INTERNAL, "pair output sizing failed");
 }
-
-template <typename T>
-T* copy_out(const std::vector<T>& v) {
-  T* p = (T*)malloc(std::max<size_t>(v.size(), 1) * sizeof(T));
-  if (p && !v.empty()) memcpy(p, v.data(), v.size() * sizeof(T));
-  return p;
-}
-
-// Sketches of the genome files paths[0..n) in device rows d_out [n x s],
-// d_lens [n] (ctx scratch "sk_out", "sk_lens"), the body of finch's
-// sketch_files (src/finch.rs:47).  With a cache directory (SURVEY.md 8(f)
-// row 4, sketch_cache.cpp) genomes with a valid entry skip ingest and K1;
-// the others are packed, sketched and stored.  host_out / host_lens, when
-// given, receive the rows as well.  Cache writes that fail (read-only
-// directory, full disk) do not fail the call: the sketches are still exact.
-gg_status sketch_paths(gg_ctx* c, const char* const* paths, uint32_t n, const char* cache_dir,
-                       hipStream_t st, uint64_t** d_out_p, uint32_t** d_lens_p, uint64_t* host_out,
-                       uint32_t* host_lens, uint32_t* n_cached) {
-  const uint32_t s = c->s;
-  uint64_t* d_out;
-  uint32_t* d_lens;
-  GG_HIP(c, scratch_t(c, "sk_out", (size_t)std::max(n, 1u) * s, &d_out));
-  GG_HIP(c, scratch_t(c, "sk_lens", std::max(n, 1u), &d_lens));
-  *d_out_p = d_out;
-  *d_lens_p = d_lens;
-  if (n_cached) *n_cached = 0;
-  if (n == 0) return GG_OK;
-  std::vector<uint8_t> hit(n, 0);
-  std::vector<uint64_t> rows_own;
-  std::vector<uint32_t> lens_own;
-  uint64_t* rows = host_out;
-  uint32_t* lens = host_lens;
-  if (cache_dir) {
-    if (!rows) {
-      rows_own.assign((size_t)n * s, 0);
-      rows = rows_own.data();
-    }
-    if (!lens) {
-      lens_own.assign(n, 0);
-      lens = lens_own.data();
-    }
-    memset(rows, 0, (size_t)n * s * sizeof(uint64_t));
-    cache_load_many(cache_dir, paths, n, c->k, s, c->seed, rows, lens, hit.data());
-  }
-  std::vector<const char*> miss;
-  std::vector<uint32_t> miss_at;
-  for (uint32_t i = 0; i < n; ++i)
-    if (!hit[i]) {
-      miss.push_back(paths[i]);
-      miss_at.push_back(i);
-    }
-  if (n_cached) *n_cached = n - (uint32_t)miss.size();
-  if (!miss.empty()) {
-    gg_packed* pk = nullptr;
-    gg_status s_ = gg_pack_files(miss.data(), (uint32_t)miss.size(), c->k, 0, &pk);
-    if (s_ != GG_OK) return fail(c, s_, g_thread_err);
-    struct Free {
-      gg_packed* p;
-      ~Free() { gg_packed_free(p); }
-    } guard{pk};
-    uint32_t* d_words;
-    GG_HIP(c, scratch_t(c, "in_words", std::max<uint64_t>(pk->n_words, 1), &d_words));
-    if (pk->n_words)
-      GG_HIP(c, hipMemcpyAsync(d_words, pk->words, pk->n_words * sizeof(uint32_t),
-                               hipMemcpyHostToDevice, st));
-    // all genomes missed: sketch straight into the output rows
-    uint64_t* d_m = d_out;
-    uint32_t* d_ml = d_lens;
-    if (miss.size() != n) {
-      GG_HIP(c, scratch_t(c, "sk_miss", miss.size() * s, &d_m));
-      GG_HIP(c, scratch_t(c, "sk_miss_lens", miss.size(), &d_ml));
-    }
-    GG_HIP(c, hipMemsetAsync(d_m, 0, miss.size() * s * sizeof(uint64_t), st));
-    s_ = sketch_core(c, d_words, pk->n_words, pk->runs, pk->n_runs, pk->n_genomes, d_m, d_ml, st);
-    if (s_ != GG_OK) return s_;
-    if (rows) {
-      std::vector<uint64_t> mrows(miss.size() * s);
-      std::vector<uint32_t> mlens(miss.size());
-      GG_HIP(c, hipMemcpyAsync(mrows.data(), d_m, mrows.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-      GG_HIP(c, hipMemcpyAsync(mlens.data(), d_ml, mlens.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-      GG_HIP(c, hipStreamSynchronize(st));
-      for (size_t m = 0; m < miss.size(); ++m) {
-        memcpy(rows + (size_t)miss_at[m] * s, &mrows[m * s], s * sizeof(uint64_t));
-        lens[miss_at[m]] = mlens[m];
-        if (cache_dir) (void)cache_store(cache_dir, miss[m], c->k, s, c->seed, &mrows[m * s], mlens[m]);
-      }
-    }
-    if (miss.size() == n) return GG_OK;  // rows already on the device
-  }
-  GG_HIP(c, hipMemcpyAsync(d_out, rows, (size_t)n * s * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-  GG_HIP(c, hipMemcpyAsync(d_lens, lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  GG_HIP(c, hipStreamSynchronize(st));
-  return GG_OK;
-}
-
-}  // namespace
 
 double ani_f64(uint32_t common, uint32_t total, int k) {
   // finch distance(): J = common/total; mash = -ln(2J/(1+J))/k clamped to
@@ -792,6 +676,11 @@ gg_ctx* gg_create(int kmer_length, uint32_t sketch_size, uint64_t hash_seed, int
 
 void gg_destroy(gg_ctx* ctx) {
   if (!ctx) return;
+  for (gg_ctx* m : ctx->devs) gg_destroy(m);
+  if (!ctx->devs.empty()) {
+    delete ctx;
+    return;
+  }
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   for (auto& kv : ctx->scratch)
@@ -802,12 +691,16 @@ void gg_destroy(gg_ctx* ctx) {
   }
   for (hipEvent_t e : ctx->spare_events) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   delete ctx;
 }
 
-int gg_device(const gg_ctx* ctx) { return ctx ? ctx->device : -1; }
+int gg_device(const gg_ctx* ctx) {
+  if (!ctx) return -1;
+  return ctx->devs.empty() ? ctx->device : ctx->devs[0]->device;
+}
 
-gg_status gg_sketch_device(gg_ctx* ctx, const uint32_t* d_words, uint64_t n_words,
+static gg_status gg_sketch_device_one(gg_ctx* ctx, const uint32_t* d_words, uint64_t n_words,
                            const gg_run* runs, uint64_t n_runs, uint32_t n_genomes,
                            uint64_t* d_out, uint32_t* d_lens, void* stream) {
   if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
@@ -815,36 +708,16 @@ gg_status gg_sketch_device(gg_ctx* ctx, const uint32_t* d_words, uint64_t n_word
     return fail(ctx, GG_ERR_INVALID_ARG, "gg_sketch_device: null buffer");
   if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
   hipStream_t st = (hipStream_t)stream;  // NULL = the default stream
-  return sketch_core(ctx, d_words, n_words, runs, n_runs, n_genomes, d_out, d_lens, st);
+  return sketch_core(ctx, d_words, n_words, runs, n_runs, n_genomes, d_out, d_lens, nullptr, st);
 }
 
-gg_status gg_sketch(gg_ctx* ctx, const gg_packed* packed, uint64_t* out_hashes,
-                    uint32_t* out_lens) {
-  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
-  if (!packed || (packed->n_genomes && (!out_hashes || !out_lens)))
-    return fail(ctx, GG_ERR_INVALID_ARG, "gg_sketch: null buffer");
-  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
-  hipStream_t st = ctx->stream;
-  const uint32_t ng = packed->n_genomes;
-  if (ng == 0) return GG_OK;
-  uint32_t* d_words;
-  uint64_t* d_out;
-  uint32_t* d_lens;
-  GG_HIP(ctx, scratch_t(ctx, "in_words", std::max<uint64_t>(packed->n_words, 1), &d_words));
-  GG_HIP(ctx, scratch_t(ctx, "sk_out", (size_t)ng * ctx->s, &d_out));
-  GG_HIP(ctx, scratch_t(ctx, "sk_lens", ng, &d_lens));
-  if (packed->n_words)
-    GG_HIP(ctx, hipMemcpyAsync(d_words, packed->words, packed->n_words * sizeof(uint32_t),
-                               hipMemcpyHostToDevice, st));
-  GG_HIP(ctx, hipMemsetAsync(d_out, 0, (size_t)ng * ctx->s * sizeof(uint64_t), st));
-  gg_status s = sketch_core(ctx, d_words, packed->n_words, packed->runs, packed->n_runs, ng, d_out,
-                            d_lens, st);
-  if (s != GG_OK) return s;
-  GG_HIP(ctx, hipMemcpyAsync(out_hashes, d_out, (size_t)ng * ctx->s * sizeof(uint64_t),
-                             hipMemcpyDeviceToHost, st));
-  GG_HIP(ctx, hipMemcpyAsync(out_lens, d_lens, ng * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  GG_HIP(ctx, hipStreamSynchronize(st));
-  return GG_OK;
+gg_status gg_sketch_device(gg_ctx* ctx, const uint32_t* d_words, uint64_t n_words,
+                           const gg_run* runs, uint64_t n_runs, uint32_t n_genomes,
+                           uint64_t* d_out, uint32_t* d_lens, void* stream) {
+  gg_ctx* m = primary(ctx);
+  const gg_status st = gg_sketch_device_one(m, d_words, n_words, runs, n_runs, n_genomes, d_out, d_lens, stream);
+  if (st != GG_OK && m != ctx) ctx->err = m->err;
+  return st;
 }
 
 uint64_t gg_pair_tiles(uint32_t n) {
@@ -882,7 +755,7 @@ void gg_pair_partition(uint32_t n, uint32_t parts, uint32_t part, uint64_t* begi
   if (*end < *begin) *end = *begin;
 }
 
-gg_status gg_pairs_device(gg_ctx* ctx, const uint64_t* d_sketches, const uint32_t* d_lens,
+static gg_status gg_pairs_device_one(gg_ctx* ctx, const uint64_t* d_sketches, const uint32_t* d_lens,
                           uint32_t n, uint64_t tile_begin, uint64_t tile_end, float min_ani,
                           gg_pair* d_out, uint64_t out_cap, uint64_t* d_count, void* stream) {
   if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
@@ -895,100 +768,13 @@ gg_status gg_pairs_device(gg_ctx* ctx, const uint64_t* d_sketches, const uint32_
                     d_count, st);
 }
 
-gg_status gg_pairs(gg_ctx* ctx, const uint64_t* sketches, const uint32_t* lens, uint32_t n,
-                   float min_ani, gg_pair** out, uint64_t* n_out) {
-  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
-  if (!out || !n_out || (n && (!sketches || !lens)))
-    return fail(ctx, GG_ERR_INVALID_ARG, "gg_pairs: null buffer");
-  if (std::isnan(min_ani)) return fail(ctx, GG_ERR_INVALID_ARG, "min_ani is NaN");
-  *out = nullptr;
-  *n_out = 0;
-  for (uint32_t i = 0; i < n; ++i)
-    if (lens[i] > ctx->s) return fail(ctx, GG_ERR_INVALID_ARG, "sketch longer than sketch_size");
-  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
-  hipStream_t st = ctx->stream;
-  std::vector<gg_pair> res;
-  if (n >= 2) {
-    uint64_t* d_sk;
-    uint32_t* d_lens;
-    GG_HIP(ctx, scratch_t(ctx, "pin_sk", (size_t)n * ctx->s, &d_sk));
-    GG_HIP(ctx, scratch_t(ctx, "pin_lens", n, &d_lens));
-    GG_HIP(ctx, hipMemcpyAsync(d_sk, sketches, (size_t)n * ctx->s * sizeof(uint64_t),
-                               hipMemcpyHostToDevice, st));
-    GG_HIP(ctx, hipMemcpyAsync(d_lens, lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    gg_status s = pairs_to_host(ctx, d_sk, d_lens, n, min_ani, res, st);
-    if (s != GG_OK) return s;
-  }
-  *out = copy_out(res);
-  if (!*out) return fail(ctx, GG_ERR_OUT_OF_MEMORY, "out of host memory");
-  *n_out = res.size();
-  return GG_OK;
-}
-
-gg_status gg_sketch_files(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
-                          const char* cache_dir, uint64_t* out_hashes, uint32_t* out_lens,
-                          uint32_t* n_cached) {
-  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
-  if (n_paths && (!paths || !out_hashes || !out_lens))
-    return fail(ctx, GG_ERR_INVALID_ARG, "gg_sketch_files: null argument");
-  if (n_cached) *n_cached = 0;
-  if (n_paths == 0) return GG_OK;
-  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
-  uint64_t* d_out;
-  uint32_t* d_lens;
-  return sketch_paths(ctx, paths, n_paths, cache_dir, ctx->stream, &d_out, &d_lens, out_hashes, out_lens,
-                      n_cached);
-}
-
-gg_status gg_precluster_files_cached(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
-                                     float min_ani, const char* cache_dir, gg_pair** pairs,
-                                     float** ani, uint64_t* n_out, uint32_t* n_cached) {
-  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
-  if (!pairs || !ani || !n_out || (n_paths && !paths))
-    return fail(ctx, GG_ERR_INVALID_ARG, "gg_precluster_files: null argument");
-  if (std::isnan(min_ani)) return fail(ctx, GG_ERR_INVALID_ARG, "min_ani is NaN");
-  *pairs = nullptr;
-  *ani = nullptr;
-  *n_out = 0;
-  if (n_cached) *n_cached = 0;
-  if (hipSetDevice(ctx->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
-  hipStream_t st = ctx->stream;
-  std::vector<gg_pair> res;
-  if (n_paths >= 2 || cache_dir) {
-    uint64_t* d_out;
-    uint32_t* d_lens;
-    gg_status s = sketch_paths(ctx, paths, n_paths, cache_dir, st, &d_out, &d_lens, nullptr, nullptr,
-                               n_cached);
-    if (s != GG_OK) return s;
-    if (n_paths >= 2) {
-      s = pairs_to_host(ctx, d_out, d_lens, n_paths, min_ani, res, st);
-      if (s != GG_OK) return s;
-    }
-  } else {
-    // one genome: no pairs, but the file must still parse (src/finch.rs:50)
-    gg_packed* pk = nullptr;
-    gg_status s = gg_pack_files(paths, n_paths, ctx->k, 0, &pk);
-    if (s != GG_OK) return fail(ctx, s, g_thread_err);
-    gg_packed_free(pk);
-  }
-  std::vector<float> a(res.size());
-  for (size_t i = 0; i < res.size(); ++i) a[i] = gg_ani_f32(res[i].common, res[i].total, ctx->k);
-  *pairs = copy_out(res);
-  *ani = copy_out(a);
-  if (!*pairs || !*ani) {
-    free(*pairs);
-    free(*ani);
-    *pairs = nullptr;
-    *ani = nullptr;
-    return fail(ctx, GG_ERR_OUT_OF_MEMORY, "out of host memory");
-  }
-  *n_out = res.size();
-  return GG_OK;
-}
-
-gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
-                              float min_ani, gg_pair** pairs, float** ani, uint64_t* n_out) {
-  return gg_precluster_files_cached(ctx, paths, n_paths, min_ani, nullptr, pairs, ani, n_out, nullptr);
+gg_status gg_pairs_device(gg_ctx* ctx, const uint64_t* d_sketches, const uint32_t* d_lens,
+                          uint32_t n, uint64_t tile_begin, uint64_t tile_end, float min_ani,
+                          gg_pair* d_out, uint64_t out_cap, uint64_t* d_count, void* stream) {
+  gg_ctx* m = primary(ctx);
+  const gg_status st = gg_pairs_device_one(m, d_sketches, d_lens, n, tile_begin, tile_end, min_ani, d_out, out_cap, d_count, stream);
+  if (st != GG_OK && m != ctx) ctx->err = m->err;
+  return st;
 }
 
 double gg_ani_f64(uint32_t common, uint32_t total, int kmer_length) {
@@ -1017,6 +803,7 @@ void gg_free(void* p) { free(p); }
 
 gg_status gg_timing_enable(gg_ctx* ctx, int on) {
   if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  for (gg_ctx* m : ctx->devs) gg_timing_enable(m, on);
   for (auto& t : ctx->timed) {
     (void)hipEventSynchronize(t.b);
     ctx->spare_events.push_back(t.a);
@@ -1031,6 +818,14 @@ gg_status gg_timing_read(gg_ctx* ctx, int kernel, gg_kernel_stats* out) {
   if (!ctx || !out || kernel < 0 || kernel >= GG_KERNEL_COUNT)
     return fail(ctx, GG_ERR_INVALID_ARG, "gg_timing_read: bad argument");
   gg_kernel_stats s{0.0, 0, 0};
+  for (gg_ctx* m : ctx->devs) {  // a multi-device context sums its members
+    gg_kernel_stats x;
+    const gg_status st = gg_timing_read(m, kernel, &x);
+    if (st != GG_OK) return fail(ctx, st, m->err);
+    s.ms += x.ms;
+    s.launches += x.launches;
+    s.work += x.work;
+  }
   for (auto& t : ctx->timed) {
     if (t.kernel != kernel) continue;
     GG_HIP(ctx, hipEventSynchronize(t.b));
@@ -1044,7 +839,7 @@ gg_status gg_timing_read(gg_ctx* ctx, int kernel, gg_kernel_stats* out) {
   return GG_OK;
 }
 
-gg_status gg_synth_clustered_device(gg_ctx* ctx, uint32_t first_genome, uint32_t n_genomes, uint32_t genome_len,
+static gg_status gg_synth_clustered_device_one(gg_ctx* ctx, uint32_t first_genome, uint32_t n_genomes, uint32_t genome_len,
                                     uint32_t cluster_size, float max_sub_rate, uint64_t seed,
                                     uint32_t* d_words, gg_run* runs, void* stream) {
   if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
@@ -1055,6 +850,15 @@ gg_status gg_synth_clustered_device(gg_ctx* ctx, uint32_t first_genome, uint32_t
   GG_HIP(ctx, launch_synth(first_genome, n_genomes, genome_len, cluster_size, max_sub_rate, seed, d_words, st));
   for (uint32_t g = 0; g < n_genomes; ++g) runs[g] = gg_run{g, genome_len, (uint64_t)g * genome_len};
   return GG_OK;
+}
+
+gg_status gg_synth_clustered_device(gg_ctx* ctx, uint32_t first_genome, uint32_t n_genomes, uint32_t genome_len,
+                                    uint32_t cluster_size, float max_sub_rate, uint64_t seed,
+                                    uint32_t* d_words, gg_run* runs, void* stream) {
+  gg_ctx* m = primary(ctx);
+  const gg_status st = gg_synth_clustered_device_one(m, first_genome, n_genomes, genome_len, cluster_size, max_sub_rate, seed, d_words, runs, stream);
+  if (st != GG_OK && m != ctx) ctx->err = m->err;
+  return st;
 }
 
 static uint64_t splitmix_host(uint64_t x) {
@@ -1078,7 +882,7 @@ gg_status gg_synth_mixed_lengths(uint32_t first_genome, uint32_t n_genomes, uint
   return GG_OK;
 }
 
-gg_status gg_synth_mixed_device(gg_ctx* ctx, uint32_t first_genome, uint32_t n_genomes, const uint32_t* lens,
+static gg_status gg_synth_mixed_device_one(gg_ctx* ctx, uint32_t first_genome, uint32_t n_genomes, const uint32_t* lens,
                                 uint32_t cluster_size, float max_sub_rate, double n_run_rate, uint64_t seed,
                                 uint32_t* d_words, gg_run* runs, uint64_t runs_cap, uint64_t* n_runs, void* stream) {
   if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
@@ -1123,6 +927,15 @@ gg_status gg_synth_mixed_device(gg_ctx* ctx, uint32_t first_genome, uint32_t n_g
   *n_runs = nr;
   if (nr > runs_cap) return fail(ctx, GG_ERR_OUTPUT_FULL, "run buffer too small");
   return GG_OK;
+}
+
+gg_status gg_synth_mixed_device(gg_ctx* ctx, uint32_t first_genome, uint32_t n_genomes, const uint32_t* lens,
+                                uint32_t cluster_size, float max_sub_rate, double n_run_rate, uint64_t seed,
+                                uint32_t* d_words, gg_run* runs, uint64_t runs_cap, uint64_t* n_runs, void* stream) {
+  gg_ctx* m = primary(ctx);
+  const gg_status st = gg_synth_mixed_device_one(m, first_genome, n_genomes, lens, cluster_size, max_sub_rate, n_run_rate, seed, d_words, runs, runs_cap, n_runs, stream);
+  if (st != GG_OK && m != ctx) ctx->err = m->err;
+  return st;
 }
 
 }  // extern "C"

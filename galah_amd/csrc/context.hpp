@@ -1,0 +1,105 @@
+// The context behind the C ABI (gg_ctx) and the single-device building
+// blocks the entry points are made of (api.cpp), shared with the
+// multi-device orchestration (multi.cpp).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "gg_internal.hpp"
+
+// A context is either ONE device (devs empty: the fields below drive it) or
+// a multi-device context whose members devs[i] are single-device contexts
+// (one per entry of the device list; the same ordinal may appear more than
+// once, each entry then being its own shard with its own stream).
+struct gg_ctx {
+  int k = 21;
+  uint32_t s = 1000;
+  uint64_t seed = 0;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  // grow-only device scratch, keyed by purpose
+  std::map<std::string, std::pair<void*, size_t>> scratch;
+  // grow-only pinned host staging buffer (streamed ingest)
+  void* pinned = nullptr;
+  size_t pinned_bytes = 0;
+  // cached cmin table
+  float cmin_key = -1.0f;
+  std::vector<uint32_t> cmin_host;
+  // per-kernel timing (gg_timing_enable)
+  struct Timed {
+    int kernel;
+    hipEvent_t a, b;
+    uint64_t work;
+  };
+  std::vector<gg::PairSeg> seg_host;
+  std::vector<uint64_t> kstart_host;
+  int pairs_kernel = 0;  // GALAHGPU_PAIRS_KERNEL: 0 gate (default), 1 table, 2 merge
+  std::vector<uint32_t> sufmin_host;
+  bool timing = false;
+  std::vector<Timed> timed;
+  std::vector<hipEvent_t> spare_events;
+  // multi-device context: the members (owned)
+  std::vector<gg_ctx*> devs;
+  // host threads for file ingest (<= 0: gg_pack_files' default)
+  int host_threads = 0;
+  // wall-clock phases of the last fused call (GG_PHASE_*)
+  double phase_ms[GG_PHASE_COUNT] = {0};
+};
+
+namespace gg {
+
+// The member that single-device entry points use on a multi-device context.
+inline gg_ctx* primary(gg_ctx* c) { return c && !c->devs.empty() ? c->devs[0] : c; }
+
+gg_status fail(gg_ctx* c, gg_status st, const std::string& msg);
+gg_status hip_fail(gg_ctx* c, hipError_t e, const char* what);
+
+#define GG_HIP(ctx, expr)                                        \
+  do {                                                           \
+    hipError_t _e = (expr);                                      \
+    if (_e != hipSuccess) return ::gg::hip_fail((ctx), _e, #expr); \
+  } while (0)
+
+// Grow-only device scratch buffer owned by the context.
+hipError_t scratch(gg_ctx* c, const char* key, size_t bytes, void** out);
+template <typename T>
+hipError_t scratch_t(gg_ctx* c, const char* key, size_t count, T** out) {
+  void* p = nullptr;
+  hipError_t e = scratch(c, key, count * sizeof(T), &p);
+  *out = (T*)p;
+  return e;
+}
+// Grow-only pinned host buffer of the context (contents not preserved).
+hipError_t pinned(gg_ctx* c, size_t bytes, void** out);
+
+// K1 over device-resident packed words; runs are host metadata with genome
+// indices in [0, n_genomes).  Row g of d_out / entry g of d_lens receive
+// genome g, or genome g goes to row d_row_of[g] when d_row_of (device, n_genomes
+// entries) is given.  Synchronises st.
+gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, const gg_run* runs,
+                      uint64_t n_runs, uint32_t n_genomes, uint64_t* d_out, uint32_t* d_lens,
+                      const uint32_t* d_row_of, hipStream_t st);
+// K2 over tiles [tb, te) of n device sketches; appends to d_out / *d_count.
+gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
+                     uint64_t tb, uint64_t te, float min_ani, gg_pair* d_out, uint64_t cap,
+                     uint64_t* d_count, hipStream_t st);
+// K2 over tiles [tb, te), passing pairs appended to res (unsorted).
+gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
+                              uint64_t tb, uint64_t te, float min_ani, std::vector<gg_pair>& res,
+                              hipStream_t st);
+
+template <typename T>
+T* copy_out(const std::vector<T>& v) {
+  T* p = (T*)malloc(std::max<size_t>(v.size(), 1) * sizeof(T));
+  if (p && !v.empty()) memcpy(p, v.data(), v.size() * sizeof(T));
+  return p;
+}
+
+}  // namespace gg

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -51,7 +52,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   const uint64_t* tau, const uint64_t* table,
                                   uint32_t cap_log2,
                                   const uint32_t* flags, uint32_t s,
-                                  uint32_t sort_pow2, uint64_t* out,
+                                  uint32_t sort_pow2, const uint32_t* row_of, uint64_t* out,
                                   uint32_t* lens, uint32_t* status,
                                   hipStream_t st);
 
@@ -152,6 +153,49 @@ hipError_t launch_synth_mixed(uint32_t first_genome, uint32_t n_genomes, const u
                               uint64_t max_words, uint32_t cluster_size, float max_sub_rate, uint64_t seed,
                               uint32_t* words, hipStream_t st);
 
+// Size and mtime of a genome file, taken before it is read: a cache entry
+// is stored only if the file still has them afterwards.
+struct FileStamp {
+  uint64_t size = 0;
+  int64_t mtime_ns = 0;
+  bool ok = false;
+};
+bool file_stamp(const char* path, FileStamp* out);
+
+// pack.cpp: streaming ingest for gg_precluster_files / gg_sketch_files.
+// Files are read, gunzipped and packed on n_threads workers (<= 0: the
+// default of gg_pack_files) in index order; consumers take genome i with
+// get(i) (blocks until it is packed) and give its memory back with
+// release(i).  Workers stop taking new files while the packed, unreleased
+// genomes hold more than budget_bytes (the genome at the release frontier
+// is always taken), so host memory stays bounded whatever the file count.
+int ingest_threads(int n_threads);
+class PackStream {
+ public:
+  PackStream(const char* const* paths, uint32_t n, int k, int n_threads, uint64_t budget_bytes,
+             bool stamp_files = false);
+  ~PackStream();
+  PackStream(const PackStream&) = delete;
+  PackStream& operator=(const PackStream&) = delete;
+  // words: 2-bit packed bases of genome i from word 0; runs: its ACGT runs
+  // (base relative to word 0, genome field unused).  Valid until release(i).
+  gg_status get(uint32_t i, const std::vector<uint32_t>** words, const std::vector<gg_run>** runs,
+                std::string* err);
+  // The file's size and mtime as stat'ed just before it was read (valid
+  // after get(i) succeeded; the streams are built with stamp_files).
+  FileStamp stamp(uint32_t i);
+  void release(uint32_t i);
+  void abort();
+  // After an abort: joins the workers and returns the error of the lowest
+  // failing file index among the files read (every index below a failing
+  // one has been read), GG_OK if none failed.
+  gg_status first_error(std::string* err);
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> p_;
+};
+
 // api.cpp helpers used by pack.cpp
 void set_thread_error(const std::string& msg);
 
@@ -159,7 +203,7 @@ void set_thread_error(const std::string& msg);
 void cache_load_many(const char* dir, const char* const* paths, uint32_t n, int k, uint32_t s,
                      uint64_t seed, uint64_t* rows, uint32_t* lens, uint8_t* hit);
 gg_status cache_store(const char* dir, const char* path, int k, uint32_t s, uint64_t seed,
-                      const uint64_t* hashes, uint32_t len);
+                      const uint64_t* hashes, uint32_t len, const FileStamp* before);
 
 // host arithmetic (api.cpp)
 double ani_f64(uint32_t common, uint32_t total, int k);

@@ -1,0 +1,664 @@
+// Multi-device orchestration of the finch precluster path and the entry
+// points that use every device of a context (include/galahgpu.h).
+//
+// galah calls FinchPreclusterer::distances once, from one thread, for all
+// genomes (src/clusterer.rs:36; src/finch.rs:47 sketches every file, :53-73
+// compares every pair).  Inside that one call this library drives every
+// device of the context with one host thread each:
+//
+//   1. sketch   genomes are dealt to the devices (files: in batches pulled
+//               from a shared cursor as the host threads finish packing them;
+//               device-resident shards: one shard per device); K1 writes each
+//               genome's row into that device's full [n x s] sketch array
+//   2. gather   every device copies the rows it did not sketch from their
+//               owners (hipMemcpyPeerAsync: on an MI355X node every GPU has a
+//               direct xGMI link to every other, so the copies from the seven
+//               peers run on seven links at once; a ring all-gather would use
+//               two of them)
+//   3. pairs    device d runs K2 over part d of the upper-triangle tiles
+//               (gg_pair_partition: equal pair counts); passing pairs come
+//               back sparse
+//   4. merge    concatenate, sort by (i, j) (SortedPairGenomeDistanceCache
+//               order), f32 ANI per pair (src/finch.rs:56-70)
+//
+// The result never depends on the device list: every pair is evaluated by
+// exactly one device on identical sketch rows.
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <mutex>
+#include <new>
+#include <thread>
+
+#include "context.hpp"
+
+namespace gg {
+namespace {
+
+using Clock = std::chrono::steady_clock;
+double ms_since(Clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(Clock::now() - t0).count();
+}
+
+std::vector<gg_ctx*> members(gg_ctx* c) { return c->devs.empty() ? std::vector<gg_ctx*>{c} : c->devs; }
+
+// f(index, member) on one host thread per member (member 0 on the calling
+// thread), each bound to its member's device.  The lowest failing member's
+// status is returned and its message copied to c (and to the calling
+// thread's error slot: gg_thread_last_error is per thread).
+template <class F>
+gg_status on_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, F&& f) {
+  std::vector<gg_status> st(ms.size(), GG_OK);
+  auto run = [&](size_t i) {
+    if (hipSetDevice(ms[i]->device) != hipSuccess) {
+      st[i] = fail(ms[i], GG_ERR_HIP, "hipSetDevice failed");
+      return;
+    }
+    st[i] = f(i, ms[i]);
+  };
+  std::vector<std::thread> th;
+  for (size_t i = 1; i < ms.size(); ++i) th.emplace_back(run, i);
+  run(0);
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < ms.size(); ++i)
+    if (st[i] != GG_OK) {
+      if (ms[i] != c) c->err = ms[i]->err;
+      set_thread_error(c->err);
+      return st[i];
+    }
+  return GG_OK;
+}
+
+// A member's full sketch array: rows [n x s] u64 and lens [n].
+struct Rows {
+  uint64_t* sk = nullptr;
+  uint32_t* len = nullptr;
+};
+
+gg_status member_rows(gg_ctx* m, uint32_t n, Rows* r) {
+  GG_HIP(m, scratch_t(m, "mg_sk", (size_t)std::max(n, 1u) * m->s, &r->sk));
+  GG_HIP(m, scratch_t(m, "mg_len", std::max(n, 1u), &r->len));
+  return GG_OK;
+}
+
+// A run of consecutive rows sketched by member `owner`.
+struct RowSpan {
+  uint32_t row0, rows, owner;
+};
+
+// Spans of the sorted row list `rows` (all sketched by `owner`).
+void spans_of(std::vector<uint32_t>& rows, uint32_t owner, std::vector<RowSpan>& out) {
+  std::sort(rows.begin(), rows.end());
+  for (size_t a = 0; a < rows.size();) {
+    size_t b = a + 1;
+    while (b < rows.size() && rows[b] == rows[b - 1] + 1) ++b;
+    out.push_back(RowSpan{rows[a], (uint32_t)(b - a), owner});
+    a = b;
+  }
+}
+
+// Member mi copies every span it does not own from the owner's array.
+gg_status replicate(gg_ctx* m, size_t mi, const std::vector<gg_ctx*>& ms, const std::vector<Rows>& rows,
+                    const std::vector<RowSpan>& spans) {
+  const size_t s = m->s;
+  for (const RowSpan& sp : spans) {
+    if (sp.owner == mi) continue;
+    const gg_ctx* o = ms[sp.owner];
+    uint64_t* dsk = rows[mi].sk + (size_t)sp.row0 * s;
+    const uint64_t* ssk = rows[sp.owner].sk + (size_t)sp.row0 * s;
+    uint32_t* dl = rows[mi].len + sp.row0;
+    const uint32_t* sl = rows[sp.owner].len + sp.row0;
+    if (o->device == m->device) {
+      GG_HIP(m, hipMemcpyAsync(dsk, ssk, (size_t)sp.rows * s * sizeof(uint64_t), hipMemcpyDeviceToDevice, m->stream));
+      GG_HIP(m, hipMemcpyAsync(dl, sl, sp.rows * sizeof(uint32_t), hipMemcpyDeviceToDevice, m->stream));
+    } else {
+      GG_HIP(m, hipMemcpyPeerAsync(dsk, m->device, ssk, o->device, (size_t)sp.rows * s * sizeof(uint64_t), m->stream));
+      GG_HIP(m, hipMemcpyPeerAsync(dl, m->device, sl, o->device, sp.rows * sizeof(uint32_t), m->stream));
+    }
+  }
+  GG_HIP(m, hipStreamSynchronize(m->stream));
+  return GG_OK;
+}
+
+// Steps 2-4 over rows resident on every member: gather, pairs, merge.
+gg_status gather_pairs_merge(gg_ctx* c, const std::vector<gg_ctx*>& ms, const std::vector<Rows>& rows,
+                             const std::vector<RowSpan>& spans, uint32_t n, float min_ani,
+                             std::vector<gg_pair>& res) {
+  const size_t M = ms.size();
+  auto t0 = Clock::now();
+  if (M > 1) {
+    gg_status st = on_members(c, ms, [&](size_t i, gg_ctx* m) { return replicate(m, i, ms, rows, spans); });
+    if (st != GG_OK) return st;
+  }
+  c->phase_ms[GG_PHASE_REPLICATE] = ms_since(t0);
+  t0 = Clock::now();
+  std::vector<std::vector<gg_pair>> part(M);
+  gg_status st = on_members(c, ms, [&](size_t i, gg_ctx* m) {
+    uint64_t tb = 0, te = 0;
+    gg_pair_partition(n, (uint32_t)M, (uint32_t)i, &tb, &te);
+    return pairs_range_to_host(m, rows[i].sk, rows[i].len, n, tb, te, min_ani, part[i], m->stream);
+  });
+  if (st != GG_OK) return st;
+  c->phase_ms[GG_PHASE_PAIRS] = ms_since(t0);
+  t0 = Clock::now();
+  size_t total = 0;
+  for (auto& p : part) total += p.size();
+  res.clear();
+  res.reserve(total);
+  for (auto& p : part) res.insert(res.end(), p.begin(), p.end());
+  std::sort(res.begin(), res.end(), [](const gg_pair& x, const gg_pair& y) {
+    return x.i != y.i ? x.i < y.i : x.j < y.j;
+  });
+  c->phase_ms[GG_PHASE_MERGE] = ms_since(t0);
+  return GG_OK;
+}
+
+gg_status pairs_with_ani(gg_ctx* c, const std::vector<gg_pair>& res, gg_pair** pairs, float** ani,
+                         uint64_t* n_out) {
+  auto t0 = Clock::now();
+  std::vector<float> a(res.size());
+  for (size_t i = 0; i < res.size(); ++i) a[i] = gg_ani_f32(res[i].common, res[i].total, c->k);
+  *pairs = copy_out(res);
+  *ani = copy_out(a);
+  if (!*pairs || !*ani) {
+    free(*pairs);
+    free(*ani);
+    *pairs = nullptr;
+    *ani = nullptr;
+    return fail(c, GG_ERR_OUT_OF_MEMORY, "out of host memory");
+  }
+  *n_out = res.size();
+  c->phase_ms[GG_PHASE_MERGE] += ms_since(t0);
+  return GG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Streamed file ingest (the body of finch's sketch_files, src/finch.rs:47).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBatchGenomes = 32;          // genomes per K1 batch
+constexpr uint64_t kBatchWords = 64ull << 20;   // or 1 Gbases of packed words, whichever first
+
+// Sketches of paths[0..n) into every member's full array (rows[i]); spans
+// receives the rows each member sketched.  Genomes with a valid entry in
+// cache_dir are read from it (every member receives those rows from the
+// host); the others are packed on the host threads and sketched in batches
+// (each batch: pinned staging -> H2D -> K1 with a row map), and stored in
+// the cache.  host_out / host_lens (optional) receive the rows.
+gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const char* const* paths, uint32_t n,
+                               const char* cache_dir, std::vector<Rows>& rows, std::vector<RowSpan>& spans,
+                               uint64_t* host_out, uint32_t* host_lens, uint32_t* n_cached) {
+  const size_t M = ms.size();
+  const uint32_t s = c->s;
+  rows.assign(M, Rows{});
+  spans.clear();
+  if (n_cached) *n_cached = 0;
+  // cache lookups (host)
+  std::vector<uint8_t> hit(n, 0);
+  std::vector<uint64_t> hit_rows;
+  std::vector<uint32_t> hit_lens;
+  if (cache_dir) {
+    hit_rows.assign((size_t)n * s, 0);
+    hit_lens.assign(n, 0);
+    cache_load_many(cache_dir, paths, n, c->k, s, c->seed, hit_rows.data(), hit_lens.data(), hit.data());
+  }
+  std::vector<const char*> miss;
+  std::vector<uint32_t> miss_at;
+  for (uint32_t i = 0; i < n; ++i)
+    if (!hit[i]) {
+      miss.push_back(paths[i]);
+      miss_at.push_back(i);
+    }
+  if (n_cached) *n_cached = n - (uint32_t)miss.size();
+  std::vector<RowSpan> hit_spans;
+  {
+    std::vector<uint32_t> h;
+    for (uint32_t i = 0; i < n; ++i)
+      if (hit[i]) h.push_back(i);
+    spans_of(h, 0, hit_spans);
+  }
+  const uint32_t nm = (uint32_t)miss.size();
+  // in-flight packed genomes: ~2 batches per member, at least 1 GiB
+  const uint64_t budget = std::max<uint64_t>(1ull << 30, 2ull * M * kBatchWords * sizeof(uint32_t));
+  PackStream stream(miss.data(), nm, c->k, c->host_threads, budget, cache_dir != nullptr);
+  std::mutex cursor_mu;
+  uint32_t cursor = 0;
+  bool stop = false;        // a member failed: the others take no more batches
+  bool file_error = false;  // ... because a file did not read or parse
+  int first_fail = -1;      // member whose failure came first (not a file)
+  std::vector<std::vector<uint32_t>> owned(M);
+
+  auto body = [&](size_t mi, gg_ctx* m) -> gg_status {
+    Rows& r = rows[mi];
+    gg_status ms_ = member_rows(m, n, &r);
+    if (ms_ != GG_OK) return ms_;
+    GG_HIP(m, hipMemsetAsync(r.sk, 0, (size_t)n * s * sizeof(uint64_t), m->stream));
+    GG_HIP(m, hipMemsetAsync(r.len, 0, (size_t)n * sizeof(uint32_t), m->stream));
+    for (const RowSpan& sp : hit_spans) {  // cached rows straight from the host
+      GG_HIP(m, hipMemcpyAsync(r.sk + (size_t)sp.row0 * s, hit_rows.data() + (size_t)sp.row0 * s,
+                               (size_t)sp.rows * s * sizeof(uint64_t), hipMemcpyHostToDevice, m->stream));
+      GG_HIP(m, hipMemcpyAsync(r.len + sp.row0, hit_lens.data() + sp.row0, sp.rows * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, m->stream));
+    }
+    GG_HIP(m, hipStreamSynchronize(m->stream));
+    std::vector<gg_run> runs;
+    std::vector<uint32_t> row_of;
+    std::vector<uint64_t> out_rows;
+    std::vector<uint32_t> out_lens;
+    for (;;) {
+      uint32_t b0, b1;
+      {
+        std::lock_guard<std::mutex> lk(cursor_mu);
+        if (stop || cursor >= nm) break;
+        b0 = cursor;
+        b1 = std::min(nm, b0 + kBatchGenomes);
+        cursor = b1;
+      }
+      // assemble the batch in the pinned staging buffer
+      runs.clear();
+      row_of.clear();
+      uint64_t nw = 0;
+      uint32_t g = 0;
+      for (uint32_t i = b0; i < b1; ++i, ++g) {
+        const std::vector<uint32_t>* w;
+        const std::vector<gg_run>* rr;
+        std::string err;
+        const gg_status gs = stream.get(i, &w, &rr, &err);
+        if (gs != GG_OK) {
+          std::lock_guard<std::mutex> lk(cursor_mu);
+          if (!stop) file_error = true;  // (an abort caused by another member is not a file error)
+          return fail(m, gs, err);
+        }
+        void* stage;
+        const size_t need = (nw + w->size()) * sizeof(uint32_t);
+        if (need > m->pinned_bytes) {  // grow, keeping what is staged
+          std::vector<uint32_t> keep((const uint32_t*)m->pinned, (const uint32_t*)m->pinned + nw);
+          GG_HIP(m, pinned(m, std::max(need, std::min<size_t>(2 * need, kBatchWords * sizeof(uint32_t) * 2)), &stage));
+          if (nw) memcpy(stage, keep.data(), nw * sizeof(uint32_t));
+        }
+        stage = m->pinned;
+        if (!w->empty()) memcpy((uint32_t*)stage + nw, w->data(), w->size() * sizeof(uint32_t));
+        for (const gg_run& x : *rr) runs.push_back(gg_run{g, x.len, x.base + nw * 16});
+        row_of.push_back(miss_at[i]);
+        nw += w->size();
+        stream.release(i);
+        if (nw >= kBatchWords && i + 1 < b1) {  // large genomes: cut the batch here, return the rest
+          std::lock_guard<std::mutex> lk(cursor_mu);
+          if (cursor == b1) {
+            cursor = i + 1;
+            b1 = i + 1;
+          }
+        }
+      }
+      const uint32_t ng = b1 - b0;
+      uint32_t* d_words;
+      uint32_t* d_row_of;
+      GG_HIP(m, scratch_t(m, "stage_words", std::max<uint64_t>(nw, 1), &d_words));
+      GG_HIP(m, scratch_t(m, "row_of", ng, &d_row_of));
+      if (nw) GG_HIP(m, hipMemcpyAsync(d_words, m->pinned, nw * sizeof(uint32_t), hipMemcpyHostToDevice, m->stream));
+      GG_HIP(m, hipMemcpyAsync(d_row_of, row_of.data(), ng * sizeof(uint32_t), hipMemcpyHostToDevice, m->stream));
+      gg_status ks = sketch_core(m, d_words, nw, runs.data(), runs.size(), ng, r.sk, r.len, d_row_of, m->stream);
+      if (ks != GG_OK) return ks;
+      owned[mi].insert(owned[mi].end(), row_of.begin(), row_of.end());
+      if (cache_dir) {  // store the new sketches (a failed store fails nothing)
+        out_rows.resize((size_t)ng * s);
+        out_lens.resize(ng);
+        for (uint32_t q = 0; q < ng; ++q) {
+          GG_HIP(m, hipMemcpyAsync(&out_rows[(size_t)q * s], r.sk + (size_t)row_of[q] * s, s * sizeof(uint64_t),
+                                   hipMemcpyDeviceToHost, m->stream));
+          GG_HIP(m, hipMemcpyAsync(&out_lens[q], r.len + row_of[q], sizeof(uint32_t), hipMemcpyDeviceToHost, m->stream));
+        }
+        GG_HIP(m, hipStreamSynchronize(m->stream));
+        for (uint32_t q = 0; q < ng; ++q) {
+          const FileStamp fs = stream.stamp(b0 + q);
+          (void)cache_store(cache_dir, miss[b0 + q], c->k, s, c->seed, &out_rows[(size_t)q * s], out_lens[q], &fs);
+        }
+      }
+    }
+    return GG_OK;
+  };
+  gg_status st = on_members(c, ms, [&](size_t mi, gg_ctx* m) -> gg_status {
+    const gg_status r = body(mi, m);
+    if (r != GG_OK) {
+      {
+        std::lock_guard<std::mutex> lk(cursor_mu);
+        if (!file_error && first_fail < 0) first_fail = (int)mi;
+        stop = true;
+      }
+      stream.abort();  // wakes members waiting for genomes nobody will pack now
+    }
+    return r;
+  });
+  if (file_error) {  // report the lowest failing file, as a serial reader would meet it
+    std::string err;
+    const gg_status fs = stream.first_error(&err);
+    if (fs != GG_OK) return fail(c, fs, err);
+  }
+  if (first_fail >= 0 && ms[first_fail]->err.size()) {
+    const gg_status fs = st != GG_OK ? st : GG_ERR_INTERNAL;
+    return fail(c, fs, ms[first_fail]->err);
+  }
+  if (st != GG_OK) return st;
+  for (size_t mi = 0; mi < M; ++mi) spans_of(owned[mi], (uint32_t)mi, spans);
+  if (host_out || host_lens) {
+    // the caller wants the rows: every row is on its owner (or, cached, everywhere)
+    std::vector<RowSpan> all = spans;
+    all.insert(all.end(), hit_spans.begin(), hit_spans.end());
+    for (const RowSpan& sp : all) {
+      gg_ctx* o = ms[sp.owner];
+      if (hipSetDevice(o->device) != hipSuccess) return fail(c, GG_ERR_HIP, "hipSetDevice failed");
+      if (host_out)
+        GG_HIP(c, hipMemcpyAsync(host_out + (size_t)sp.row0 * s, rows[sp.owner].sk + (size_t)sp.row0 * s,
+                                 (size_t)sp.rows * s * sizeof(uint64_t), hipMemcpyDeviceToHost, o->stream));
+      if (host_lens)
+        GG_HIP(c, hipMemcpyAsync(host_lens + sp.row0, rows[sp.owner].len + sp.row0, sp.rows * sizeof(uint32_t),
+                                 hipMemcpyDeviceToHost, o->stream));
+    }
+    for (gg_ctx* o : ms) {
+      if (hipSetDevice(o->device) != hipSuccess) return fail(c, GG_ERR_HIP, "hipSetDevice failed");
+      GG_HIP(c, hipStreamSynchronize(o->stream));
+    }
+  }
+  return GG_OK;
+}
+
+// Contiguous genome ranges with about equal k-mer counts, one per member.
+std::vector<uint32_t> balance_genomes(const gg_run* runs, uint64_t n_runs, uint32_t n_genomes, int k, size_t M) {
+  std::vector<uint64_t> per(n_genomes + 1, 0);
+  for (uint64_t r = 0; r < n_runs; ++r) per[runs[r].genome + 1] += (uint64_t)runs[r].len - (uint64_t)k + 1;
+  for (uint32_t g = 0; g < n_genomes; ++g) per[g + 1] += per[g];
+  std::vector<uint32_t> cut(M + 1, n_genomes);
+  cut[0] = 0;
+  for (size_t m = 1; m < M; ++m) {
+    const long double target = (long double)per[n_genomes] * m / M;
+    uint32_t g = (uint32_t)(std::lower_bound(per.begin(), per.end(), (uint64_t)target) - per.begin());
+    cut[m] = std::max(cut[m - 1], std::min(g, n_genomes));
+  }
+  return cut;
+}
+
+}  // namespace
+}  // namespace gg
+
+using namespace gg;
+
+extern "C" {
+
+gg_ctx* gg_create_multi(int kmer_length, uint32_t sketch_size, uint64_t hash_seed, const int* devices,
+                        uint32_t n_devices, gg_status* status) {
+  gg_status dummy;
+  if (!status) status = &dummy;
+  std::vector<int> list;
+  if (devices) {
+    list.assign(devices, devices + n_devices);
+  } else {
+    int vis = 0;
+    if (hipGetDeviceCount(&vis) != hipSuccess || vis == 0) {
+      *status = fail(nullptr, GG_ERR_NO_DEVICE, "no HIP device visible (libgalahgpu has no CPU path)");
+      return nullptr;
+    }
+    const char* env = getenv("GALAHGPU_DEVICES");
+    if (n_devices == 0 && env && *env) {
+      for (const char* p = env; *p;) {
+        char* end = nullptr;
+        const long v = strtol(p, &end, 10);
+        if (end == p) {
+          *status = fail(nullptr, GG_ERR_INVALID_ARG, std::string("GALAHGPU_DEVICES: not a device list: ") + env);
+          return nullptr;
+        }
+        list.push_back((int)v);
+        p = (*end == ',') ? end + 1 : end;
+      }
+    } else {
+      const int want = n_devices ? (int)n_devices : vis;
+      if (want > vis) {
+        *status = fail(nullptr, GG_ERR_NO_DEVICE, "fewer devices visible than requested");
+        return nullptr;
+      }
+      for (int d = 0; d < want; ++d) list.push_back(d);
+    }
+  }
+  if (list.empty()) {
+    *status = fail(nullptr, GG_ERR_INVALID_ARG, "empty device list");
+    return nullptr;
+  }
+  if (list.size() == 1) return gg_create(kmer_length, sketch_size, hash_seed, list[0], status);
+  gg_ctx* c = new (std::nothrow) gg_ctx();
+  if (!c) {
+    *status = fail(nullptr, GG_ERR_OUT_OF_MEMORY, "out of host memory");
+    return nullptr;
+  }
+  c->k = kmer_length;
+  c->s = sketch_size;
+  c->seed = hash_seed;
+  for (int d : list) {
+    if (d < 0) {
+      gg_destroy(c);
+      *status = fail(nullptr, GG_ERR_INVALID_ARG, "negative device ordinal in the device list");
+      return nullptr;
+    }
+    gg_ctx* m = gg_create(kmer_length, sketch_size, hash_seed, d, status);
+    if (!m) {
+      const std::string e = gg_thread_last_error();
+      gg_destroy(c);
+      set_thread_error(e);
+      return nullptr;
+    }
+    c->devs.push_back(m);
+  }
+  c->device = list[0];
+  // direct xGMI peer access between every pair of distinct devices (a copy
+  // between devices without it is staged through the host)
+  for (int a : list)
+    for (int b : list) {
+      if (a == b) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can && hipSetDevice(a) == hipSuccess) {
+        const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+        if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+      }
+    }
+  (void)hipSetDevice(list[0]);
+  *status = GG_OK;
+  return c;
+}
+
+uint32_t gg_device_count(const gg_ctx* ctx) {
+  if (!ctx) return 0;
+  return ctx->devs.empty() ? 1u : (uint32_t)ctx->devs.size();
+}
+
+gg_ctx* gg_device_ctx(gg_ctx* ctx, uint32_t index) {
+  if (!ctx) return nullptr;
+  if (ctx->devs.empty()) return index == 0 ? ctx : nullptr;
+  return index < ctx->devs.size() ? ctx->devs[index] : nullptr;
+}
+
+gg_status gg_set_host_threads(gg_ctx* ctx, int n_threads) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  ctx->host_threads = n_threads > 0 ? n_threads : 0;
+  for (gg_ctx* m : ctx->devs) m->host_threads = ctx->host_threads;
+  return GG_OK;
+}
+
+gg_status gg_phase_times(const gg_ctx* ctx, double* ms) {
+  if (!ctx || !ms) return fail(nullptr, GG_ERR_INVALID_ARG, "gg_phase_times: null argument");
+  for (int i = 0; i < GG_PHASE_COUNT; ++i) ms[i] = ctx->phase_ms[i];
+  return GG_OK;
+}
+
+gg_status gg_sketch(gg_ctx* ctx, const gg_packed* packed, uint64_t* out_hashes, uint32_t* out_lens) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (!packed || (packed->n_genomes && (!out_hashes || !out_lens)))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_sketch: null buffer");
+  const uint32_t ng = packed->n_genomes;
+  if (ng == 0) return GG_OK;
+  const std::vector<gg_ctx*> ms = members(ctx);
+  const size_t s = ctx->s;
+  // contiguous genome ranges of about equal k-mer counts; each member copies
+  // the packed words its range spans and sketches it
+  const std::vector<uint32_t> cut = balance_genomes(packed->runs, packed->n_runs, ng, ctx->k, ms.size());
+  return on_members(ctx, ms, [&](size_t mi, gg_ctx* m) -> gg_status {
+    const uint32_t g0 = cut[mi], g1 = cut[mi + 1];
+    if (g0 >= g1) return GG_OK;
+    const gg_run* rall = packed->runs;
+    const gg_run* rend = packed->runs + packed->n_runs;
+    const gg_run* rb = std::lower_bound(rall, rend, g0,
+                                        [](const gg_run& r, uint32_t g) { return r.genome < g; });
+    const gg_run* re = std::lower_bound(rb, rend, g1,
+                                        [](const gg_run& r, uint32_t g) { return r.genome < g; });
+    uint64_t w0 = 0, w1 = 0;
+    if (rb != re) {
+      w0 = rb->base / 16;
+      for (const gg_run* r = rb; r != re; ++r) w1 = std::max<uint64_t>(w1, (r->base + r->len + 15) / 16);
+    }
+    std::vector<gg_run> runs(rb, re);
+    for (gg_run& r : runs) {
+      r.genome -= g0;
+      r.base -= w0 * 16;
+    }
+    uint32_t* d_words;
+    uint64_t* d_out;
+    uint32_t* d_lens;
+    const uint32_t nl = g1 - g0;
+    GG_HIP(m, scratch_t(m, "in_words", std::max<uint64_t>(w1 - w0, 1), &d_words));
+    GG_HIP(m, scratch_t(m, "sk_out", (size_t)nl * s, &d_out));
+    GG_HIP(m, scratch_t(m, "sk_lens", nl, &d_lens));
+    if (w1 > w0)
+      GG_HIP(m, hipMemcpyAsync(d_words, packed->words + w0, (w1 - w0) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                               m->stream));
+    GG_HIP(m, hipMemsetAsync(d_out, 0, (size_t)nl * s * sizeof(uint64_t), m->stream));
+    gg_status st = sketch_core(m, d_words, w1 - w0, runs.data(), runs.size(), nl, d_out, d_lens, nullptr, m->stream);
+    if (st != GG_OK) return st;
+    GG_HIP(m, hipMemcpyAsync(out_hashes + (size_t)g0 * s, d_out, (size_t)nl * s * sizeof(uint64_t),
+                             hipMemcpyDeviceToHost, m->stream));
+    GG_HIP(m, hipMemcpyAsync(out_lens + g0, d_lens, nl * sizeof(uint32_t), hipMemcpyDeviceToHost, m->stream));
+    GG_HIP(m, hipStreamSynchronize(m->stream));
+    return GG_OK;
+  });
+}
+
+gg_status gg_pairs(gg_ctx* ctx, const uint64_t* sketches, const uint32_t* lens, uint32_t n, float min_ani,
+                   gg_pair** out, uint64_t* n_out) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (!out || !n_out || (n && (!sketches || !lens))) return fail(ctx, GG_ERR_INVALID_ARG, "gg_pairs: null buffer");
+  if (std::isnan(min_ani)) return fail(ctx, GG_ERR_INVALID_ARG, "min_ani is NaN");
+  *out = nullptr;
+  *n_out = 0;
+  for (uint32_t i = 0; i < n; ++i)
+    if (lens[i] > ctx->s) return fail(ctx, GG_ERR_INVALID_ARG, "sketch longer than sketch_size");
+  std::vector<gg_pair> res;
+  if (n >= 2) {
+    const std::vector<gg_ctx*> ms = members(ctx);
+    std::vector<Rows> rows(ms.size());
+    gg_status st = on_members(ctx, ms, [&](size_t mi, gg_ctx* m) -> gg_status {
+      gg_status r = member_rows(m, n, &rows[mi]);
+      if (r != GG_OK) return r;
+      GG_HIP(m, hipMemcpyAsync(rows[mi].sk, sketches, (size_t)n * m->s * sizeof(uint64_t), hipMemcpyHostToDevice,
+                               m->stream));
+      GG_HIP(m, hipMemcpyAsync(rows[mi].len, lens, n * sizeof(uint32_t), hipMemcpyHostToDevice, m->stream));
+      GG_HIP(m, hipStreamSynchronize(m->stream));
+      return GG_OK;
+    });
+    if (st != GG_OK) return st;
+    // every member holds every row: nothing to replicate
+    st = gather_pairs_merge(ctx, ms, rows, {}, n, min_ani, res);
+    if (st != GG_OK) return st;
+  }
+  *out = copy_out(res);
+  if (!*out) return fail(ctx, GG_ERR_OUT_OF_MEMORY, "out of host memory");
+  *n_out = res.size();
+  return GG_OK;
+}
+
+gg_status gg_sketch_files(gg_ctx* ctx, const char* const* paths, uint32_t n_paths, const char* cache_dir,
+                          uint64_t* out_hashes, uint32_t* out_lens, uint32_t* n_cached) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (n_paths && (!paths || !out_hashes || !out_lens))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_sketch_files: null argument");
+  if (n_cached) *n_cached = 0;
+  if (n_paths == 0) return GG_OK;
+  const std::vector<gg_ctx*> ms = members(ctx);
+  std::vector<Rows> rows;
+  std::vector<RowSpan> spans;
+  return sketch_files_members(ctx, ms, paths, n_paths, cache_dir, rows, spans, out_hashes, out_lens, n_cached);
+}
+
+gg_status gg_precluster_files_cached(gg_ctx* ctx, const char* const* paths, uint32_t n_paths, float min_ani,
+                                     const char* cache_dir, gg_pair** pairs, float** ani, uint64_t* n_out,
+                                     uint32_t* n_cached) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (!pairs || !ani || !n_out || (n_paths && !paths))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_precluster_files: null argument");
+  if (std::isnan(min_ani)) return fail(ctx, GG_ERR_INVALID_ARG, "min_ani is NaN");
+  *pairs = nullptr;
+  *ani = nullptr;
+  *n_out = 0;
+  if (n_cached) *n_cached = 0;
+  for (double& x : ctx->phase_ms) x = 0.0;
+  const std::vector<gg_ctx*> ms = members(ctx);
+  std::vector<Rows> rows;
+  std::vector<RowSpan> spans;
+  std::vector<gg_pair> res;
+  auto t0 = Clock::now();
+  // every file is read and sketched, even a lone one: a file that does not
+  // parse fails the call as finch's sketch_files does (src/finch.rs:50)
+  gg_status st = sketch_files_members(ctx, ms, paths, n_paths, cache_dir, rows, spans, nullptr, nullptr, n_cached);
+  if (st != GG_OK) return st;
+  ctx->phase_ms[GG_PHASE_SKETCH] = ms_since(t0);
+  if (n_paths >= 2) {
+    st = gather_pairs_merge(ctx, ms, rows, spans, n_paths, min_ani, res);
+    if (st != GG_OK) return st;
+  }
+  return pairs_with_ani(ctx, res, pairs, ani, n_out);
+}
+
+gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths, uint32_t n_paths, float min_ani,
+                              gg_pair** pairs, float** ani, uint64_t* n_out) {
+  return gg_precluster_files_cached(ctx, paths, n_paths, min_ani, nullptr, pairs, ani, n_out, nullptr);
+}
+
+gg_status gg_precluster_shards(gg_ctx* ctx, const gg_shard* shards, float min_ani, gg_pair** pairs, float** ani,
+                               uint64_t* n_out) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (!shards || !pairs || !ani || !n_out) return fail(ctx, GG_ERR_INVALID_ARG, "gg_precluster_shards: null argument");
+  if (std::isnan(min_ani)) return fail(ctx, GG_ERR_INVALID_ARG, "min_ani is NaN");
+  *pairs = nullptr;
+  *ani = nullptr;
+  *n_out = 0;
+  for (double& x : ctx->phase_ms) x = 0.0;
+  const std::vector<gg_ctx*> ms = members(ctx);
+  const size_t M = ms.size();
+  std::vector<uint32_t> off(M + 1, 0);
+  for (size_t i = 0; i < M; ++i) {
+    if (shards[i].n_runs && (!shards[i].runs || !shards[i].d_words))
+      return fail(ctx, GG_ERR_INVALID_ARG, "gg_precluster_shards: null shard buffer");
+    if ((uint64_t)off[i] + shards[i].n_genomes > 0xFFFFFFFFull)
+      return fail(ctx, GG_ERR_INVALID_ARG, "gg_precluster_shards: too many genomes");
+    off[i + 1] = off[i] + shards[i].n_genomes;
+  }
+  const uint32_t n = off[M];
+  std::vector<Rows> rows(M);
+  std::vector<RowSpan> spans;
+  for (size_t i = 0; i < M; ++i)
+    if (shards[i].n_genomes) spans.push_back(RowSpan{off[i], shards[i].n_genomes, (uint32_t)i});
+  auto t0 = Clock::now();
+  gg_status st = on_members(ctx, ms, [&](size_t mi, gg_ctx* m) -> gg_status {
+    gg_status r = member_rows(m, n, &rows[mi]);
+    if (r != GG_OK) return r;
+    const gg_shard& sh = shards[mi];
+    if (sh.n_genomes == 0) return GG_OK;
+    // K1 writes the shard's rows at their global offset
+    return sketch_core(m, sh.d_words, sh.n_words, sh.runs, sh.n_runs, sh.n_genomes,
+                       rows[mi].sk + (size_t)off[mi] * m->s, rows[mi].len + off[mi], nullptr, m->stream);
+  });
+  if (st != GG_OK) return st;
+  ctx->phase_ms[GG_PHASE_SKETCH] = ms_since(t0);
+  std::vector<gg_pair> res;
+  if (n >= 2) {
+    st = gather_pairs_merge(ctx, ms, rows, spans, n, min_ani, res);
+    if (st != GG_OK) return st;
+  }
+  return pairs_with_ani(ctx, res, pairs, ani, n_out);
+}
+
+}  // extern "C"

@@ -21,10 +21,12 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -385,6 +387,155 @@ int default_threads() {
 }
 
 }  // namespace
+
+int ingest_threads(int n_threads) { return n_threads > 0 ? n_threads : default_threads(); }
+
+// ---------------------------------------------------------------------------
+// PackStream: files packed on a worker pool, handed to consumers genome by
+// genome with bounded host memory (see gg_internal.hpp).
+// ---------------------------------------------------------------------------
+struct PackStream::Impl {
+  const char* const* paths;
+  uint32_t n;
+  int k;
+  uint64_t budget;
+  bool stamping = false;
+  std::vector<FileStamp> stamps;
+  std::mutex mu;
+  std::condition_variable cv_done;   // a genome finished packing
+  std::condition_variable cv_space;  // in-flight bytes dropped / abort
+  std::vector<std::unique_ptr<GenomePacker>> g;
+  std::vector<uint8_t> state;  // 0 pending, 1 packing, 2 ready, 3 released
+  std::vector<gg_status> st;
+  std::vector<std::string> err;
+  uint32_t next = 0;      // next file index a worker takes
+  uint32_t frontier = 0;  // lowest index not yet released
+  uint64_t inflight = 0;  // bytes of packed, unreleased genomes
+  bool stop = false;
+  std::vector<std::thread> workers;
+
+  void work() {
+    std::vector<uint8_t> buf;
+    for (;;) {
+      uint32_t i;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        // the genome every consumer waits for next is always taken, so
+        // waiting for space here cannot starve a consumer
+        cv_space.wait(lk, [&] { return stop || next >= n || inflight < budget || next <= frontier; });
+        if (stop || next >= n) return;
+        i = next++;
+        state[i] = 1;
+      }
+      auto gp = std::make_unique<GenomePacker>(k);
+      gg_status s = GG_OK;
+      std::string e;
+      if (stamping) file_stamp(paths[i], &stamps[i]);
+      if (!paths[i]) {
+        s = GG_ERR_INVALID_ARG;
+        e = "null path";
+      } else if (!read_file(paths[i], buf, e)) {
+        s = GG_ERR_IO;
+      } else {
+        s = pack_buffer(buf.data(), buf.size(), paths[i], *gp, e);
+        gp->finish();
+      }
+      if (buf.capacity() > (256u << 20)) std::vector<uint8_t>().swap(buf);  // do not pin a huge buffer
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        inflight += gp->words.size() * sizeof(uint32_t) + gp->runs.size() * sizeof(gg_run);
+        g[i] = std::move(gp);
+        st[i] = s;
+        err[i] = std::move(e);
+        state[i] = 2;
+      }
+      cv_done.notify_all();
+    }
+  }
+};
+
+PackStream::PackStream(const char* const* paths, uint32_t n, int k, int n_threads, uint64_t budget_bytes,
+                       bool stamp_files)
+    : p_(new Impl()) {
+  Impl& m = *p_;
+  m.stamping = stamp_files;
+  m.stamps.resize(stamp_files ? n : 0);
+  m.paths = paths;
+  m.n = n;
+  m.k = k;
+  m.budget = std::max<uint64_t>(budget_bytes, 1);
+  m.g.resize(n);
+  m.state.assign(n, 0);
+  m.st.assign(n, GG_OK);
+  m.err.resize(n);
+  const int t = (int)std::min<uint32_t>((uint32_t)ingest_threads(n_threads), std::max(1u, n));
+  for (int w = 0; w < t; ++w) m.workers.emplace_back([this] { p_->work(); });
+}
+
+PackStream::~PackStream() {
+  abort();
+  for (auto& t : p_->workers)
+    if (t.joinable()) t.join();
+}
+
+void PackStream::abort() {
+  {
+    std::lock_guard<std::mutex> lk(p_->mu);
+    p_->stop = true;
+  }
+  p_->cv_space.notify_all();
+  p_->cv_done.notify_all();
+}
+
+gg_status PackStream::get(uint32_t i, const std::vector<uint32_t>** words, const std::vector<gg_run>** runs,
+                          std::string* err) {
+  Impl& m = *p_;
+  std::unique_lock<std::mutex> lk(m.mu);
+  m.cv_done.wait(lk, [&] { return m.state[i] >= 2 || (m.stop && m.state[i] == 0); });
+  if (m.state[i] < 2) {
+    if (err) *err = "ingest aborted";
+    return GG_ERR_INTERNAL;
+  }
+  if (m.st[i] != GG_OK) {
+    if (err) *err = m.err[i];
+    return m.st[i];
+  }
+  *words = &m.g[i]->words;
+  *runs = &m.g[i]->runs;
+  return GG_OK;
+}
+
+FileStamp PackStream::stamp(uint32_t i) {
+  std::lock_guard<std::mutex> lk(p_->mu);
+  return p_->stamping ? p_->stamps[i] : FileStamp{};
+}
+
+void PackStream::release(uint32_t i) {
+  Impl& m = *p_;
+  {
+    std::lock_guard<std::mutex> lk(m.mu);
+    if (m.state[i] != 2) return;
+    m.inflight -= m.g[i]->words.size() * sizeof(uint32_t) + m.g[i]->runs.size() * sizeof(gg_run);
+    m.g[i].reset();
+    m.state[i] = 3;
+    while (m.frontier < m.n && m.state[m.frontier] == 3) ++m.frontier;
+  }
+  m.cv_space.notify_all();
+}
+
+gg_status PackStream::first_error(std::string* err) {
+  Impl& m = *p_;
+  abort();
+  for (auto& t : m.workers)
+    if (t.joinable()) t.join();
+  for (uint32_t i = 0; i < m.n; ++i)
+    if (m.state[i] == 2 && m.st[i] != GG_OK) {
+      if (err) *err = m.err[i];
+      return m.st[i];
+    }
+  return GG_OK;
+}
+
 }  // namespace gg
 
 using namespace gg;

@@ -443,12 +443,14 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
     const uint64_t* __restrict__ tau, const uint64_t* __restrict__ table,
     uint32_t cap_log2,
     const uint32_t* __restrict__ flags, uint32_t s, uint32_t sort_pow2,
-    uint64_t* __restrict__ out, uint32_t* __restrict__ lens,
+    const uint32_t* __restrict__ row_of, uint64_t* __restrict__ out, uint32_t* __restrict__ lens,
     uint32_t* __restrict__ status) {
   extern __shared__ uint64_t buf[];
   __shared__ uint32_t fill;
   const uint32_t slot = slot_list[blockIdx.x];
-  const uint32_t g = slot_genome[slot];
+  // output row of the genome: the caller's row map when given (batches of a
+  // streamed file list land on their global rows)
+  const uint32_t g = row_of ? row_of[slot_genome[slot]] : slot_genome[slot];
   const uint32_t f = flags[slot];
   if (f & kFlagOverflow) {
     if (threadIdx.x == 0) {
@@ -544,7 +546,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   const uint64_t* tau, const uint64_t* table,
                                   uint32_t cap_log2,
                                   const uint32_t* flags, uint32_t s,
-                                  uint32_t sort_pow2, uint64_t* out,
+                                  uint32_t sort_pow2, const uint32_t* row_of, uint64_t* out,
                                   uint32_t* lens, uint32_t* status,
                                   hipStream_t st) {
   if (n_slots == 0) return hipSuccess;
@@ -559,7 +561,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
   const int threads = sort_pow2 >= 4096 ? kFinalizeMaxBlock : kBlock;
   hipLaunchKernelGGL(sketch_finalize_kernel, dim3(n_slots), dim3(threads), lds, st,
                      slot_list, slot_genome, tau, table, cap_log2, flags, s,
-                     sort_pow2, out, lens, status);
+                     sort_pow2, row_of, out, lens, status);
   return hipGetLastError();
 }
 

@@ -148,10 +148,17 @@ int load_entry(const char* dir, const char* path, int k, uint32_t s, uint64_t se
 }
 
 gg_status store_entry(const char* dir, const char* path, int k, uint32_t s, uint64_t seed,
-                      const uint64_t* hashes, uint32_t len) {
+                      const uint64_t* hashes, uint32_t len, const FileStamp* before) {
   FileId id;
   if (!file_id(path, id)) {
     set_thread_error(std::string("sketch cache: cannot stat ") + path);
+    return GG_ERR_IO;
+  }
+  // the file was stamped before it was read: if it changed since, the
+  // sketch may belong to the old contents and must not be filed under the
+  // new size and mtime
+  if (before && (!before->ok || before->size != id.size || before->mtime_ns != id.mtime_ns)) {
+    set_thread_error(std::string("sketch cache: ") + path + " changed while it was sketched; not stored");
     return GG_ERR_IO;
   }
   if (!make_dirs(dir)) {
@@ -211,8 +218,16 @@ void cache_load_many(const char* dir, const char* const* paths, uint32_t n, int 
 }
 
 gg_status cache_store(const char* dir, const char* path, int k, uint32_t s, uint64_t seed,
-                      const uint64_t* hashes, uint32_t len) {
-  return store_entry(dir, path, k, s, seed, hashes, len);
+                      const uint64_t* hashes, uint32_t len, const FileStamp* before) {
+  return store_entry(dir, path, k, s, seed, hashes, len, before);
+}
+
+bool file_stamp(const char* path, FileStamp* out) {
+  struct stat st;
+  out->ok = path && stat(path, &st) == 0;
+  out->size = out->ok ? (uint64_t)st.st_size : 0;
+  out->mtime_ns = out->ok ? (int64_t)st.st_mtim.tv_sec * 1000000000ll + st.st_mtim.tv_nsec : 0;
+  return out->ok;
 }
 
 }  // namespace gg
@@ -245,7 +260,7 @@ gg_status gg_sketch_cache_store(const char* cache_dir, const char* path, int kme
       gg::set_thread_error("gg_sketch_cache_store: hashes must be strictly ascending");
       return GG_ERR_INVALID_ARG;
     }
-  return gg::store_entry(cache_dir, path, kmer_length, sketch_size, hash_seed, hashes, len);
+  return gg::store_entry(cache_dir, path, kmer_length, sketch_size, hash_seed, hashes, len, nullptr);
 }
 
 }  // extern "C"

@@ -23,9 +23,12 @@
  *   - Inputs are borrowed for the duration of the call.  Buffers returned
  *     through pointer-to-pointer arguments are library-owned and released
  *     with gg_free / gg_packed_free.
- *   - A context is bound to one HIP device; calls on one context must be
- *     serialised by the caller (galah calls distances() once, from one
- *     thread: src/clusterer.rs:36).
+ *   - A context drives one HIP device (gg_create) or several
+ *     (gg_create_multi: one host thread per device inside each call; sketches
+ *     are replicated between the devices by peer copies over xGMI and the
+ *     pair tiles are partitioned).  Calls on one context must be serialised
+ *     by the caller (galah calls distances() once, from one thread:
+ *     src/clusterer.rs:36).
  *   - There is NO CPU fallback: gg_create fails with GG_ERR_NO_DEVICE when
  *     no MI355X (gfx950) device is visible.
  *   - *_device entry points take device pointers on the context's device
@@ -45,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 1u
+#define GG_ABI_VERSION 2u
 
 typedef enum gg_status {
   GG_OK = 0,
@@ -104,7 +107,40 @@ const char* gg_thread_last_error(void);
 gg_ctx* gg_create(int kmer_length, uint32_t sketch_size, uint64_t hash_seed,
                   int device, gg_status* status);
 void gg_destroy(gg_ctx* ctx);
+/* HIP ordinal of the context's (first) device. */
 int gg_device(const gg_ctx* ctx);
+
+/* ---- multi-device context (SURVEY.md 8(b) n_gpus, 8(e)) ----------------- */
+/* devices[0 .. n_devices): HIP ordinals, one shard each; an ordinal may
+ * repeat (each entry is then its own shard with its own stream on that
+ * device -- how the sharded path is exercised on one GPU).
+ * devices == NULL: the first n_devices visible devices, or, for
+ * n_devices == 0, the GALAHGPU_DEVICES environment variable (comma-separated
+ * ordinals) when it is set and every visible device otherwise -- galah's
+ * `n_gpus = 0` ("all").  One resolved device gives a plain single-device
+ * context.  gg_sketch, gg_pairs, gg_sketch_files, gg_precluster_files(_cached)
+ * and gg_precluster_shards use every member; the other entry points act on
+ * the first member.  Results never depend on the device list. */
+gg_ctx* gg_create_multi(int kmer_length, uint32_t sketch_size, uint64_t hash_seed,
+                        const int* devices, uint32_t n_devices, gg_status* status);
+/* Number of members (1 for a single-device context). */
+uint32_t gg_device_count(const gg_ctx* ctx);
+/* Member `index` as a single-device context (owned by ctx, valid until
+ * gg_destroy(ctx)); ctx itself when it is a single-device context and
+ * index == 0; NULL otherwise. */
+gg_ctx* gg_device_ctx(gg_ctx* ctx, uint32_t index);
+/* Host threads that read, gunzip and pack genome files inside
+ * gg_sketch_files / gg_precluster_files(_cached): galah's --threads
+ * (CAP:1327-1332).  <= 0 restores the default (GALAHGPU_THREADS, else
+ * OMP_NUM_THREADS, else the CPUs of the process's affinity mask). */
+gg_status gg_set_host_threads(gg_ctx* ctx, int n_threads);
+
+/* Wall-clock phases of the last gg_precluster_files(_cached) /
+ * gg_precluster_shards call on ctx, in ms: ingest + K1 (files are streamed,
+ * so reading and sketching overlap), replication of the sketches between
+ * devices, K2 on every device + D2H, host merge (sort by (i, j) + ANI). */
+enum { GG_PHASE_SKETCH = 0, GG_PHASE_REPLICATE = 1, GG_PHASE_PAIRS = 2, GG_PHASE_MERGE = 3, GG_PHASE_COUNT = 4 };
+gg_status gg_phase_times(const gg_ctx* ctx, double* ms /* [GG_PHASE_COUNT] */);
 
 /* ---- host-side ingest: FASTA/FASTQ (plain or gz) -> 2-bit runs --------- */
 /* Replaces needletail parse_fastx_file + normalize(false) + the ACGT
@@ -164,10 +200,32 @@ gg_status gg_pairs_device(gg_ctx* ctx, const uint64_t* d_sketches,
                           uint64_t* d_count, void* stream);
 
 /* ---- the fused FinchPreclusterer::distances body ------------------------ */
-/* paths -> sorted passing pairs plus their f32 ANI (src/finch.rs:70 value). */
+/* paths -> sorted passing pairs plus their f32 ANI (src/finch.rs:70 value).
+ * Files are streamed: read, gunzipped and packed on the host threads
+ * (gg_set_host_threads) while earlier batches are copied to the devices and
+ * sketched; host memory stays bounded whatever the number of files. */
 gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths,
                               uint32_t n_paths, float min_ani, gg_pair** pairs,
                               float** ani, uint64_t* n_out);
+
+/* One member's shard of device-resident packed genomes for
+ * gg_precluster_shards: d_words lives on that member's device, runs are host
+ * metadata whose genome field indexes the shard's n_genomes genomes.  The
+ * global genome order is shard 0's genomes, then shard 1's, ... */
+typedef struct gg_shard {
+  const uint32_t* d_words;
+  uint64_t n_words;
+  const gg_run* runs;
+  uint64_t n_runs;
+  uint32_t n_genomes;
+} gg_shard;
+/* The fused precluster step over genomes already resident in HBM:
+ * K1 on every member's shard, sketches replicated to every member (peer
+ * copies), K2 over each member's share of the pair tiles (gg_pair_partition),
+ * sparse results gathered and sorted by (i, j) with their f32 ANI.
+ * shards has gg_device_count(ctx) entries.  Synchronous. */
+gg_status gg_precluster_shards(gg_ctx* ctx, const gg_shard* shards, float min_ani, gg_pair** pairs,
+                               float** ani, uint64_t* n_out);
 
 /* ---- sketch cache --------------------------------- */
 /* galah sketches every genome on every run (src/finch.rs:47); these entry

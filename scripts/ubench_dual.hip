@@ -58,12 +58,42 @@ constexpr int kChains = 16;
   X(29, "mix mad_u64 + xor v,v", MIXW("v_mad_u64_u32 %1, vcc, %3, %3, %1", "v_xor_b32 %0, %2, %0")) \
   X(30, "cndmask_e32 vcc", A32("v_cndmask_b32_e32 %0, %2, %0, vcc"))                    \
   X(31, "bfe_u32 v,inl,inl", A32("v_bfe_u32 %0, %0, 8, 8"))                             \
-  X(32, "lshlrev_b32 sdwa", A32("v_lshlrev_b32_sdwa %0, 3, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"))
+  X(32, "lshlrev_b32 sdwa", A32("v_lshlrev_b32_sdwa %0, 3, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1")) \
+  X(33, "cmp_lt_u32 + cndmask_e32 (2)", A64P("v_cmp_lt_u32_e32 vcc, %0, %3\n v_cndmask_b32_e32 %0, %3, %0, vcc")) \
+  X(34, "cndmask_e64 sgpr-pair mask", A32M("v_cndmask_b32_e64 %0, %0, %2, %3"))            \
+  X(35, "add_u32 literal,v", A32("v_add_u32_e32 %0, 0x12345, %0"))                        \
+  X(36, "xor_b32 literal,v", A32("v_xor_b32_e32 %0, 0x12345678, %0"))                     \
+  X(37, "or3_b32 v,v,v", A32("v_or3_b32 %0, %0, %2, %2"))                                  \
+  X(38, "and_or_b32 v,inl,v", A32("v_and_or_b32 %0, %0, 63, %2"))                          \
+  X(39, "lshl_or_b32 v,inl,v", A32("v_lshl_or_b32 %0, %0, 3, %2"))                         \
+  X(40, "perm_b32 v,v,v", A32("v_perm_b32 %0, %0, %2, %2"))                                \
+  X(41, "mov_b32 from sgpr", A32("v_mov_b32 %0, %1"))                                      \
+  X(42, "lshlrev_b32 v,v", A32("v_lshlrev_b32 %0, %2, %0"))                                \
+  X(43, "lshl_add_u32 v,inl,v", A32("v_lshl_add_u32 %0, %0, 3, %2"))                       \
+  X(44, "sub_u32 v,v", A32("v_sub_u32 %0, %0, %2"))                                        \
+  X(45, "ffbl_b32 v", A32("v_ffbl_b32 %0, %0"))                                            \
+  X(46, "add_co_u32_e32 v,v (carry out)", A32("v_add_co_u32_e32 %0, vcc, %2, %0"))         \
+  X(47, "mad_u32_u24 v,v,v", A32("v_mad_u32_u24 %0, %0, %2, %2"))                          \
+  X(48, "mul_u32_u24 v,v", A32("v_mul_u32_u24 %0, %0, %2"))                                \
+  X(49, "mul_hi_u32_u24 v,v", A32("v_mul_hi_u32_u24 %0, %0, %2"))                          \
+  X(50, "xad_u32 v,v,v", A32("v_xad_u32 %0, %0, %2, %2"))                                  \
+  X(51, "bitop3_b32 v,v,v", A32("v_bitop3_b32 %0, %0, %2, %2 bitop3:0x96"))                \
+  X(52, "alignbit v,v,v", A32("v_alignbit_b32 %0, %0, %2, %2"))                            \
+  X(53, "lshrrev+xor pair (xorshift)", A64P("v_lshrrev_b32 %1, 1, %0\n v_xor_b32 %0, %0, %1")) \
+  X(54, "add_u32 v,v dep chain x1", A1("v_add_u32 %0, %0, %2"))                            \
+  X(55, "cmp_lt_u64 + 2 cndmask (3)", A64Q("v_cmp_lt_u64_e32 vcc, %0, %3\n v_cndmask_b32_e32 %1, %1, %4, vcc\n v_cndmask_b32_e32 %2, %2, %5, vcc")) \
+  X(56, "pk_mul_lo_u16 v,v", A32("v_pk_mul_lo_u16 %0, %0, %2"))                            \
+  X(57, "lshlrev_b32 inl,v e64", A32("v_lshlrev_b32_e64 %0, 3, %0"))                       \
+  X(58, "lshlrev_b16 inl,v", A32("v_lshlrev_b16 %0, 3, %0"))                               \
+  X(59, "add_lshl_u32 v,v,inl", A32("v_add_lshl_u32 %0, %0, %2, 3"))
 
 // 32-bit chains r[q]; 64-bit chains w[q]; y: a VGPR, c: an SGPR
 #define A32(S) asm volatile(S : "+v"(r[q]) : "s"(c), "v"(y));
 #define A64(S) asm volatile(S : "+v"(w[q]) : "s"(c), "v"(y), "v"(y) : "vcc");
 #define A64P(S) asm volatile(S : "+v"(lo[q]), "+v"(hi[q]) : "s"(c), "v"(y) : "vcc");
+#define A32M(S) asm volatile(S : "+v"(r[q]) : "s"(c), "v"(y), "s"(mask));
+#define A1(S) { if (q == 0) asm volatile(S : "+v"(r[q]) : "s"(c), "v"(y)); }
+#define A64Q(S) asm volatile(S : "+v"(w[q]), "+v"(lo[q]), "+v"(hi[q]) : "v"(wy), "v"(y), "v"(y) : "vcc");
 #define MIX(S1, S2)                                            \
   {                                                            \
     if (q & 1) asm volatile(S1 : "+v"(r[q]) : "s"(c), "v"(y)); \
@@ -86,6 +116,8 @@ __global__ __launch_bounds__(256) void ubench(uint32_t* out, uint32_t seed) {
   uint64_t w[kChains];
   const uint32_t y = threadIdx.x * 0x9E3779B9u + seed;
   const uint32_t c = 0x85EBCA6Bu ^ seed;
+  const uint64_t mask = 0xF0F0F0F0F0F0F0F0ull ^ seed;
+  const uint64_t wy = ((uint64_t)y << 32) | (y * 5u);
 #pragma unroll
   for (int q = 0; q < kChains; ++q) {
     r[q] = threadIdx.x + q * 7919u + seed;
@@ -120,7 +152,8 @@ int run(uint32_t* d_out, int n_cu, int wps) {
   CHK(hipEventSynchronize(b));
   float ms = 0;
   CHK(hipEventElapsedTime(&ms, a, b));
-  const double instr = (V == 24 ? 2.0 : 1.0) * kIters * kChains * wps;  // wave-instructions per SIMD
+  const double per = (V == 24 || V == 33 || V == 53) ? 2.0 : V == 55 ? 3.0 : V == 54 ? 1.0 / kChains : 1.0;
+  const double instr = per * kIters * kChains * wps;  // wave-instructions per SIMD
   std::printf("{\"variant\": %d, \"name\": \"%s\", \"waves_per_simd\": %d, \"ms_per_launch\": %.4f, "
               "\"cycles_per_instr_at_2.4GHz\": %.3f}\n",
               V, kNames[V], wps, ms / reps, (ms / reps) * 1e-3 * 2.4e9 / instr);

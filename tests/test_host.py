@@ -48,7 +48,7 @@ def test_abi_exports_every_declared_symbol():
     L = ga.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert ga.abi_version() == 1
+    assert ga.abi_version() == 2
 
 
 def test_no_oracle_in_product_library():
@@ -69,7 +69,30 @@ def test_create_without_device_fails_loudly():
     assert e.value.status == ga.GG_ERR_NO_DEVICE
 
 
+def test_create_multi_without_device_fails_loudly(monkeypatch):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    for devs in ("all", [0, 0], [0]):
+        with pytest.raises(ga.GalahGpuError) as e:
+            ga.Context(devices=devs)
+        assert e.value.status == ga.GG_ERR_NO_DEVICE
+    monkeypatch.setenv("GALAHGPU_DEVICES", "0,0")
+    with pytest.raises(ga.GalahGpuError):
+        ga.Context(devices="all")
+
+
 # ------------------------------------------------------------- packer ----
+def test_pack_files_thread_count_does_not_change_packing(golden):
+    """galah --threads (CAP:1327-1332) bounds ingest; the packed bases and
+    runs are the same for 1 thread and for many."""
+    one = ga.pack_files(golden["paths"], threads=1)
+    many = ga.pack_files(golden["paths"], threads=7)
+    assert (one.words == many.words).all()
+    assert (one.runs == many.runs).all()
+    assert (one.genome_kmers == many.genome_kmers).all()
+
+
 def test_packer_matches_oracle_on_golden_genomes(golden):
     pk = ga.pack_files(golden["paths"], k=21)
     assert pk.n_genomes == len(golden["paths"])
