@@ -112,32 +112,14 @@ def sync_all(devs):
 # roofline of the dominant kernel
 # ---------------------------------------------------------------------------
 def k1_fingerprint():
-    """sha1 of K1's (k = 21, seed 0) machine code in the loaded library, or None."""
+    """sha1 of K1's (k = 21, seed 0) machine code in the loaded library (scripts/k1_isa.py), or None."""
     try:
-        import hashlib
-        out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "-d", "--offloading", ga.LIB_PATH,
-                              "--output-dir=/tmp"], capture_output=True, text=True, timeout=60)
-        del out
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import k1_isa
+        listing = k1_isa.kernel_listing(ga.LIB_PATH)
+        return k1_isa.fingerprint(listing) if listing else None
     except Exception:
         return None
-    import glob
-    objs = sorted(glob.glob("/tmp/%s*gfx950*" % os.path.basename(ga.LIB_PATH)))
-    if not objs:
-        return None
-    try:
-        txt = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "-d", objs[-1]], capture_output=True,
-                             text=True, timeout=60).stdout
-    except Exception:
-        return None
-    body, on = [], False
-    for line in txt.splitlines():
-        if line.endswith(">:"):
-            on = "sketch_candidates_kernelILi21ELb1E" in line
-            continue
-        if on and "\t" in line:
-            body.append(line.split("//")[0].split("\t", 1)[-1].strip())
-    import hashlib
-    return hashlib.sha1("\n".join(body).encode()).hexdigest() if body else None
 
 
 def roofline(kst_sk, kst_pr, s, config_note):
@@ -164,6 +146,11 @@ def roofline(kst_sk, kst_pr, s, config_note):
         k1["traffic_bytes_per_kmer_pmc"] = model.get("hbm_bytes_per_kmer_pmc")
         k1["peak_stale"] = (fp is None or fp != model.get("k1_fingerprint"))
         k1["frac"] = k1_gkmer / model["peak_gkmer_per_s"]
+        # the same instructions if every one of them dual-issued (2.3 cycles,
+        # MI355X_MICROARCH.md's "2 cycles per wave64 VALU"): the headroom a
+        # cheaper instruction mix could reach
+        all_dual = N_SIMD * CLK_GHZ * 64 / (model["valu_per_wave_kmer"] * model["class_cost_cycles"]["dual"])
+        k1["frac_vs_all_dual_issue"] = k1_gkmer / all_dual
     k2 = {"kernel": "pairs_gate_kernel (+ gate_build_kernel, gate_lo32_kernel)", "unit": "Gpair/s",
           "achieved": pairs / (pr_ms * 1e-3) / 1e9 if pr_ms > 0 else 0.0, "avg_ms": pr_ms, "work_per_launch": pairs,
           "merge_priced_GBps": pairs * 16.0 * s / (pr_ms * 1e-3) / 1e9 if pr_ms > 0 else 0.0,
@@ -173,14 +160,16 @@ def roofline(kst_sk, kst_pr, s, config_note):
     roof = {"bound": dom.get("bound", "valu"), "achieved": round(dom["achieved"], 3),
             "peak": round(dom.get("peak", 0.0), 3), "unit": dom["unit"],
             "frac": round(dom.get("frac", 0.0), 4),
-            "traffic": (round(model["hbm_bytes_per_kmer_pmc"] * kmers) if (model and dom is k1
+            "traffic": (round(2 * model["hbm_bytes_per_kmer_pmc"] * kmers) if (model and dom is k1
                         and model.get("hbm_bytes_per_kmer_pmc")) else None),
             "kernel": dom["kernel"], "avg_launch_ms": round(dom["avg_ms"], 4),
             "note": ("K1 is bound by VALU issue: peak = 1024 SIMDs x %.1f GHz x 64 k-mers / floor cycles per wave of "
                      "64 k-mers; floor = K1's VALU instructions per wave-k-mer (PMC at HEAD) at the issue cost of "
                      "their class measured on this chip (dual-issued simple ops ~2.3 cycles, others ~4.2, 64-bit "
-                     "~5.0; profiles/r02_k1_issue_model.json); traffic = HBM bytes per launch from the PMC pass "
-                     "(FETCH_SIZE, per k-mer) x k-mers; %s" % (CLK_GHZ, config_note)),
+                     "~5.0; profiles/r02_k1_issue_model.json); traffic = HBM bytes per launch from the PMC pass: "
+                     "FETCH_SIZE x 2 (the gfx950 factor, calibrated for 4-, 8- and 16-B loads by "
+                     "scripts/ubench_fetch.hip: profiles/r02_pmc_head/fetch) per k-mer x k-mers; %s"
+                     % (CLK_GHZ, config_note)),
             "kernels": [{kk: (round(v, 5) if isinstance(v, float) else v) for kk, v in x.items()} for x in (k1, k2)]}
     return roof
 
