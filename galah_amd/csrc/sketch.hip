@@ -59,19 +59,14 @@ __device__ __forceinline__ uint64_t rotl64(uint64_t x) {
   return ((uint64_t)nh << 32) | nl;
 }
 
-// rotl(x, 31) + y: the two v_alignbit_b32 halves feed a 32-bit add/addc
-// pair directly (hipcc otherwise splits the rotate into two 64-bit adds and
-// a move to re-pair the halves).
+// rotl(x, 31) + y: two v_alignbit_b32 and one v_lshl_add_u64 (a 64-bit
+// add in one instruction, ~5 cycles per wave against 2 x 4.2 for an
+// add_co / addc pair: profiles/r02_ubench_dual_8wps.txt).
 __device__ __forceinline__ uint64_t add_rotl31(uint64_t x, uint64_t y) {
-  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  const uint32_t nh = __builtin_amdgcn_alignbit(hi, lo, 1);
-  const uint32_t nl = __builtin_amdgcn_alignbit(lo, hi, 1);
-  uint32_t rl, rh;
-  asm("v_add_co_u32 %0, vcc, %2, %4\n\tv_addc_co_u32 %1, vcc, %3, %5, vcc"
-      : "=&v"(rl), "=v"(rh)
-      : "v"(nl), "v"(nh), "v"((uint32_t)y), "v"((uint32_t)(y >> 32))
-      : "vcc");
-  return ((uint64_t)rh << 32) | rl;
+  const uint64_t r = rotl64<31>(x);
+  uint64_t out;
+  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(out) : "v"(r), "v"(y));
+  return out;
 }
 
 // fmix64 without its final k ^= k >> 33, which leaves the high word alone
@@ -104,9 +99,10 @@ struct HashShape {
   static constexpr bool TAIL_TAB = TAIL >= 1 && TAIL <= kTailMaxBases;
   // per full block (u64 units): k1 group tables of 16-byte {T * (c2 << 31),
   // hi(T)} and 8-byte {hi(T * (c2 << 31)), hi(T)} entries (the second group's
-  // T has a zero low word, so has its product), k2 group tables of 8-byte T
-  // and 4-byte hi(T) entries
-  static constexpr int BLK_U64 = 512 + 256 + 256 + 128;
+  // T has a zero low word, so has its product), k2 group tables of 16-byte
+  // {P(T), hi(T), 0} (see hash_parts) and 4-byte hi(T) entries
+  static constexpr int K1A = 0, K1B = 512, K2A = 768, K2B = 1280;
+  static constexpr int BLK_U64 = 512 + 256 + 512 + 128;
   // tail: a whole-word table, or one 8-byte group table per tail group
   static constexpr int TAIL_GROUPS = TAIL_TAB ? 0 : NW - 4 * NBLK;
   static constexpr int TAIL_ENTRIES = TAIL_TAB ? (1 << (2 * TAIL)) : 0;
@@ -157,18 +153,25 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
 #pragma unroll
   for (int b = 0; b < S::NBLK; ++b) {
     const uint64_t* bt = tab + b * S::BLK_U64;
-    const ulonglong2 e0 = *(const ulonglong2*)(bt + 2 * group_byte(hi, lo, 4 * b));
-    const uint2 e1 = *(const uint2*)(bt + 512 + group_byte(hi, lo, 4 * b + 1));
-    const uint64_t t2 = bt[768 + group_byte(hi, lo, 4 * b + 2)];
-    const uint32_t t3 = ((const uint32_t*)(bt + 1024))[group_byte(hi, lo, 4 * b + 3)];
-    uint64_t k2 = t2 + ((uint64_t)t3 << 32);  // = k2 * c2
+    const ulonglong2 e0 = *(const ulonglong2*)(bt + S::K1A + 2 * group_byte(hi, lo, 4 * b));
+    const uint2 e1 = *(const uint2*)(bt + S::K1B + group_byte(hi, lo, 4 * b + 1));
+    const uint4 e2 = *(const uint4*)(bt + S::K2A + 2 * group_byte(hi, lo, 4 * b + 2));
+    const uint32_t t3 = ((const uint32_t*)(bt + S::K2B))[group_byte(hi, lo, 4 * b + 3)];
     // rotl(k1 * c1, 31) * c2
     const uint32_t v = ((uint32_t)e0.y + e1.y) >> 1;
     uint64_t k1 = (uint64_t)v * (uint32_t)c2 + (e0.x + ((uint64_t)e1.x << 32));
     k1 += (uint64_t)(v * (uint32_t)(c2 >> 32)) << 32;
+    // rotl(k2 * c2, 33) * c1 = P + hx * (2 c1): x = k2 * c2 = T2 + (hi(T3) << 32);
+    // rotl(x, 33) = (x << 33) + (x >> 31) (disjoint bits) and x >> 31 =
+    // 2 hi(x) + bit 31 of lo(x) = 2 hi(x) + bit 31 of lo(T2), so
+    // rotl(x, 33) * c1 = [T2 * (c1 << 33) + (lo(T2) >> 31) * c1] + hi(x) * 2 c1,
+    // the bracket a table entry P of group 4b+2, hi(x) = hi(T2) + hi(T3)
+    const uint32_t hx = e2.z + t3;
+    uint64_t k2 = (uint64_t)hx * (uint32_t)(c1 << 1) + (((uint64_t)e2.y << 32) | e2.x);
+    k2 += (uint64_t)(hx * (uint32_t)((c1 << 1) >> 32)) << 32;
     h1 ^= k1;
     h1 = rotl64<27>(h1); h1 += h2; h1 = times5_plus(h1, 0x52dce729);
-    k2 = rotl64<33>(k2); k2 *= c1; h2 ^= k2;
+    h2 ^= k2;
     h2 = add_rotl31(h2, h1); h2 = times5_plus(h2, 0x38495ab5);
   }
   const uint64_t* tt = tab + S::TAIL_BASE;
@@ -231,10 +234,11 @@ __device__ __forceinline__ void build_tables(uint64_t* tab) {
       } else if (r < 768) {  // k1 group 4b+1: {hi(T * (c2 << 31)), hi(T)}
         const uint64_t t = group_term<K>((int)(4 * b + 1), r - 512);
         tab[i] = ((t * c2r) >> 32) | (t & 0xFFFFFFFF00000000ull);
-      } else if (r < 1024) {  // k2 group 4b+2: T
-        tab[i] = group_term<K>((int)(4 * b + 2), r - 768);
+      } else if (r < 1280) {  // k2 group 4b+2: {P = T * (c1 << 33) + (lo(T) >> 31) * c1, hi(T)}
+        const uint64_t t = group_term<K>((int)(4 * b + 2), (r - 768) >> 1);
+        tab[i] = (r & 1u) ? (t >> 32) : t * (c1 << 33) + ((t & 0xFFFFFFFFull) >> 31) * c1;
       } else {  // k2 group 4b+3: hi(T), two entries per u64
-        const uint32_t g = 2 * (r - 1024);
+        const uint32_t g = 2 * (r - 1280);
         tab[i] = (group_term<K>((int)(4 * b + 3), g) >> 32) |
                  (group_term<K>((int)(4 * b + 3), g + 1) & 0xFFFFFFFF00000000ull);
       }
