@@ -154,7 +154,7 @@ class _KStats(ctypes.Structure):
 
 _sig("gg_timing_enable", _i32, [_vp, _i32])
 _sig("gg_timing_read", _i32, [_vp, _i32, ctypes.POINTER(_KStats)])
-KERNEL_SKETCH, KERNEL_FINALIZE, KERNEL_PAIRS = 0, 1, 2
+KERNEL_SKETCH, KERNEL_FINALIZE, KERNEL_PAIRS, KERNEL_PAIRS_INDEX = 0, 1, 2, 3
 
 
 def lib():

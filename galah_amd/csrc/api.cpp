@@ -480,6 +480,73 @@ gg_status pairs_gate(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
   return GG_OK;
 }
 
+// Inverted-index K2 (pairs_index.hip) over tiles [tb, te).  *used = false
+// when the index path does not apply (a hash shared by more than kMaxRun
+// sketches); nothing has been emitted then and the caller runs the gate
+// kernel.  Eligibility (no pass without a shared hash, sizes) is the
+// caller's.
+gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n, uint64_t nb,
+                      uint64_t tb, uint64_t te, const uint32_t* d_cmin, const uint32_t* d_sufmin, gg_pair* d_out,
+                      uint64_t cap, uint64_t* d_count, uint64_t work, hipStream_t st, bool* used) {
+  constexpr uint32_t kMaxRun = 4096;
+  *used = false;
+  const uint64_t total = (uint64_t)n * c->s;
+  uint32_t kbits = 1;
+  while ((1u << kbits) < c->s) ++kbits;
+  IndexBuild b;
+  b.sketches = d_sk;
+  b.lens = d_lens;
+  b.n = n;
+  b.stride = c->s;
+  b.kbits = kbits;
+  b.max_run = kMaxRun;
+  GG_HIP(c, scratch_t(c, "idx_keys_in", total, &b.keys_in));
+  GG_HIP(c, scratch_t(c, "idx_keys_out", total, &b.keys_out));
+  GG_HIP(c, scratch_t(c, "idx_vals_in", total, &b.vals_in));
+  GG_HIP(c, scratch_t(c, "idx_vals_out", total, &b.vals_out));
+  GG_HIP(c, scratch_t(c, "idx_runinfo", total, &b.runinfo));
+  b.sort_tmp_bytes = index_sort_tmp_bytes(total);
+  GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
+  GG_HIP(c, scratch_t(c, "idx_flags", 4, &b.flags));
+  uint32_t flags[4] = {0, 0, 0, 0};
+  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_build(b, st); }));
+  GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof flags, hipMemcpyDeviceToHost, st));
+  GG_HIP(c, hipStreamSynchronize(st));
+  if (flags[0]) return GG_OK;  // a run longer than kMaxRun
+  // rows of the tile rows that intersect [tb, te)
+  uint64_t I0 = UINT64_MAX, I1 = 0, t = 0;
+  for (uint64_t I = 0; I < nb && t < te; ++I) {
+    const uint64_t first = t, last = t + (nb - I);
+    t = last;
+    if (std::max(first, tb) >= std::min(last, te)) continue;
+    I0 = std::min(I0, I);
+    I1 = std::max(I1, I + 1);
+  }
+  *used = true;
+  if (I0 == UINT64_MAX) return GG_OK;
+  IndexLaunch a;
+  a.sketches = d_sk;
+  a.lens = d_lens;
+  a.n = n;
+  a.stride = c->s;
+  a.kbits = kbits;
+  a.row0 = (uint32_t)(I0 * GG_PAIR_TILE);
+  a.nb = nb;
+  a.tile_begin = tb;
+  a.tile_end = te;
+  a.runinfo = b.runinfo;
+  a.vals = b.vals_out;
+  a.cmin = d_cmin;
+  a.sufmin = d_sufmin;
+  a.tmax = 2 * c->s;
+  a.out = d_out;
+  a.out_cap = cap;
+  a.count = (unsigned long long*)d_count;
+  const uint32_t rows = (uint32_t)(std::min<uint64_t>(n, I1 * GG_PAIR_TILE) - a.row0);
+  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_index_pairs(a, rows, st); }));
+  return GG_OK;
+}
+
 }  // namespace
 
 gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
@@ -491,7 +558,22 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
   const uint64_t nb = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
   te = std::min<uint64_t>(te, gg_pair_tiles(n));
   const uint64_t work = c->timing ? pairs_in_tiles(n, tb, te) : 0;
-  const int kern = (c->pairs_kernel == 1 && pairs_table_rows(c->s) == 0) ? 2 : c->pairs_kernel;
+  int kern = (c->pairs_kernel == 1 && pairs_table_rows(c->s) == 0) ? 2 : c->pairs_kernel;
+  // auto (0) / index (4): the inverted index when no pair without a shared
+  // hash can pass (min_ani > 0) and the packed (row, position) values fit
+  // 32 bits; "auto" also leaves tiny sets to the gate kernel
+  if (kern == 0 || kern == 4) {
+    uint32_t kbits = 1;
+    while ((1u << kbits) < c->s) ++kbits;
+    const bool fits = (uint64_t)n * c->s < (1ull << 31) && kbits < 32 && ((uint64_t)n << kbits) <= (1ull << 32);
+    if (c->sufmin_host[0] != 0 && fits && n >= 2 && (kern == 4 || n >= 512)) {
+      bool used = false;
+      gg_status is = pairs_index(c, d_sk, d_lens, n, nb, tb, te, d_cmin, d_sufmin, d_out, cap, d_count, work, st,
+                                 &used);
+      if (is != GG_OK || used) return is;
+    }
+    kern = 0;
+  }
   if (kern == 2) {
     PairsLaunch a;
     a.sketches = d_sk;
@@ -509,7 +591,8 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs(a, st); }));
     return GG_OK;
   }
-  if (kern == 0) return pairs_gate(c, d_sk, d_lens, n, nb, tb, te, d_cmin, d_sufmin, d_out, cap, d_count, work, st);
+  if (kern == 0 || kern == 3)
+    return pairs_gate(c, d_sk, d_lens, n, nb, tb, te, d_cmin, d_sufmin, d_out, cap, d_count, work, st);
   build_segments(c->seg_host, nb, tb, te, kSegTiles);
   if (c->seg_host.empty()) return GG_OK;
   PairSeg* d_segs;
@@ -660,8 +743,16 @@ gg_ctx* gg_create(int kmer_length, uint32_t sketch_size, uint64_t hash_seed, int
   c->s = sketch_size;
   c->seed = hash_seed;
   c->device = dev;
+  // GALAHGPU_PAIRS_KERNEL: auto (default: the inverted index where it
+  // applies, else the gate kernel), gate, index, table, merge -- for A/B
+  // runs and the parity tests; results never depend on it
   const char* pk = getenv("GALAHGPU_PAIRS_KERNEL");
-  c->pairs_kernel = !pk ? 0 : strcmp(pk, "table") == 0 ? 1 : strcmp(pk, "merge") == 0 ? 2 : 0;
+  c->pairs_kernel = !pk ? 0
+                    : strcmp(pk, "table") == 0 ? 1
+                    : strcmp(pk, "merge") == 0 ? 2
+                    : strcmp(pk, "gate") == 0  ? 3
+                    : strcmp(pk, "index") == 0 ? 4
+                                               : 0;
   hipError_t e = hipSetDevice(dev);
   if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   (void)e;

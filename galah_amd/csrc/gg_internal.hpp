@@ -144,6 +144,47 @@ struct GateLaunch {
 hipError_t launch_gate_build(const GateBuildLaunch& a, hipStream_t st);
 hipError_t launch_pairs_gate(const GateLaunch& a, hipStream_t st);
 
+// pairs_index.hip: the inverted-index pair kernel (default K2 when
+// eligible; see the file header).
+struct IndexBuild {
+  const uint64_t* sketches;
+  const uint32_t* lens;
+  uint32_t n;
+  uint32_t stride;
+  uint32_t kbits;      // bits of a position k < stride in a packed value
+  uint32_t max_run;    // longer runs: overflow (gate kernel instead)
+  uint64_t* keys_in;   // [n * stride]
+  uint64_t* keys_out;
+  uint32_t* vals_in;
+  uint32_t* vals_out;
+  uint64_t* runinfo;   // [n * stride]
+  void* sort_tmp;
+  size_t sort_tmp_bytes;
+  uint32_t* flags;     // [4]: overflow, pad, events (u64)
+};
+struct IndexLaunch {
+  const uint64_t* sketches;
+  const uint32_t* lens;
+  uint32_t n;
+  uint32_t stride;
+  uint32_t kbits;
+  uint32_t row0;         // first row processed (blockIdx.x = row - row0)
+  uint64_t nb;           // tile rows
+  uint64_t tile_begin;
+  uint64_t tile_end;
+  const uint64_t* runinfo;
+  const uint32_t* vals;  // sorted values (row << kbits | k)
+  const uint32_t* cmin;
+  const uint32_t* sufmin;
+  uint32_t tmax;
+  gg_pair* out;
+  uint64_t out_cap;
+  unsigned long long* count;
+};
+hipError_t index_build(const IndexBuild& b, hipStream_t st);
+size_t index_sort_tmp_bytes(uint64_t total);
+hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st);
+
 // synth.hip
 hipError_t launch_synth(uint32_t first_genome, uint32_t n_genomes, uint32_t genome_len,
                         uint32_t cluster_size, float max_sub_rate,

@@ -309,8 +309,11 @@ void gg_free(void* p);
  * synchronises on those events and returns the summed duration, the number
  * of launches and the algorithmic work units (k-mer positions for
  * GG_KERNEL_SKETCH, genomes for GG_KERNEL_FINALIZE, evaluated pairs for
- * GG_KERNEL_PAIRS) since the last gg_timing_enable. */
-enum { GG_KERNEL_SKETCH = 0, GG_KERNEL_FINALIZE = 1, GG_KERNEL_PAIRS = 2, GG_KERNEL_COUNT = 3 };
+ * GG_KERNEL_PAIRS; GG_KERNEL_PAIRS_INDEX is the inverted-index pair kernel's
+ * sort and run pass, whose pair pass counts under GG_KERNEL_PAIRS) since the
+ * last gg_timing_enable. */
+enum { GG_KERNEL_SKETCH = 0, GG_KERNEL_FINALIZE = 1, GG_KERNEL_PAIRS = 2, GG_KERNEL_PAIRS_INDEX = 3,
+       GG_KERNEL_COUNT = 4 };
 typedef struct gg_kernel_stats {
   double ms;
   uint64_t launches;

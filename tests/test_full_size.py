@@ -16,7 +16,8 @@ the reference loops; the oracle restates them):
     inside a cluster (45 per cluster: these are all the pairs whose ANI is
     near the cutoff; every one within +-3 of cmin[total] is among them and
     counted), and for 2,000 random pairs across clusters;
-  * the gate kernel's full pair set equal to the independent merge kernel
+  * the default pair kernel's (the inverted index at these sizes) pair set
+    equal to the gate kernel's and to the independent merge kernel's
     (GALAHGPU_PAIRS_KERNEL=merge, one lane per pair, the literal merge) over
     a band of 1,024 rows against all columns.
 """
@@ -164,20 +165,23 @@ def check_config(ctx, d_words, runs, n, s, thr, genome_bases, spot):
     tb, te = tile_row_range(n, row0, 1024)
     band_gate = device_pairs(ctx, d_sk, d_len, n, tb, te, thr)
     old = os.environ.get("GALAHGPU_PAIRS_KERNEL")
-    os.environ["GALAHGPU_PAIRS_KERNEL"] = "merge"
+    bands = {}
     try:
-        with ga.Context(k=21, sketch_size=s) as mctx:
-            band_merge = device_pairs(mctx, d_sk, d_len, n, tb, te, thr)
+        for kern in ("merge", "gate", "index"):
+            os.environ["GALAHGPU_PAIRS_KERNEL"] = kern
+            with ga.Context(k=21, sketch_size=s) as mctx:
+                bands[kern] = device_pairs(mctx, d_sk, d_len, n, tb, te, thr)
     finally:
         if old is None:
             os.environ.pop("GALAHGPU_PAIRS_KERNEL")
         else:
             os.environ["GALAHGPU_PAIRS_KERNEL"] = old
-    assert np.array_equal(band_gate, band_merge)
+    for kern in bands:
+        assert np.array_equal(band_gate, bands[kern]), kern
     in_band = (P[:, 0] >= row0) & (P[:, 0] < row0 + 1024)
     assert np.array_equal(P[in_band], band_gate)
     print("\n%d genomes, s=%d: %d passing pairs, %d within-cluster pairs checked (%d pass, %d within +-3 of "
-          "cmin), %d cross-cluster pairs, band of 1024 rows: %d pairs gate == merge"
+          "cmin), %d cross-cluster pairs, band of 1024 rows: %d pairs default == gate == index == merge"
           % (n, s, len(P), len(ii), int(opass.sum()), near, len(ri), len(band_gate)))
     assert near > 0
     del d_sk, d_len

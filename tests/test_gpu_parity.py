@@ -276,13 +276,12 @@ def test_gate_table_and_merge_kernels_match_oracle(monkeypatch, s, min_ani):
     o = oracle.pairs(sk, lens.astype(np.int32), np.float32(min_ani))
     exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
     got = {}
-    for kern in ("gate", "table", "merge"):
+    for kern in ("gate", "table", "merge", "index", "auto"):
         monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", kern)
         with ga.Context(k=21, sketch_size=s) as ctx:
             got[kern] = as_tuples(ctx.pairs(sk, lens, np.float32(min_ani)))
-    assert got["merge"] == exp
-    assert got["table"] == exp
-    assert got["gate"] == exp
+    for kern in got:
+        assert got[kern] == exp, kern
 
 
 def test_c5_mixed_sizes_s10000(gpu_ctx, monkeypatch):
@@ -359,9 +358,10 @@ def test_gate_kernel_low_word_collisions(monkeypatch, s):
     for thr in (0.0, 0.5, 0.9):
         o = oracle.pairs(sk, lens.astype(np.int32), np.float32(thr))
         exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
-        monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "gate")
-        with ga.Context(k=21, sketch_size=s) as ctx:
-            assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, thr
+        for kern in ("gate", "index"):
+            monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", kern)
+            with ga.Context(k=21, sketch_size=s) as ctx:
+                assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, (thr, kern)
 
 
 @pytest.mark.parametrize("n", [1, 2, 3, 31, 33, 65, 129])
@@ -372,3 +372,73 @@ def test_gate_kernel_small_and_ragged_n(gpu_ctx, n):
         p = gpu_ctx.pairs(sk, lens, np.float32(thr))
         o = oracle.pairs(sk, lens.astype(np.int32), np.float32(thr))
         assert as_tuples(p) == [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+
+
+def test_index_kernel_tile_ranges_and_partition(monkeypatch):
+    """The inverted-index kernel over explicit tile ranges (multi-GPU parts):
+    the union over 1, 2, 3 and 7 parts equals the oracle."""
+    torch = torch_dev()
+    monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
+    rng = np.random.default_rng(23)
+    n = 701
+    sk, lens = random_sketch_set(rng, n, 1000, 9)
+    o = oracle.pairs(sk, lens.astype(np.int32), np.float32(0.9))
+    exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+    d_sk = torch.from_numpy(sk.view(np.int64)).cuda()
+    d_lens = torch.from_numpy(lens.view(np.int32)).cuda()
+    cap = n * n
+    with ga.Context(k=21, sketch_size=1000) as ctx:
+        for parts in (1, 2, 3, 7):
+            got = []
+            for part in range(parts):
+                b, e = ga.pair_partition(n, parts, part)
+                d_out = torch.zeros(cap * 4, dtype=torch.int32, device="cuda")
+                d_cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+                ctx.pairs_device(d_sk, d_lens, n, b, e, np.float32(0.9), d_out, cap, d_cnt)
+                torch.cuda.synchronize()
+                c = int(d_cnt.item())
+                arr = d_out[:c * 4].cpu().numpy().view(np.uint32).reshape(-1, 4)
+                got += [tuple(map(int, r)) for r in arr]
+            assert sorted(got) == exp, parts
+
+
+def test_index_kernel_many_partners_and_long_runs(monkeypatch):
+    """Row 0 shares one hash with each of 2,999 other rows (more partners
+    than one LDS map holds: the row is counted in several passes), and a hash
+    shared by more sketches than the index kernel's run limit (the call falls
+    back to the gate kernel before emitting anything): both equal the oracle."""
+    rng = np.random.default_rng(29)
+    s = 1000
+    n = 3000
+    base = np.unique(rng.integers(1, 2**62, 4 * s, dtype=np.uint64))[:s]
+    sk = np.zeros((n, s), np.uint64)
+    lens = np.zeros(n, np.uint32)
+    sk[0] = base
+    lens[0] = s
+    for i in range(1, n):
+        v = np.unique(np.concatenate([[base[i % s]], rng.integers(2**62, 2**63, 40, dtype=np.uint64)]))
+        sk[i, :len(v)] = v
+        lens[i] = len(v)
+    for thr in (0.001, 0.5):
+        o = oracle.pairs(sk, lens.astype(np.int32), np.float32(thr))
+        exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+        for kern in ("index", "gate"):
+            monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", kern)
+            with ga.Context(k=21, sketch_size=s) as ctx:
+                assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, (thr, kern)
+    # 5,000 sketches that all hold one hash: a run of 5,000 > the run limit
+    n = 5000
+    s = 40
+    shared = np.uint64(12345)
+    sk = np.zeros((n, s), np.uint64)
+    lens = np.zeros(n, np.uint32)
+    for i in range(n):
+        v = np.unique(np.concatenate([[shared], rng.integers(2**40, 2**63, s - 1, dtype=np.uint64)]))[:s]
+        sk[i, :len(v)] = v
+        lens[i] = len(v)
+    o = oracle.pairs(sk, lens.astype(np.int32), np.float32(0.01))
+    exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+    assert len(exp) > 0
+    monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
+    with ga.Context(k=21, sketch_size=s) as ctx:
+        assert as_tuples(ctx.pairs(sk, lens, np.float32(0.01))) == exp
