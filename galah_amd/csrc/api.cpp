@@ -509,8 +509,19 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
   GG_HIP(c, scratch_t(c, "idx_flags", 4, &b.flags));
   uint32_t flags[4] = {0, 0, 0, 0};
-  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_build(b, st); }));
+  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_fill(b, st); }));
   GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof flags, hipMemcpyDeviceToHost, st));
+  GG_HIP(c, hipStreamSynchronize(st));
+  // sort on the bits below the largest hash + 1 (padding keys, 2^64 - 1,
+  // then still sort after every hash)
+  const uint64_t maxh = (uint64_t)flags[2] | ((uint64_t)flags[3] << 32);
+  uint32_t end_bit = 64;
+  if (maxh != ~0ull) {
+    end_bit = 1;
+    while (end_bit < 64 && ((maxh + 1) >> end_bit) != 0) ++end_bit;
+  }
+  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st, [&] { return index_build(b, end_bit, st); }));
+  GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   GG_HIP(c, hipStreamSynchronize(st));
   if (flags[0]) return GG_OK;  // a run longer than kMaxRun
   // rows of the tile rows that intersect [tb, te)

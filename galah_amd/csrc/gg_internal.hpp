@@ -160,7 +160,7 @@ struct IndexBuild {
   uint64_t* runinfo;   // [n * stride]
   void* sort_tmp;
   size_t sort_tmp_bytes;
-  uint32_t* flags;     // [4]: overflow, pad, events (u64)
+  uint32_t* flags;     // [4]: overflow, pad, largest hash (u64)
 };
 struct IndexLaunch {
   const uint64_t* sketches;
@@ -181,7 +181,10 @@ struct IndexLaunch {
   uint64_t out_cap;
   unsigned long long* count;
 };
-hipError_t index_build(const IndexBuild& b, hipStream_t st);
+// keys/vals of every entry and the largest hash (flags[2..3]); then, with
+// the sort's bit range, the sort and the run pass (overflow: flags[0]).
+hipError_t index_fill(const IndexBuild& b, hipStream_t st);
+hipError_t index_build(const IndexBuild& b, uint32_t end_bit, hipStream_t st);
 size_t index_sort_tmp_bytes(uint64_t total);
 hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st);
 
