@@ -25,6 +25,7 @@
 //     values below tau (tau < 2^64-1) or overflows, the host moves tau and
 //     re-runs the affected genomes only; the result is exact in both cases
 //     because every distinct hash <= tau is in the set.
+#include "device_util.hpp"
 #include "gg_internal.hpp"
 
 namespace gg {
@@ -36,10 +37,15 @@ constexpr int kGroup = 4;       // k-mers per tau-check branch
 template <int K>
 constexpr int seg_len() { return ((65 - K) / kGroup) * kGroup < 48 ? ((65 - K) / kGroup) * kGroup : 48; }
 constexpr int kBlock = 256;
-// min waves per SIMD forced on the register allocator (8 = 64 VGPRs; the
-// k = 21 body then spills a few dwords and runs ~1% slower than at 66 VGPRs)
+// min waves per SIMD forced on the register allocator: 7 (72 VGPRs, 4 dwords
+// spilled at k = 21) beats the unconstrained 76 VGPRs / 6 waves with the
+// candidate queue (C3 K1 49.3 -> 49.1 ms, C5 78.7 -> 77.9 ms)
 #ifndef GG_K1_MIN_WAVES
-#define GG_K1_MIN_WAVES 1
+#define GG_K1_MIN_WAVES 7
+#endif
+// candidates through the per-wave LDS queue (1) or inserted where they arise (0)
+#ifndef GG_K1_QUEUE
+#define GG_K1_QUEUE 1
 #endif
 
 // 64-bit rotate left by a compile-time amount as two v_alignbit_b32
@@ -175,7 +181,7 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
     h2 = add_rotl31(h2, h1); h2 = times5_plus(h2, 0x38495ab5);
   }
   const uint64_t* tt = tab + S::TAIL_BASE;
-  if (S::TAIL_TAB) {
+  if constexpr (S::TAIL_TAB) {
     const uint32_t w = S::NBLK ? lo : hi;
     h1 ^= tt[w >> (32 - 2 * S::TAIL)];  // includes ^= len
   } else {
@@ -276,6 +282,56 @@ __device__ __forceinline__ void insert_candidate(uint64_t* __restrict__ tab,
   atomicOr(flags, kFlagOverflow);  // table full
 }
 
+// Per-wave LDS queue of exact candidates (hash, genome slot).  Candidates
+// are rare (0.05% of k-mers at s = 1000, 0.4% at s = 10000) and arise in
+// scattered lanes; inserting each where it arises runs the atomicCAS probe
+// loop with one or two lanes active and exposes its latency once per
+// candidate.  Queued, they are inserted at segment ends, 32 or more at a
+// time, one per lane.  Everything is LDS atomics (no ballot: the hash loop
+// must stay fully unrolled, and the lanes of a wave diverge at run
+// boundaries): a push takes a position with ds_add; a push that finds the
+// ring full inserts directly; a drain hands out entries with ds_add too.
+constexpr uint32_t kQueue = 64;
+constexpr uint32_t kQueueDrain = 32;
+struct CandQueue {
+  uint64_t h[kQueue];
+  uint32_t slot[kQueue];
+  uint32_t head, tail, claim;
+};
+
+__device__ __forceinline__ void queue_push(CandQueue& q, uint64_t hv, uint32_t slot, uint64_t* __restrict__ table,
+                                           uint32_t cap_log2, uint32_t* __restrict__ flags) {
+  const uint32_t pos = atomicAdd(&q.tail, 1u);
+  if (pos - __atomic_load_n(&q.head, __ATOMIC_RELAXED) < kQueue) {
+    q.h[pos & (kQueue - 1)] = hv;
+    q.slot[pos & (kQueue - 1)] = slot;
+  } else {  // ring full: insert now
+    insert_candidate(table + ((uint64_t)slot << cap_log2), (1u << cap_log2) - 1u, flags + slot, hv);
+  }
+}
+
+// Insert the queued candidates with the lanes that are active (all of them
+// at the end of the kernel).  Positions past head + kQueue were inserted by
+// their pushes.
+__device__ __forceinline__ void queue_drain(CandQueue& q, uint64_t* __restrict__ table, uint32_t cap_log2,
+                                            uint32_t* __restrict__ flags, uint32_t min_pending) {
+  const uint32_t head = __atomic_load_n(&q.head, __ATOMIC_RELAXED);
+  const uint32_t tail = __atomic_load_n(&q.tail, __ATOMIC_RELAXED);
+  if (tail - head < min_pending || tail == head) return;
+  const uint32_t end = tail - head < kQueue ? tail : head + kQueue;
+  const uint32_t cap_mask = (1u << cap_log2) - 1u;
+  for (;;) {
+    const uint32_t e = atomicAdd(&q.claim, 1u);
+    if (e >= end) break;
+    const uint32_t x = e & (kQueue - 1);
+    const uint32_t sl = q.slot[x];
+    insert_candidate(table + ((uint64_t)sl << cap_log2), cap_mask, flags + sl, q.h[x]);
+  }
+  // every active lane is past its last claim here (lockstep): reopen the ring
+  __atomic_store_n(&q.head, tail, __ATOMIC_RELAXED);
+  __atomic_store_n(&q.claim, tail, __ATOMIC_RELAXED);
+}
+
 // Largest r with run_kstart[r] <= p, searching forward from `from`
 // (positions of one lane increase monotonically).
 __device__ __forceinline__ uint32_t find_run(const uint64_t* __restrict__ ks,
@@ -348,11 +404,13 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
   constexpr int kSeg = seg_len<K>();
   static_assert(K >= 1 && K <= 32 && kSeg + K - 1 <= 64 && kSeg % kGroup == 0, "window");
   __shared__ __attribute__((aligned(16))) uint64_t mtab[HashShape<K>::TAB_U64];  // murmur word tables (hash_parts)
+  __shared__ CandQueue queues[kBlock / 64];
+  CandQueue& q = queues[threadIdx.x >> 6];
+  if ((threadIdx.x & 63) == 0) q.head = q.tail = q.claim = 0;
   build_tables<K>(mtab);
   __syncthreads();
 
   const uint64_t seed = SEED0 ? 0ull : a.seed;
-  const uint32_t cap_mask = (1u << a.cap_log2) - 1u;
   const uint64_t nseg = (a.n_kmers + kSeg - 1) / kSeg;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   uint32_t r = 0;
@@ -374,7 +432,6 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
       // 2^32; every S passes when hi(tau) = 2^32 - 1)
       const uint32_t tau_hi = (uint32_t)(tau >> 32);
       const uint32_t thr = tau_hi == 0xFFFFFFFFu ? 0xFFFFFFFFu : tau_hi + 1u;
-      uint64_t* gset = a.table + ((uint64_t)slot << a.cap_log2);
       const uint64_t b = run.base + (p - rk0);  // first base of k-mer p
 
       const uint64_t wi = b >> 4;
@@ -411,8 +468,19 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
         for (int j = 0; j < kGroup; ++j)
           any |= (uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr;
         if (any) {
-          // rare (a lane of the wave has a k-mer whose high-word sum can
-          // reach tau): finish the exact test per candidate k-mer only
+#if GG_K1_QUEUE
+          // (a lane of the wave has a k-mer whose high-word sum can reach
+          // tau): finish the exact test for the group's k-mers and queue
+          // the candidates
+#pragma unroll
+          for (int j = 0; j < kGroup; ++j) {
+            const uint64_t hv = fmix_last(f1[j]) + fmix_last(f2[j]);
+            if (((uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr) &&
+                (uint32_t)(g * kGroup + j) < cnt && hv <= tau)
+              queue_push(q, hv, slot, a.table, a.cap_log2, a.flags);
+          }
+#else
+          // finish the exact test per candidate k-mer and insert it now
           uint32_t pending = 0;
 #pragma unroll
           for (int j = 0; j < kGroup; ++j)
@@ -423,51 +491,67 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
             pending &= pending - 1;
             uint64_t a1 = f1[0], a2 = f2[0];
 #pragma unroll
-            for (int q = 1; q < kGroup; ++q) {
-              a1 = (j == q) ? f1[q] : a1;
-              a2 = (j == q) ? f2[q] : a2;
+            for (int x = 1; x < kGroup; ++x) {
+              a1 = (j == x) ? f1[x] : a1;
+              a2 = (j == x) ? f2[x] : a2;
             }
             const uint64_t hv = fmix_last(a1) + fmix_last(a2);
-            if (hv <= tau) insert_candidate(gset, cap_mask, a.flags + slot, hv);
+            if (hv <= tau)
+              insert_candidate(a.table + ((uint64_t)slot << a.cap_log2), (1u << a.cap_log2) - 1u, a.flags + slot, hv);
           }
+#endif
         }
       }
       p = stop;
       if (p < pend) ++r;
     }
+    queue_drain(q, a.table, a.cap_log2, a.flags, kQueueDrain);
   }
+  queue_drain(q, a.table, a.cap_log2, a.flags, 1);  // every lane of the wave is back
 }
 
-// One workgroup per genome slot: gather the set, bitonic sort in LDS, keep
-// the first s.  Writes status[] for the host retry loop.  Any block size up
-// to kFinalizeMaxBlock (large sorts, one workgroup per CU: 1024 threads).
+// One workgroup per genome slot: gather the set into LDS, sort it, keep the
+// first s.  Writes status[] for the host retry loop.  The candidates are
+// distinct values spread uniformly over [0, tau], so they are sorted by
+// buckets of the top bits below tau (a counting sort: LDS histogram, scan,
+// scatter into the genome's own candidate table in HBM, which the next pass
+// re-initialises anyway), then every bucket (~4 values) is sorted in
+// registers by one thread: ~4 passes over the candidates instead of a
+// bitonic network's log2(n)(log2(n)+1)/2 (105 at s = 10000; 6.7 -> ~1 ms
+// per C5 step).  Any block size up to kFinalizeMaxBlock.
 constexpr int kFinalizeMaxBlock = 1024;
+constexpr uint32_t kBucketRegs = 16;  // bucket sizes sorted in registers (larger: in place)
 __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
     const uint32_t* __restrict__ slot_list, const uint32_t* __restrict__ slot_genome,
-    const uint64_t* __restrict__ tau, const uint64_t* __restrict__ table,
+    const uint64_t* __restrict__ tau, uint64_t* __restrict__ table,
     uint32_t cap_log2,
-    const uint32_t* __restrict__ flags, uint32_t s, uint32_t sort_pow2,
+    const uint32_t* __restrict__ flags, uint32_t s, uint32_t sort_pow2, uint32_t nb_log2,
     const uint32_t* __restrict__ row_of, uint64_t* __restrict__ out, uint32_t* __restrict__ lens,
     uint32_t* __restrict__ status) {
-  extern __shared__ uint64_t buf[];
+  extern __shared__ uint64_t buf[];  // [sort_pow2] values, then [1 << nb_log2] u32 bucket counters
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(buf + sort_pow2);
   __shared__ uint32_t fill;
+  __shared__ uint32_t wsum[kFinalizeMaxBlock / 64];
   const uint32_t slot = slot_list[blockIdx.x];
   // output row of the genome: the caller's row map when given (batches of a
   // streamed file list land on their global rows)
   const uint32_t g = row_of ? row_of[slot_genome[slot]] : slot_genome[slot];
   const uint32_t f = flags[slot];
+  const uint32_t T = blockDim.x, tid = threadIdx.x;
   if (f & kFlagOverflow) {
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
       status[slot] = kSketchRetrySmaller;
       lens[g] = 0;
     }
     return;
   }
-  if (threadIdx.x == 0) fill = 0;
+  const uint32_t NB = 1u << nb_log2;
+  if (tid == 0) fill = 0;
+  for (uint32_t i = tid; i < NB; i += T) cnt[i] = 0;
   __syncthreads();
-  const uint64_t* tab = table + ((uint64_t)slot << cap_log2);
+  uint64_t* tab = table + ((uint64_t)slot << cap_log2);
   const uint32_t cap = 1u << cap_log2;
-  for (uint32_t i = threadIdx.x; i < cap; i += blockDim.x) {
+  for (uint32_t i = tid; i < cap; i += T) {
     const uint64_t v = tab[i];
     if (v != kEmpty) {
       const uint32_t at = atomicAdd(&fill, 1u);
@@ -476,44 +560,95 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
   }
   __syncthreads();
   const uint32_t n = fill;  // distinct candidates <= tau
+  const uint64_t t = tau[slot];
   uint32_t st = kSketchOk;
   if (n > sort_pow2) st = kSketchRetrySmaller;  // cannot sort in LDS
-  else if (n < s && tau[slot] != kEmpty) st = kSketchRetryLarger;
+  else if (n < s && t != kEmpty) st = kSketchRetryLarger;
   if (st != kSketchOk) {
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
       status[slot] = st;
       lens[g] = 0;
     }
     return;
   }
-  uint32_t P = 1;
-  while (P < n) P <<= 1;
-  for (uint32_t i = n + threadIdx.x; i < P; i += blockDim.x) buf[i] = kEmpty;
+  // bucket = the nb_log2 bits below tau's top bit (monotone in the value)
+  const uint32_t tbits = 64 - __builtin_clzll(t | 1ull);
+  const uint32_t shift = tbits > nb_log2 ? tbits - nb_log2 : 0u;
+  for (uint32_t e = tid; e < n; e += T) atomicAdd(&cnt[(uint32_t)(buf[e] >> shift)], 1u);
   __syncthreads();
-  for (uint32_t size = 2; size <= P; size <<= 1) {
-    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-      for (uint32_t t = threadIdx.x; t < P / 2; t += blockDim.x) {
-        const uint32_t lo = 2 * t - (t & (stride - 1));
-        const uint32_t hi = lo + stride;
-        const bool up = ((lo & size) == 0);
-        const uint64_t x = buf[lo], y = buf[hi];
-        if ((x > y) == up) {
-          buf[lo] = y;
-          buf[hi] = x;
-        }
-      }
-      __syncthreads();
+  // exclusive scan of the counters: each thread a contiguous range, the
+  // ranges' totals scanned across waves
+  {
+    const uint32_t per = (NB + T - 1) / T;
+    const uint32_t b0 = min(tid * per, NB), b1 = min(b0 + per, NB);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b) sum += cnt[b];
+    uint32_t inc = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if ((tid & 63) >= (uint32_t)o) inc += y;
+    }
+    if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+    __syncthreads();
+    uint32_t run = inc - sum;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) run += wsum[w];
+    for (uint32_t b = b0; b < b1; ++b) {
+      const uint32_t c = cnt[b];
+      cnt[b] = run;
+      run += c;
     }
   }
-  uint32_t m = min(s, n);
-  uint64_t* o = out + (uint64_t)g * s;
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) o[i] = buf[i];
-  if ((f & kFlagSawMax) && m < s) {
-    if (threadIdx.x == 0) o[m] = kEmpty;  // 2^64-1 is the largest hash
-    ++m;
+  __syncthreads();
+  // scatter into the table (afterwards cnt[b] = end of bucket b)
+  for (uint32_t e = tid; e < n; e += T) {
+    const uint64_t v = buf[e];
+    tab[atomicAdd(&cnt[(uint32_t)(v >> shift)], 1u)] = v;
   }
-  if (threadIdx.x == 0) {
-    lens[g] = m;
+  __syncthreads();
+  // sort every bucket that starts below s; write the first s values
+  uint64_t* o = out + (uint64_t)g * s;
+  const uint32_t m = min(s, n);
+  for (uint32_t b = tid; b < NB; b += T) {
+    const uint32_t b0 = b ? cnt[b - 1] : 0u, b1 = cnt[b];
+    if (b0 >= m || b1 == b0) continue;
+    const uint32_t c = b1 - b0;
+    if (c <= kBucketRegs) {
+      uint64_t r[kBucketRegs];
+#pragma unroll
+      for (uint32_t q = 0; q < kBucketRegs; ++q) r[q] = q < c ? tab[b0 + q] : kEmpty;
+      // insertion sort, unrolled over the register array
+#pragma unroll
+      for (uint32_t q = 1; q < kBucketRegs; ++q) {
+#pragma unroll
+        for (uint32_t w = q; w > 0; --w) {
+          const uint64_t x = r[w - 1], y = r[w];
+          r[w - 1] = x < y ? x : y;
+          r[w] = x < y ? y : x;
+        }
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < kBucketRegs; ++q)
+        if (q < c && b0 + q < m) o[b0 + q] = r[q];
+    } else {  // a large bucket (never expected): insertion sort in place
+      for (uint32_t q = b0 + 1; q < b1; ++q) {
+        const uint64_t x = tab[q];
+        uint32_t w = q;
+        while (w > b0 && tab[w - 1] > x) {
+          tab[w] = tab[w - 1];
+          --w;
+        }
+        tab[w] = x;
+      }
+      for (uint32_t q = b0; q < b1 && q < m; ++q) o[q] = tab[q];
+    }
+  }
+  uint32_t mm = m;
+  if ((f & kFlagSawMax) && mm < s) {
+    if (tid == 0) o[mm] = kEmpty;  // 2^64-1 is the largest hash
+    ++mm;
+  }
+  if (tid == 0) {
+    lens[g] = mm;
     status[slot] = kSketchOk;
   }
 }
@@ -547,14 +682,17 @@ hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,
 
 hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   const uint32_t* slot_genome,
-                                  const uint64_t* tau, const uint64_t* table,
+                                  const uint64_t* tau, uint64_t* table,
                                   uint32_t cap_log2,
                                   const uint32_t* flags, uint32_t s,
                                   uint32_t sort_pow2, const uint32_t* row_of, uint64_t* out,
                                   uint32_t* lens, uint32_t* status,
                                   hipStream_t st) {
   if (n_slots == 0) return hipSuccess;
-  const size_t lds = (size_t)sort_pow2 * sizeof(uint64_t);
+  // ~4 candidates per bucket
+  uint32_t nb_log2 = 6;
+  while (nb_log2 < 12 && (1u << (nb_log2 + 2)) < sort_pow2) ++nb_log2;
+  const size_t lds = (size_t)sort_pow2 * sizeof(uint64_t) + ((size_t)4 << nb_log2);
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)sketch_finalize_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -565,7 +703,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
   const int threads = sort_pow2 >= 4096 ? kFinalizeMaxBlock : kBlock;
   hipLaunchKernelGGL(sketch_finalize_kernel, dim3(n_slots), dim3(threads), lds, st,
                      slot_list, slot_genome, tau, table, cap_log2, flags, s,
-                     sort_pow2, row_of, out, lens, status);
+                     sort_pow2, nb_log2, row_of, out, lens, status);
   return hipGetLastError();
 }
 
