@@ -406,6 +406,8 @@ gg_status pairs_gate(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
                      uint64_t cap, uint64_t* d_count, uint64_t work, hipStream_t st) {
   constexpr uint32_t kGateXcdRun = 64;  // ~ workgroups resident per XCD (32 CUs x 2)
   const GateParams gp = gate_params(c->s);
+  if (gp.cap > 65535u || c->s > kMaxSketch)
+    return fail(c, GG_ERR_INTERNAL, "gate kernel: R * s exceeds its 16-bit positions");
   std::vector<PairSeg> items;
   uint32_t I0 = UINT32_MAX, I1 = 0;
   {
@@ -723,7 +725,7 @@ gg_ctx* gg_create(int kmer_length, uint32_t sketch_size, uint64_t hash_seed, int
                   gg_status* status) {
   gg_status dummy;
   if (!status) status = &dummy;
-  if (kmer_length < 1 || kmer_length > 32 || sketch_size < 1 || sketch_size > 12000) {
+  if (kmer_length < 1 || kmer_length > 32 || sketch_size < 1 || sketch_size > kMaxSketch) {
     *status = fail(nullptr, GG_ERR_INVALID_ARG, "kmer_length must be 1..32 and sketch_size 1..12000");
     return nullptr;
   }

@@ -97,6 +97,13 @@ hipError_t launch_pairs_table(const PairsTableLaunch& a, hipStream_t st);
 
 // pairs_gate.hip: the gated-table pair kernel (default K2).
 constexpr uint32_t kGateCap = 32768;    // keys per row block (R * s)
+// Largest sketch size gg_create accepts, and the gate kernel bounds that
+// depend on it: its per-lane 8-bit row counters hold at most ceil(s / 64)
+// hits per lane, bucket starts / counts and queued column positions are
+// 16-bit (R * s <= 65535).  gate_params() re-checks R * s at run time.
+constexpr uint32_t kMaxSketch = 12000;
+static_assert((kMaxSketch + 63) / 64 <= 255, "gate kernel: 8-bit per-lane row counters");
+static_assert(kMaxSketch <= 65535, "gate kernel: 16-bit column positions and bucket starts");
 constexpr uint32_t kGateRowsMax = 32;   // rows per row block (bits of a row mask)
 constexpr uint32_t kGateSegTiles = 8;   // column tiles per work item
 struct GateParams {
@@ -110,7 +117,7 @@ struct GateParams {
   uint32_t wide;      // two-bit gate + directory in LDS (large sketches)
   uint64_t block_bytes;
 };
-GateParams gate_params(uint32_t s);  // requires s <= kGateCap
+GateParams gate_params(uint32_t s);  // requires s <= kMaxSketch (cap = R * s <= 65535)
 struct GateBuildLaunch {
   const uint64_t* sketches;
   const uint32_t* lens;

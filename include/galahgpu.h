@@ -189,7 +189,9 @@ void gg_pair_partition(uint32_t n, uint32_t parts, uint32_t part,
  * src/finch.rs:56-69 does. */
 gg_status gg_pairs(gg_ctx* ctx, const uint64_t* sketches, const uint32_t* lens,
                    uint32_t n, float min_ani, gg_pair** out, uint64_t* n_out);
-/* Device-resident: sketches [n x sketch_size] u64, lens [n] u32.
+/* Device-resident: sketches [n x sketch_size] u64, lens [n] u32 with every
+ * lens[i] <= sketch_size and row i ascending in its first lens[i] entries
+ * (not checked on the device; gg_pairs checks the lengths of host input).
  * Appends passing pairs of tiles [tile_begin, tile_end) to d_out (unsorted),
  * *d_count (device u64) incremented by the number found; entries past
  * out_cap are dropped (caller compares *d_count with out_cap). Async. */
