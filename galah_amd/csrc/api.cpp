@@ -287,21 +287,29 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
         run_src = sub.data();
         nr = sub.size();
       }
-      std::vector<uint64_t>& rk = c->kstart_host;
-      rk.resize(nr + 1);
-      uint64_t kacc = 0;
       const uint32_t kk = (uint32_t)c->k;
+      // K1 segments never straddle runs: run r owns segments
+      // [rs[r], rs[r + 1]), ceil(k-mers / seg) of them, so every lane of a
+      // wave hashes exactly one piece per segment (a segment across a run
+      // boundary made its wave run the hashing loop twice: +30% VALU at C5,
+      // where runs are ~10 kb)
+      const uint32_t seg = (uint32_t)sketch_segment_len(c->k);
+      std::vector<uint64_t>& rs = c->sstart_host;
+      rs.resize(nr + 1);
+      uint64_t kacc = 0, sacc = 0;
       for (uint64_t r = 0; r < nr; ++r) {
-        rk[r] = kacc;
-        kacc += run_src[r].len - kk + 1;
+        rs[r] = sacc;
+        const uint64_t nk = run_src[r].len - kk + 1;
+        kacc += nk;
+        sacc += (nk + seg - 1) / seg;
       }
-      rk[nr] = kacc;
+      rs[nr] = sacc;
       gg_run* d_runs;
-      uint64_t* d_rk;
+      uint64_t* d_rs;
       GG_HIP(c, scratch_t(c, "runs", std::max<size_t>(nr, 1), &d_runs));
-      GG_HIP(c, scratch_t(c, "run_kstart", nr + 1, &d_rk));
+      GG_HIP(c, scratch_t(c, "run_sstart", nr + 1, &d_rs));
       if (nr) GG_HIP(c, hipMemcpyAsync(d_runs, run_src, nr * sizeof(gg_run), hipMemcpyHostToDevice, st));
-      GG_HIP(c, hipMemcpyAsync(d_rk, rk.data(), (nr + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+      GG_HIP(c, hipMemcpyAsync(d_rs, rs.data(), (nr + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
       GG_HIP(c, hipMemcpyAsync(d_tau, h_tau.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
       GG_HIP(c, hipMemcpyAsync(d_slot_list, active.data(), active.size() * sizeof(uint32_t),
                                hipMemcpyHostToDevice, st));
@@ -318,17 +326,16 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       a.words = d_words;
       a.n_words = n_words;
       a.runs = d_runs;
-      a.run_kstart = d_rk;
+      a.run_sstart = d_rs;
       a.slot_genome0 = g0;
       a.n_runs = (uint32_t)nr;
-      a.n_kmers = kacc;
+      a.n_segs = sacc;
       a.tau = d_tau;
       a.table = d_table;
       a.cap_log2 = geom.cap_log2;
       a.flags = d_flags;
       a.seed = c->seed;
-      const uint64_t segs = (kacc + 31) / 32;
-      const int g = (int)std::min<uint64_t>((uint64_t)grid, std::max<uint64_t>(1, (segs + 255) / 256));
+      const int g = (int)std::min<uint64_t>((uint64_t)grid, std::max<uint64_t>(1, (sacc + 255) / 256));
       GG_HIP(c, timed_launch(c, GG_KERNEL_SKETCH, kacc, st,
                              [&] { return launch_sketch_candidates(c->k, a, g, st); }));
       GG_HIP(c, timed_launch(c, GG_KERNEL_FINALIZE, active.size(), st, [&] {

@@ -39,7 +39,7 @@ struct gg_ctx {
     uint64_t work;
   };
   std::vector<gg::PairSeg> seg_host;
-  std::vector<uint64_t> kstart_host;
+  std::vector<uint64_t> sstart_host;
   int pairs_kernel = 0;  // GALAHGPU_PAIRS_KERNEL: 0 auto, 1 table, 2 merge, 3 gate, 4 index
   std::vector<uint32_t> sufmin_host;
   bool timing = false;

@@ -29,14 +29,20 @@ constexpr uint32_t kFlagSawMax = 2u;
 // Largest number of candidates the finalize kernel sorts in LDS.
 constexpr uint32_t kSortCap = 16384;
 
+// K1 segment: k-mer positions one lane hashes from one 64-base window
+// (k = 21: 44), a multiple of the tau-branch group g, capped to bound the
+// unrolled code.  Segments never straddle runs (sketch_core).
+inline constexpr int k1_seg_len(int k, int g) { return ((65 - k) / g) * g < 48 ? ((65 - k) / g) * g : 48; }
+int sketch_segment_len(int k);  // k1_seg_len at K1's tau-branch group
+
 struct SketchLaunch {
   const uint32_t* words;
   uint64_t n_words;
   const gg_run* runs;          // [n_runs] (genome - slot_genome0 = slot within the batch)
-  const uint64_t* run_kstart;  // [n_runs + 1] exclusive prefix of k-mer counts
+  const uint64_t* run_sstart;  // [n_runs + 1] exclusive prefix of per-run segment counts
   uint32_t slot_genome0;       // genome of batch slot 0
   uint32_t n_runs;
-  uint64_t n_kmers;
+  uint64_t n_segs;
   const uint64_t* tau;         // [slots]
   uint64_t* table;             // [slots << cap_log2]
   uint32_t cap_log2;

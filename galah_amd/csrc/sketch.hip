@@ -31,11 +31,7 @@
 namespace gg {
 namespace {
 
-constexpr int kGroup = 4;       // k-mers per tau-check branch
-// k-mer positions per lane per segment: as many as one 64-base window holds
-// (k = 21: 44), capped to bound the unrolled code
-template <int K>
-constexpr int seg_len() { return ((65 - K) / kGroup) * kGroup < 48 ? ((65 - K) / kGroup) * kGroup : 48; }
+constexpr int kGroup = 4;  // k-mers per tau-check branch (1 measured no faster, even at s = 10000)
 constexpr int kBlock = 256;
 // min waves per SIMD forced on the register allocator: 7 (72 VGPRs, 4 dwords
 // spilled at k = 21) beats the unconstrained 76 VGPRs / 6 waves with the
@@ -332,8 +328,8 @@ __device__ __forceinline__ void queue_drain(CandQueue& q, uint64_t* __restrict__
   __atomic_store_n(&q.claim, tail, __ATOMIC_RELAXED);
 }
 
-// Largest r with run_kstart[r] <= p, searching forward from `from`
-// (positions of one lane increase monotonically).
+// Largest r with ks[r] <= p, searching forward from `from` (the segments
+// of one lane increase monotonically).
 __device__ __forceinline__ uint32_t find_run(const uint64_t* __restrict__ ks,
                                              uint32_t n_runs, uint64_t p,
                                              uint32_t from) {
@@ -391,17 +387,17 @@ __device__ __forceinline__ uint64_t window64(const uint32_t (&w)[4], const uint6
   return ((uint64_t)window32(w, t) << 32) | window32(w, t + 16);
 }
 
-// Each lane owns kSeg consecutive k-mer positions.  For every maximal piece
-// of the segment inside one run it loads the 64-base window starting at the
-// piece's first base (5 words, funnel-shifted to the base offset) and its
-// reverse complement.  The forward and reverse-complement codes of k-mer i
-// of the window are then static 64-bit slices of the two windows, top-aligned
-// (bits below the k-mer hold the following bases and are ignored): no
-// rolling state, and the canonical code is a 64-bit min.  K-mers past the
-// piece (i >= cnt) are hashed but never inserted.
+// Each lane owns one segment: kSeg consecutive k-mer positions of one run
+// (the last segment of a run is shorter).  It loads the 64-base window
+// starting at the segment's first base (5 words, funnel-shifted to the base
+// offset) and its reverse complement.  The forward and reverse-complement
+// codes of k-mer i of the window are then static 64-bit slices of the two
+// windows, top-aligned (bits below the k-mer hold the following bases and
+// are ignored): no rolling state, and the canonical code is a 64-bit min.
+// K-mers past the segment (i >= cnt) are hashed but never inserted.
 template <int K, bool SEED0>
 __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_kernel(SketchLaunch a) {
-  constexpr int kSeg = seg_len<K>();
+  constexpr int kSeg = k1_seg_len(K, kGroup);
   static_assert(K >= 1 && K <= 32 && kSeg + K - 1 <= 64 && kSeg % kGroup == 0, "window");
   __shared__ __attribute__((aligned(16))) uint64_t mtab[HashShape<K>::TAB_U64];  // murmur word tables (hash_parts)
   __shared__ CandQueue queues[kBlock / 64];
@@ -411,99 +407,91 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
   __syncthreads();
 
   const uint64_t seed = SEED0 ? 0ull : a.seed;
-  const uint64_t nseg = (a.n_kmers + kSeg - 1) / kSeg;
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   uint32_t r = 0;
 
-  for (uint64_t seg = (uint64_t)blockIdx.x * kBlock + threadIdx.x; seg < nseg; seg += stride) {
-    uint64_t p = seg * kSeg;
-    const uint64_t pend = min(p + (uint64_t)kSeg, a.n_kmers);
-    r = find_run(a.run_kstart, a.n_runs, p, r);
-    while (p < pend) {
-      const uint64_t rk0 = a.run_kstart[r];
-      const uint64_t stop = min(pend, a.run_kstart[r + 1]);
-      const uint32_t cnt = (uint32_t)(stop - p);
-      const gg_run run = a.runs[r];
-      const uint32_t slot = run.genome - a.slot_genome0;
-      const uint64_t tau = a.tau[slot];
-      // prefilter on the high words: h = fmix_last(f1) + fmix_last(f2)
-      // has high word S or S + 1 (carry), S = hi(f1) + hi(f2), so h <= tau
-      // needs S <= hi(tau) or S = 2^32 - 1, i.e. S + 1 <= hi(tau) + 1 (mod
-      // 2^32; every S passes when hi(tau) = 2^32 - 1)
-      const uint32_t tau_hi = (uint32_t)(tau >> 32);
-      const uint32_t thr = tau_hi == 0xFFFFFFFFu ? 0xFFFFFFFFu : tau_hi + 1u;
-      const uint64_t b = run.base + (p - rk0);  // first base of k-mer p
+  for (uint64_t sg = (uint64_t)blockIdx.x * kBlock + threadIdx.x; sg < a.n_segs; sg += stride) {
+    r = find_run(a.run_sstart, a.n_runs, sg, r);
+    const gg_run run = a.runs[r];
+    const uint32_t k0 = (uint32_t)(sg - a.run_sstart[r]) * (uint32_t)kSeg;  // first k-mer of the segment in the run
+    const uint32_t cnt = min((uint32_t)kSeg, run.len - (uint32_t)K + 1u - k0);
+    const uint32_t slot = run.genome - a.slot_genome0;
+    const uint64_t tau = a.tau[slot];
+    // prefilter on the high words: h = fmix_last(f1) + fmix_last(f2)
+    // has high word S or S + 1 (carry), S = hi(f1) + hi(f2), so h <= tau
+    // needs S <= hi(tau) or S = 2^32 - 1, i.e. S + 1 <= hi(tau) + 1 (mod
+    // 2^32; every S passes when hi(tau) = 2^32 - 1)
+    const uint32_t tau_hi = (uint32_t)(tau >> 32);
+    const uint32_t thr = tau_hi == 0xFFFFFFFFu ? 0xFFFFFFFFu : tau_hi + 1u;
+    const uint64_t b = run.base + k0;  // first base of the segment's first k-mer
 
-      const uint64_t wi = b >> 4;
-      const uint32_t off = (uint32_t)b & 15u;
-      uint32_t w[5];
+    const uint64_t wi = b >> 4;
+    const uint32_t off = (uint32_t)b & 15u;
+    uint32_t w[5];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) w[j] = (wi + j < a.n_words) ? a.words[wi + j] : 0u;
-      uint32_t F[4], R[4];
+    for (int j = 0; j < 5; ++j) w[j] = (wi + j < a.n_words) ? a.words[wi + j] : 0u;
+    uint32_t F[4], R[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        F[j] = off ? __builtin_amdgcn_alignbit(w[j], w[j + 1], 32 - 2 * off) : w[j];
+    for (int j = 0; j < 4; ++j)
+      F[j] = off ? __builtin_amdgcn_alignbit(w[j], w[j + 1], 32 - 2 * off) : w[j];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) R[m] = revcomp16(F[3 - m]);
-      uint64_t FP[4], RP[4];
+    for (int m = 0; m < 4; ++m) R[m] = revcomp16(F[3 - m]);
+    uint64_t FP[4], RP[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        FP[m] = ((uint64_t)F[m] << 32) | (m + 1 < 4 ? F[m + 1] : 0u);
-        RP[m] = ((uint64_t)R[m] << 32) | (m + 1 < 4 ? R[m + 1] : 0u);
+    for (int m = 0; m < 4; ++m) {
+      FP[m] = ((uint64_t)F[m] << 32) | (m + 1 < 4 ? F[m + 1] : 0u);
+      RP[m] = ((uint64_t)R[m] << 32) | (m + 1 < 4 ? R[m + 1] : 0u);
+    }
+
+#pragma unroll
+    for (int g = 0; g < kSeg / kGroup; ++g) {
+      uint64_t f1[kGroup], f2[kGroup];
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) {
+        const int i = g * kGroup + j;
+        const uint64_t fwd = window64<K>(F, FP, i);
+        const int t0 = 64 - K - i;  // reverse complement of k-mer i starts here
+        const uint64_t rev = window64<K>(R, RP, t0);
+        hash_parts<K>(fwd < rev ? fwd : rev, mtab, seed, f1[j], f2[j]);
       }
-
+      bool any = false;
 #pragma unroll
-      for (int g = 0; g < kSeg / kGroup; ++g) {
-        uint64_t f1[kGroup], f2[kGroup];
+      for (int j = 0; j < kGroup; ++j)
+        any |= (uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr;
+      if (any) {
+#if GG_K1_QUEUE
+        // (a lane of the wave has a k-mer whose high-word sum can reach
+        // tau): finish the exact test for the group's k-mers and queue
+        // the candidates
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
-          const int i = g * kGroup + j;
-          const uint64_t fwd = window64<K>(F, FP, i);
-          const int t0 = 64 - K - i;  // reverse complement of k-mer i starts here
-          const uint64_t rev = window64<K>(R, RP, t0);
-          hash_parts<K>(fwd < rev ? fwd : rev, mtab, seed, f1[j], f2[j]);
+          const uint64_t hv = fmix_last(f1[j]) + fmix_last(f2[j]);
+          if (((uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr) &&
+              (uint32_t)(g * kGroup + j) < cnt && hv <= tau)
+            queue_push(q, hv, slot, a.table, a.cap_log2, a.flags);
         }
-        bool any = false;
+#else
+        // finish the exact test per candidate k-mer and insert it now
+        uint32_t pending = 0;
 #pragma unroll
         for (int j = 0; j < kGroup; ++j)
-          any |= (uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr;
-        if (any) {
-#if GG_K1_QUEUE
-          // (a lane of the wave has a k-mer whose high-word sum can reach
-          // tau): finish the exact test for the group's k-mers and queue
-          // the candidates
+          pending |= (((uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr) &
+                      ((uint32_t)(g * kGroup + j) < cnt)) ? (1u << j) : 0u;
+        while (pending) {
+          const int j = __builtin_ctz(pending);
+          pending &= pending - 1;
+          uint64_t a1 = f1[0], a2 = f2[0];
 #pragma unroll
-          for (int j = 0; j < kGroup; ++j) {
-            const uint64_t hv = fmix_last(f1[j]) + fmix_last(f2[j]);
-            if (((uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr) &&
-                (uint32_t)(g * kGroup + j) < cnt && hv <= tau)
-              queue_push(q, hv, slot, a.table, a.cap_log2, a.flags);
+          for (int x = 1; x < kGroup; ++x) {
+            a1 = (j == x) ? f1[x] : a1;
+            a2 = (j == x) ? f2[x] : a2;
           }
-#else
-          // finish the exact test per candidate k-mer and insert it now
-          uint32_t pending = 0;
-#pragma unroll
-          for (int j = 0; j < kGroup; ++j)
-            pending |= (((uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr) &
-                        ((uint32_t)(g * kGroup + j) < cnt)) ? (1u << j) : 0u;
-          while (pending) {
-            const int j = __builtin_ctz(pending);
-            pending &= pending - 1;
-            uint64_t a1 = f1[0], a2 = f2[0];
-#pragma unroll
-            for (int x = 1; x < kGroup; ++x) {
-              a1 = (j == x) ? f1[x] : a1;
-              a2 = (j == x) ? f2[x] : a2;
-            }
-            const uint64_t hv = fmix_last(a1) + fmix_last(a2);
-            if (hv <= tau)
-              insert_candidate(a.table + ((uint64_t)slot << a.cap_log2), (1u << a.cap_log2) - 1u, a.flags + slot, hv);
-          }
-#endif
+          const uint64_t hv = fmix_last(a1) + fmix_last(a2);
+          if (hv <= tau)
+            insert_candidate(a.table + ((uint64_t)slot << a.cap_log2), (1u << a.cap_log2) - 1u, a.flags + slot, hv);
         }
+#endif
       }
-      p = stop;
-      if (p < pend) ++r;
     }
     queue_drain(q, a.table, a.cap_log2, a.flags, kQueueDrain);
   }
@@ -666,9 +654,11 @@ hipError_t launch_k(const SketchLaunch& a, int grid, hipStream_t st) {
 
 }  // namespace
 
+int sketch_segment_len(int k) { return k1_seg_len(k, kGroup); }
+
 hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,
                                     hipStream_t st) {
-  if (a.n_kmers == 0) return hipSuccess;
+  if (a.n_segs == 0) return hipSuccess;
   switch (k) {
 #define GG_K(N) case N: return launch_k<N>(a, grid, st);
     GG_K(1) GG_K(2) GG_K(3) GG_K(4) GG_K(5) GG_K(6) GG_K(7) GG_K(8)
