@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -12,6 +13,7 @@
 #include <mutex>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "context.hpp"
@@ -188,46 +190,121 @@ bool advance_tau(TauSearch& t, uint32_t status) {
   return true;
 }
 
-gg_status validate_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t n_genomes,
-                        uint64_t n_words) {
-  uint32_t prev = 0;
-  for (uint64_t r = 0; r < n_runs; ++r) {
-    const gg_run& x = runs[r];
+// f(t, begin, end) over T contiguous chunks of [0, n) on T threads.
+template <class F>
+void parallel_chunks(uint64_t n, int T, F&& f) {
+  if (T <= 1 || n < 2) {
+    f(0, (uint64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 1; t < T; ++t) th.emplace_back([&, t] { f(t, n * t / T, n * (t + 1) / T); });
+  f(0, (uint64_t)0, n / T);
+  for (auto& x : th) x.join();
+}
+
+// One parallel pass over the caller's run table: checks it (grouped by
+// non-decreasing genome < n_genomes, every run >= k bases and inside the
+// packed words), and lays out what K1 needs: the first run of every genome,
+// every genome's k-mer count (for its initial tau) and the start of every
+// run's K1 segments (ceil(k-mers / seg) per run, exclusive prefix; entry
+// n_runs = the total).  C5's 3.6M runs: 11 ms in four serial loops before.
+struct RunIndex {
+  std::vector<uint64_t> gr;  // [n_genomes + 1]
+  std::vector<uint64_t> nk;  // [n_genomes]
+  std::vector<uint64_t> rs;  // [n_runs + 1]
+};
+
+gg_status index_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t n_genomes, uint64_t n_words,
+                     uint32_t seg, RunIndex& ix) {
+  const int T = n_runs >= (1u << 18) ? std::max(1, std::min(16, ingest_threads(c->host_threads))) : 1;
+  const uint32_t k = (uint32_t)c->k;
+  ix.gr.assign((size_t)n_genomes + 1, ~0ull);
+  ix.rs.resize(n_runs + 1);
+  std::vector<uint64_t> bad(T, ~0ull), csum(T, 0);
+  parallel_chunks(n_runs, T, [&](int t, uint64_t b, uint64_t e) {
+    uint64_t segs = 0;
+    for (uint64_t r = b; r < e; ++r) {
+      const gg_run& x = runs[r];
+      const uint32_t prev = r ? runs[r - 1].genome : 0u;
+      if (x.genome >= n_genomes || x.genome < prev || x.len < k || x.base + x.len > n_words * 16ull) {
+        bad[t] = r;
+        return;
+      }
+      if (r == 0 || x.genome != prev) ix.gr[x.genome] = r;
+      ix.rs[r] = (x.len - k + 1 + seg - 1) / seg;
+      segs += ix.rs[r];
+    }
+    csum[t] = segs;
+  });
+  const uint64_t first_bad = *std::min_element(bad.begin(), bad.end());
+  if (first_bad != ~0ull) {
+    const gg_run& x = runs[first_bad];
+    const uint32_t prev = first_bad ? runs[first_bad - 1].genome : 0u;
     if (x.genome >= n_genomes || x.genome < prev)
       return fail(c, GG_ERR_INVALID_ARG, "runs must be grouped by non-decreasing genome < n_genomes");
-    if (x.len < (uint32_t)c->k)
-      return fail(c, GG_ERR_INVALID_ARG, "run shorter than k");
-    if (x.base + x.len > n_words * 16ull)
-      return fail(c, GG_ERR_INVALID_ARG, "run extends past the packed words");
-    prev = x.genome;
+    if (x.len < k) return fail(c, GG_ERR_INVALID_ARG, "run shorter than k");
+    return fail(c, GG_ERR_INVALID_ARG, "run extends past the packed words");
   }
+  ix.gr[n_genomes] = n_runs;
+  for (uint32_t g = n_genomes; g-- > 0;)  // genomes without runs start where the next one does
+    if (ix.gr[g] == ~0ull) ix.gr[g] = ix.gr[g + 1];
+  std::vector<uint64_t> coff(T + 1, 0);
+  for (int t = 0; t < T; ++t) coff[t + 1] = coff[t] + csum[t];
+  ix.rs[n_runs] = coff[T];
+  ix.nk.assign(n_genomes, 0);
+  parallel_chunks(n_runs, T, [&](int t, uint64_t b, uint64_t e) {
+    uint64_t acc = coff[t];
+    for (uint64_t r = b; r < e; ++r) {
+      const uint64_t v = ix.rs[r];
+      ix.rs[r] = acc;
+      acc += v;
+    }
+  });
+  parallel_chunks(n_genomes, T, [&](int, uint64_t b, uint64_t e) {
+    for (uint64_t g = b; g < e; ++g) {
+      uint64_t nk = 0;
+      for (uint64_t r = ix.gr[g]; r < ix.gr[g + 1]; ++r) nk += runs[r].len - k + 1;
+      ix.nk[g] = nk;
+    }
+  });
   return GG_OK;
 }
 
 }  // namespace
 
+// GALAHGPU_HOST_PROFILE=1: per-stage host wall times of sketch_core on stderr
+struct HostProf {
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  HostProf() : on(getenv("GALAHGPU_HOST_PROFILE") != nullptr), t(std::chrono::steady_clock::now()) {}
+  void mark(const char* what) {
+    if (!on) return;
+    const auto n = std::chrono::steady_clock::now();
+    fprintf(stderr, "[sketch_core] %-24s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+    t = n;
+  }
+};
+
 gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, const gg_run* runs,
                       uint64_t n_runs, uint32_t n_genomes, uint64_t* d_out, uint32_t* d_lens,
                       const uint32_t* d_row_of, hipStream_t st) {
-  gg_status vs = validate_runs(c, runs, n_runs, n_genomes, n_words);
+  HostProf hp;
+  if (n_genomes == 0) {
+    if (n_runs) return fail(c, GG_ERR_INVALID_ARG, "runs must be grouped by non-decreasing genome < n_genomes");
+    return GG_OK;
+  }
+  const uint32_t seg = (uint32_t)sketch_segment_len(c->k);
+  RunIndex ix;
+  gg_status vs = index_runs(c, runs, n_runs, n_genomes, n_words, seg, ix);
   if (vs != GG_OK) return vs;
-  if (n_genomes == 0) return GG_OK;
+  hp.mark("index runs");
   const SketchGeom geom = sketch_geom(c->s);
   const uint64_t cap = 1ull << geom.cap_log2;
   // genomes per batch: tables limited to ~4 GiB
   const uint32_t max_batch = (uint32_t)std::max<uint64_t>(
       1, std::min<uint64_t>(n_genomes, (4ull << 30) / (cap * sizeof(uint64_t))));
-
-  // per-genome run ranges
-  std::vector<uint64_t> gr(n_genomes + 1, n_runs);
-  {
-    uint64_t r = 0;
-    for (uint32_t g = 0; g < n_genomes; ++g) {
-      while (r < n_runs && runs[r].genome < g) ++r;
-      gr[g] = r;
-    }
-    gr[n_genomes] = n_runs;
-  }
+  const std::vector<uint64_t>& gr = ix.gr;
 
   int n_cu = 256;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -260,15 +337,14 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
     std::vector<uint64_t> h_tau(nb);
     std::vector<uint32_t> h_slot_genome(nb), h_slot_list(nb);
     for (uint32_t i = 0; i < nb; ++i) {
-      uint64_t nk = 0;
-      for (uint64_t r = gr[g0 + i]; r < gr[g0 + i + 1]; ++r) nk += runs[r].len - c->k + 1;
-      ts[i].tau = initial_tau(nk, c->s, geom.over);
+      ts[i].tau = initial_tau(ix.nk[g0 + i], c->s, geom.over);
       h_tau[i] = ts[i].tau;
       h_slot_genome[i] = g0 + i;
       h_slot_list[i] = i;
     }
     GG_HIP(c, hipMemcpyAsync(d_slot_genome, h_slot_genome.data(), nb * sizeof(uint32_t),
                              hipMemcpyHostToDevice, st));
+    hp.mark("initial tau");
 
     // active genome slots for this pass
     std::vector<uint32_t> active = h_slot_list;
@@ -287,32 +363,40 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
         run_src = sub.data();
         nr = sub.size();
       }
-      const uint32_t kk = (uint32_t)c->k;
       // K1 segments never straddle runs: run r owns segments
       // [rs[r], rs[r + 1]), ceil(k-mers / seg) of them, so every lane of a
       // wave hashes exactly one piece per segment (a segment across a run
       // boundary made its wave run the hashing loop twice: +30% VALU at C5,
-      // where runs are ~10 kb)
-      const uint32_t seg = (uint32_t)sketch_segment_len(c->k);
-      std::vector<uint64_t>& rs = c->sstart_host;
-      rs.resize(nr + 1);
-      uint64_t kacc = 0, sacc = 0;
-      for (uint64_t r = 0; r < nr; ++r) {
-        rs[r] = sacc;
-        const uint64_t nk = run_src[r].len - kk + 1;
-        kacc += nk;
-        sacc += (nk + seg - 1) / seg;
+      // where runs are ~10 kb).  First pass: the batch's slice of the index
+      // (segments numbered from rs[first run]); retries: the subset's own.
+      const uint64_t* rs = ix.rs.data() + gr[g0];
+      uint64_t kacc = 0;
+      if (!all) {
+        std::vector<uint64_t>& sub_rs = c->sstart_host;
+        sub_rs.resize(nr + 1);
+        uint64_t sacc = 0;
+        for (uint64_t r = 0; r < nr; ++r) {
+          sub_rs[r] = sacc;
+          sacc += (run_src[r].len - (uint32_t)c->k + 1 + seg - 1) / seg;
+        }
+        sub_rs[nr] = sacc;
+        rs = sub_rs.data();
+        for (uint32_t slot : active) kacc += ix.nk[g0 + slot];
+      } else {
+        for (uint32_t i = 0; i < nb; ++i) kacc += ix.nk[g0 + i];
       }
-      rs[nr] = sacc;
+      const uint64_t seg0 = rs[0], sacc = rs[nr] - rs[0];
+      hp.mark("segment starts");
       gg_run* d_runs;
       uint64_t* d_rs;
       GG_HIP(c, scratch_t(c, "runs", std::max<size_t>(nr, 1), &d_runs));
       GG_HIP(c, scratch_t(c, "run_sstart", nr + 1, &d_rs));
       if (nr) GG_HIP(c, hipMemcpyAsync(d_runs, run_src, nr * sizeof(gg_run), hipMemcpyHostToDevice, st));
-      GG_HIP(c, hipMemcpyAsync(d_rs, rs.data(), (nr + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+      GG_HIP(c, hipMemcpyAsync(d_rs, rs, (nr + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
       GG_HIP(c, hipMemcpyAsync(d_tau, h_tau.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
       GG_HIP(c, hipMemcpyAsync(d_slot_list, active.data(), active.size() * sizeof(uint32_t),
                                hipMemcpyHostToDevice, st));
+      hp.mark("H2D runs/starts");
       if (pass == 0) {
         GG_HIP(c, hipMemsetAsync(d_table, 0xFF, (size_t)nb * cap * sizeof(uint64_t), st));
         GG_HIP(c, hipMemsetAsync(d_flags, 0, nb * sizeof(uint32_t), st));
@@ -329,6 +413,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       a.run_sstart = d_rs;
       a.slot_genome0 = g0;
       a.n_runs = (uint32_t)nr;
+      a.seg0 = seg0;
       a.n_segs = sacc;
       a.tau = d_tau;
       a.table = d_table;
@@ -343,9 +428,11 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
                                       d_table, geom.cap_log2, d_flags, c->s,
                                       geom.sort_pow2, d_row_of, d_out, d_lens, d_status, st);
       }));
+      hp.mark("enqueue K1 + finalize");
       std::vector<uint32_t> status(nb);
       GG_HIP(c, hipMemcpyAsync(status.data(), d_status, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
       GG_HIP(c, hipStreamSynchronize(st));
+      hp.mark("wait (GPU)");
       std::vector<uint32_t> next;
       for (uint32_t slot : active) {
         if (status[slot] == kSketchOk) continue;

@@ -39,9 +39,10 @@ struct SketchLaunch {
   const uint32_t* words;
   uint64_t n_words;
   const gg_run* runs;          // [n_runs] (genome - slot_genome0 = slot within the batch)
-  const uint64_t* run_sstart;  // [n_runs + 1] exclusive prefix of per-run segment counts
+  const uint64_t* run_sstart;  // [n_runs + 1] first segment of each run (segments seg0 .. seg0 + n_segs)
   uint32_t slot_genome0;       // genome of batch slot 0
   uint32_t n_runs;
+  uint64_t seg0;
   uint64_t n_segs;
   const uint64_t* tau;         // [slots]
   uint64_t* table;             // [slots << cap_log2]

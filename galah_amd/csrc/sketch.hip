@@ -410,7 +410,8 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   uint32_t r = 0;
 
-  for (uint64_t sg = (uint64_t)blockIdx.x * kBlock + threadIdx.x; sg < a.n_segs; sg += stride) {
+  const uint64_t send = a.seg0 + a.n_segs;
+  for (uint64_t sg = a.seg0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; sg < send; sg += stride) {
     r = find_run(a.run_sstart, a.n_runs, sg, r);
     const gg_run run = a.runs[r];
     const uint32_t k0 = (uint32_t)(sg - a.run_sstart[r]) * (uint32_t)kSeg;  // first k-mer of the segment in the run

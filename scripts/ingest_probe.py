@@ -1,13 +1,19 @@
 """Ingest probe: write synthetic FASTA files (plain and
 gzip) to a scratch directory, then time gg_pack_files (host: read, gunzip,
-parse, 2-bit pack) and the whole gg_precluster_files path on them.
+parse, 2-bit pack) and the whole gg_precluster_files path on them (streamed:
+bounded batches of packed files overlap decode with H2D and K1).  Each
+gg_precluster_files run happens in a fresh process so its peak RSS can be
+read; --repeat lists path-list multiplicities (the same files listed R
+times: galah sketches duplicate paths twice) to show that peak RSS does not
+grow with the number of genomes.
 
-    python scripts/ingest_probe.py [--files 256] [--len 3000000] [--threads 16]
+    python scripts/ingest_probe.py [--files 256] [--len 3000000] [--threads 16] [--repeat 1,4]
 """
 import argparse
 import gzip
 import json
 import os
+import subprocess
 import sys
 import tempfile
 import time
@@ -24,7 +30,11 @@ def main():
     ap.add_argument("--len", type=int, default=3000000)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--repeat", default="1,4")
+    ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
     a = ap.parse_args()
+    if a.child:
+        return child(a)
     d = a.dir or tempfile.mkdtemp(prefix="gg_ingest_")
     os.makedirs(d, exist_ok=True)
     rng = np.random.default_rng(5)
@@ -58,13 +68,40 @@ def main():
         out["pack_%s_s" % kind] = round(t, 3)
         out["pack_%s_gbases_per_s" % kind] = round(bases / t / 1e9, 3)
         pk.free()
-    with ga.Context(k=21, sketch_size=1000) as ctx:
-        ctx.precluster_files(paths["gz"][:8], ga.parse_percentage(95))  # warm
-        t0 = time.perf_counter()
-        pairs, ani = ctx.precluster_files(paths["gz"], ga.parse_percentage(95))
-        out["precluster_files_gz_s"] = round(time.perf_counter() - t0, 3)
-        out["pairs_found"] = int(len(pairs))
+    listing = os.path.join(d, "gz_paths.txt")
+    with open(listing, "w") as f:
+        f.write("\n".join(paths["gz"]))
+    runs = []
+    for rep in [int(x) for x in a.repeat.split(",")]:
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", listing, "--repeat", str(rep),
+                            "--threads", str(a.threads)], capture_output=True, text=True, timeout=900)
+        if r.returncode != 0:
+            raise SystemExit(r.stderr)
+        runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    out["precluster_files_gz"] = runs
+    out["precluster_files_gz_s"] = runs[0]["s"]
+    out["pairs_found"] = runs[0]["pairs"]
+    out["precluster_over_pack_gz"] = round(runs[0]["s"] / out["pack_gz_s"], 3)
     print(json.dumps(out), flush=True)
+
+
+def child(a):
+    """One gg_precluster_files call over the listed paths x repeat (after a
+    small warm-up call), in its own process: time and peak RSS."""
+    import resource
+    with open(a.child) as f:
+        paths = [x for x in f.read().split("\n") if x] * int(a.repeat)
+    rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    with ga.Context(k=21, sketch_size=1000, host_threads=a.threads) as ctx:
+        ctx.precluster_files(paths[:8], ga.parse_percentage(95))  # device and library warm-up
+        rss1 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+        t0 = time.perf_counter()
+        pairs, ani = ctx.precluster_files(paths, ga.parse_percentage(95))
+        t = time.perf_counter() - t0
+    rss2 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    print(json.dumps({"genomes": len(paths), "repeat": int(a.repeat), "s": round(t, 3), "pairs": int(len(pairs)),
+                      "peak_rss_mib_before": round(rss1 / 1024, 1), "peak_rss_mib": round(rss2 / 1024, 1),
+                      "rss_mib_at_start": round(rss0 / 1024, 1)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -442,3 +442,52 @@ def test_index_kernel_many_partners_and_long_runs(monkeypatch):
     monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
     with ga.Context(k=21, sketch_size=s) as ctx:
         assert as_tuples(ctx.pairs(sk, lens, np.float32(0.01))) == exp
+
+
+def test_many_runs_index_and_run_table_errors(gpu_ctx):
+    """> 2^18 runs (the host run index runs in parallel chunks), ragged run
+    lengths around one K1 segment (44 k-mers), genomes without runs between
+    others, and every run-table error, through gg_sketch_device."""
+    torch = torch_dev()
+    rng = np.random.default_rng(77)
+    n_words = 1 << 21
+    words = rng.integers(0, 2**32, n_words, dtype=np.uint64).astype(np.uint32)
+    d_words = torch.from_numpy(words.view(np.int32)).cuda()
+    n_runs, n_genomes = 300000, 64
+    lens = rng.integers(21, 160, n_runs).astype(np.uint32)
+    lens[::7] = rng.integers(21, 66, len(lens[::7]))   # around one segment (k-mers 1..45)
+    gaps = rng.integers(1, 40, n_runs).astype(np.uint64)
+    base = np.cumsum(lens.astype(np.uint64) + gaps) - lens.astype(np.uint64)
+    assert base[-1] + lens[-1] <= n_words * 16
+    # genomes 5, 6 and 40 get no runs
+    owners = np.array([g for g in range(n_genomes) if g not in (5, 6, 40)], np.uint32)
+    genome = owners[np.sort(rng.integers(0, len(owners), n_runs))]
+    runs = np.zeros(n_runs, ga.RUN_DTYPE)
+    runs["genome"], runs["len"], runs["base"] = genome, lens, base
+    d_out = torch.zeros((n_genomes, 1000), dtype=torch.int64, device="cuda")
+    d_lens = torch.zeros(n_genomes, dtype=torch.int32, device="cuda")
+    gpu_ctx.sketch_device(d_words, runs, n_genomes, d_out, d_lens)
+    torch.cuda.synchronize()
+    sk = d_out.cpu().numpy().view(np.uint64)
+    gl = d_lens.cpu().numpy().view(np.uint32)
+    for g in list(range(0, n_genomes, 9)) + [5, 6, 40, n_genomes - 1]:
+        sel = runs[runs["genome"] == g]
+        recs = [unpack_run(words, int(r["base"]), int(r["len"])) for r in sel]
+        exp = oracle.sketch_records(recs) if recs else np.zeros(0, np.uint64)
+        assert gl[g] == len(exp) and (sk[g][:gl[g]] == exp).all(), g
+    bad = []
+    r1 = runs.copy()
+    r1["genome"][1000], r1["genome"][1001] = r1["genome"][1001] + 1, r1["genome"][1000]
+    bad.append((r1, "non-decreasing genome"))
+    r2 = runs.copy()
+    r2["len"][250000] = 20
+    bad.append((r2, "shorter than k"))
+    r3 = runs.copy()
+    r3["base"][-1] = n_words * 16 - 10
+    bad.append((r3, "past the packed words"))
+    r4 = runs.copy()
+    r4["genome"][-1] = n_genomes
+    bad.append((r4, "non-decreasing genome"))
+    for r, msg in bad:
+        with pytest.raises(ga.GalahGpuError, match=msg):
+            gpu_ctx.sketch_device(d_words, r, n_genomes, d_out, d_lens)
