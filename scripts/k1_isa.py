@@ -25,8 +25,9 @@ OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 K1_SYMBOL = "sketch_candidates_kernelILi21ELb1E"
 
 
-def kernel_listing(lib_path, symbol=K1_SYMBOL):
-    """[(mnemonic, operands)] of the kernel whose mangled name contains symbol."""
+def kernel_listing(lib_path, symbol=K1_SYMBOL, with_addr=False):
+    """[(mnemonic, operands)] of the kernel whose mangled name contains symbol
+    ([(address, mnemonic, operands, branch target or None)] with with_addr)."""
     tmp = tempfile.mkdtemp(prefix="k1isa")
     try:
         lib = os.path.join(tmp, "lib.so")
@@ -44,16 +45,54 @@ def kernel_listing(lib_path, symbol=K1_SYMBOL):
                     on = symbol in line
                     continue
                 if on and line.startswith("\t"):
-                    ins = line.split("//")[0].strip()
+                    code, _, comment = line.partition("//")
+                    ins = code.strip()
                     if not ins:
                         continue
                     parts = ins.split(None, 1)
-                    out.append((parts[0], parts[1] if len(parts) > 1 else ""))
+                    if with_addr:
+                        m = re.match(r"\s*([0-9A-Fa-f]+):", comment)
+                        t = re.search(r"<[^>]*\+0x([0-9a-f]+)>", comment)
+                        out.append((int(m.group(1), 16) if m else None, parts[0], parts[1] if len(parts) > 1 else "",
+                                    int(t.group(1), 16) if t else None))
+                    else:
+                        out.append((parts[0], parts[1] if len(parts) > 1 else ""))
             if out:
                 break
         return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def hot_path(listing_addr):
+    """The instructions one segment of the hashing loop executes when no
+    candidate branch is taken: from the first k-mer's table read to the last
+    k-mer's, skipping every forward s_cbranch_execz body inside that span (the
+    candidate test and queue push run for ~12% of 4-k-mer groups at C3, so
+    the static listing over-weights them).  [(mnemonic, operands)]"""
+    if not listing_addr:
+        return []
+    base = listing_addr[0][0]
+    reads = [i for i, x in enumerate(listing_addr) if x[1] == "ds_read_b128"]
+    if len(reads) < 2:
+        return [(x[1], x[2]) for x in listing_addr]
+    lo, hi = reads[0], reads[-1]
+    # the last k-mer's body: up to the next guarded branch after the last read
+    end = hi
+    while end < len(listing_addr) and listing_addr[end][1] != "s_cbranch_execz":
+        end += 1
+    out, i = [], lo
+    while i < end:
+        addr, mn, ops, tgt = listing_addr[i]
+        if mn == "s_cbranch_execz" and tgt is not None and tgt + base > addr:
+            j = i + 1
+            while j < len(listing_addr) and listing_addr[j][0] < tgt + base:
+                j += 1
+            i = j
+            continue
+        out.append((mn, ops))
+        i += 1
+    return out
 
 
 def fingerprint(listing):
@@ -93,7 +132,9 @@ if __name__ == "__main__":
                                                              "libgalahgpu.so")
     L = kernel_listing(lib)
     print(len(L), "instructions; fingerprint", fingerprint(L))
-    print(histogram(L))
+    print("static", histogram(L))
+    H = hot_path(kernel_listing(lib, with_addr=True))
+    print("hot path (%d instructions)" % len(H), histogram(H))
     from collections import Counter
     c = Counter((mn, classify(mn, ops)) for mn, ops in L if mn.startswith("v_"))
     for (mn, cl), k in c.most_common(40):

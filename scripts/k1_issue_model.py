@@ -8,7 +8,9 @@ Inputs (all measured on the MI355X, committed under profiles/):
     GRBM_GUI_ACTIVE / 8, 8 waves per SIMD, independent chains):
       dual ~2.3 (pairs co-issue), full ~4.2, wide (64-bit) ~5.0
   * K1's machine code in the library (scripts/k1_isa.py): the share of each
-    class among its VALU instructions.
+    class among the VALU instructions of its hot path (one segment of the
+    unrolled hashing loop with no candidate branch taken, k1_isa.hot_path;
+    the whole-kernel static shares are recorded beside it).
 
 floor (cycles per wave of 64 k-mers) = VALU per wave-k-mer (PMC) x
     sum_class share_class x cost_class
@@ -75,9 +77,12 @@ def main():
     c, dur = counters(pmc_dir, "sketch_candidates_kernel<21")
     costs = class_costs(os.path.join(ROOT, "profiles", "r02_pmc_ubench_dual.csv"))
     listing = k1_isa.kernel_listing(lib)
-    h = k1_isa.histogram(listing)
+    hs = k1_isa.histogram(listing)
+    h = k1_isa.histogram(k1_isa.hot_path(k1_isa.kernel_listing(lib, with_addr=True)))
     nv = h["dual"] + h["full"] + h["wide"]
     share = {k: h[k] / nv for k in ("dual", "full", "wide")}
+    nvs = hs["dual"] + hs["full"] + hs["wide"]
+    share_static = {k: hs[k] / nvs for k in ("dual", "full", "wide")}
     waves = C3_KMERS / 64.0
     valu = c["SQ_INSTS_VALU"] / waves
     per_instr = sum(share[k] * costs[k] for k in share)
@@ -86,13 +91,15 @@ def main():
     measured = cyc_simd * 1024 / waves
     peak = 1024 * 2.4e9 * 64 / floor / 1e9
     model = {
-        "note": ("floor = %.2f VALU per wave-k-mer (PMC, C3 launch) x %.3f cycles (static class shares dual %.3f / "
+        "note": ("floor = %.2f VALU per wave-k-mer (PMC, C3 launch) x %.3f cycles (hot-path class shares dual %.3f / "
                  "full %.3f / wide %.3f at %.2f / %.2f / %.2f cycles, ubench_dual PMC) = %.1f cycles; peak = 1024 "
                  "SIMDs x 2.4 GHz x 64 / floor" % (valu, per_instr, share["dual"], share["full"], share["wide"],
                                                    costs["dual"], costs["full"], costs["wide"], floor)),
         "k1_fingerprint": k1_isa.fingerprint(listing),
         "valu_per_wave_kmer": valu,
-        "class_share_static": share,
+        "class_share_hot_path": share,
+        "hot_path_valu_per_kmer": nv / 44.0,
+        "class_share_static": share_static,
         "class_cost_cycles": costs,
         "floor_cycles_per_wave_kmer": floor,
         "peak_gkmer_per_s": peak,
