@@ -596,6 +596,8 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   b.stride = c->s;
   b.kbits = kbits;
   b.max_run = kMaxRun;
+  GG_HIP(c, scratch_t(c, "idx_offs", std::max(n, 1u), &b.offs));
+  GG_HIP(c, scratch_t(c, "idx_info", 2, &b.info));
   GG_HIP(c, scratch_t(c, "idx_keys_in", total, &b.keys_in));
   GG_HIP(c, scratch_t(c, "idx_keys_out", total, &b.keys_out));
   GG_HIP(c, scratch_t(c, "idx_vals_in", total, &b.vals_in));
@@ -604,19 +606,20 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   b.sort_tmp_bytes = index_sort_tmp_bytes(total);
   GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
   GG_HIP(c, scratch_t(c, "idx_flags", 4, &b.flags));
-  uint32_t flags[4] = {0, 0, 0, 0};
+  uint64_t info[2] = {0, 0};
   GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_fill(b, st); }));
-  GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof flags, hipMemcpyDeviceToHost, st));
+  GG_HIP(c, hipMemcpyAsync(info, b.info, sizeof info, hipMemcpyDeviceToHost, st));
   GG_HIP(c, hipStreamSynchronize(st));
-  // sort on the bits below the largest hash + 1 (padding keys, 2^64 - 1,
-  // then still sort after every hash)
-  const uint64_t maxh = (uint64_t)flags[2] | ((uint64_t)flags[3] << 32);
-  uint32_t end_bit = 64;
-  if (maxh != ~0ull) {
-    end_bit = 1;
-    while (end_bit < 64 && ((maxh + 1) >> end_bit) != 0) ++end_bit;
-  }
-  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st, [&] { return index_build(b, end_bit, st); }));
+  // keys = the top 32 significant bits of each hash (the low 32 bits travel
+  // with the entry): shift by the bits of the largest hash beyond 32
+  const uint64_t n_entries = info[0], maxh = info[1];
+  uint32_t bits = 0;
+  while (bits < 64 && (maxh >> bits) != 0) ++bits;
+  const uint32_t sh = bits > 32 ? bits - 32 : 0;
+  const uint32_t end_bit = std::max(1u, bits - sh);
+  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
+                         [&] { return index_build(b, n_entries, sh, end_bit, st); }));
+  uint32_t flags[1] = {0};
   GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   GG_HIP(c, hipStreamSynchronize(st));
   if (flags[0]) return GG_OK;  // a run longer than kMaxRun

@@ -167,14 +167,16 @@ struct IndexBuild {
   uint32_t stride;
   uint32_t kbits;      // bits of a position k < stride in a packed value
   uint32_t max_run;    // longer runs: overflow (gate kernel instead)
-  uint64_t* keys_in;   // [n * stride]
-  uint64_t* keys_out;
-  uint32_t* vals_in;
-  uint32_t* vals_out;
+  uint64_t* offs;      // [n] first entry of each row
+  uint64_t* info;      // [2] entries, largest hash
+  uint32_t* keys_in;   // [n * stride]
+  uint32_t* keys_out;
+  uint64_t* vals_in;
+  uint64_t* vals_out;
   uint64_t* runinfo;   // [n * stride]
   void* sort_tmp;
   size_t sort_tmp_bytes;
-  uint32_t* flags;     // [4]: overflow, pad, largest hash (u64)
+  uint32_t* flags;     // [4]: overflow
 };
 struct IndexLaunch {
   const uint64_t* sketches;
@@ -187,7 +189,7 @@ struct IndexLaunch {
   uint64_t tile_begin;
   uint64_t tile_end;
   const uint64_t* runinfo;
-  const uint32_t* vals;  // sorted values (row << kbits | k)
+  const uint64_t* vals;  // hash order; low 32 bits: the entry (row << kbits | k)
   const uint32_t* cmin;
   const uint32_t* sufmin;
   uint32_t tmax;
@@ -195,10 +197,11 @@ struct IndexLaunch {
   uint64_t out_cap;
   unsigned long long* count;
 };
-// keys/vals of every entry and the largest hash (flags[2..3]); then, with
-// the sort's bit range, the sort and the run pass (overflow: flags[0]).
+// Row offsets, the entry count and the largest hash (info[0], info[1]);
+// then, with the key shift and the sort's bit range, the keys, the sort and
+// the run pass (overflow: flags[0]).
 hipError_t index_fill(const IndexBuild& b, hipStream_t st);
-hipError_t index_build(const IndexBuild& b, uint32_t end_bit, hipStream_t st);
+hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_t end_bit, hipStream_t st);
 size_t index_sort_tmp_bytes(uint64_t total);
 hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st);
 

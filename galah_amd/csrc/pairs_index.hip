@@ -5,10 +5,15 @@
 // iff common >= cmin[total]).  common(i, j) is the number of hash values
 // that occur in both sketches, and a hash occurs at most once per sketch, so
 //
-//   1. every sketch entry (hash, row, position) is radix-sorted by hash
-//      (hipCUB / rocPRIM onesweep, 64-bit keys): equal hashes form runs;
-//   2. each run of g >= 2 entries writes (run start, g) to every member's
-//      row-major slot (runinfo), g = 1 writes 0;
+//   1. every sketch entry (row i, position k < len_i) is radix-sorted
+//      (hipCUB / rocPRIM onesweep) by the top 32 significant bits of its
+//      hash, carrying the hash's low 32 bits with (i, k): 32-bit keys need at
+//      most 4 digit passes where the 64-bit hashes needed 7-8, and key and
+//      low word together still hold the whole hash;
+//   2. a run pass finds the runs of equal keys, splits the rare ones that
+//      hold more than one hash (equal top bits, different low words: sorted
+//      in place by the thread that owns the run), and writes (run start, g)
+//      to every member's row-major slot (runinfo; g = 1 writes 0);
 //   3. one workgroup per row i walks its own runinfo (coalesced), reads the
 //      members of its runs and counts every partner j > i in an LDS hash map
 //      -> common(i, j) exactly, for every pair that shares a hash;
@@ -36,6 +41,7 @@ constexpr int kRowThreads = 256;
 constexpr uint32_t kMapLog2 = 11;
 constexpr uint32_t kMap = 1u << kMapLog2;  // LDS partner map slots per row
 constexpr uint32_t kMapFull = kMap * 3 / 4;
+constexpr int kScanThreads = 1024;
 
 // #{ e < n : a[e] <= x }, a ascending
 __device__ __forceinline__ uint32_t count_le(const uint64_t* __restrict__ a, uint32_t n, uint64_t x) {
@@ -48,62 +54,118 @@ __device__ __forceinline__ uint32_t count_le(const uint64_t* __restrict__ a, uin
   return lo;
 }
 
-// keys[e] = hash of entry e = (row i, position k) of the [n x stride] array
-// (2^64 - 1 for padding k >= len_i), vals[e] = i << kbits | k.
+// One workgroup: offs[i] = sum of lens[0..i) (entries before row i), the
+// total -> info[0], the largest hash of any sketch (its last entry) ->
+// info[1].  n is at most a few 10^5 rows.
+__global__ __launch_bounds__(kScanThreads) void index_scan_kernel(const uint64_t* __restrict__ sk,
+                                                                  const uint32_t* __restrict__ lens, uint32_t n,
+                                                                  uint32_t stride, uint64_t* __restrict__ offs,
+                                                                  unsigned long long* __restrict__ info) {
+  __shared__ unsigned long long wsum[kScanThreads / 64], wmax[kScanThreads / 64];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (n + kScanThreads - 1) / kScanThreads;
+  const uint32_t b0 = min(tid * per, n), b1 = min(b0 + per, n);
+  unsigned long long sum = 0, mx = 0;
+  for (uint32_t i = b0; i < b1; ++i) {
+    const uint32_t l = lens[i];
+    sum += l;
+    if (l) mx = max(mx, (unsigned long long)sk[(uint64_t)i * stride + l - 1]);
+  }
+  unsigned long long inc = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(inc, o);
+    if ((tid & 63) >= (uint32_t)o) inc += y;
+  }
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned long long)__shfl_xor(mx, o));
+  if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+  if ((tid & 63) == 0) wmax[tid >> 6] = mx;
+  __syncthreads();
+  unsigned long long run = inc - sum;
+  for (uint32_t w = 0; w < (tid >> 6); ++w) run += wsum[w];
+  for (uint32_t i = b0; i < b1; ++i) {
+    offs[i] = run;
+    run += lens[i];
+  }
+  if (tid == kScanThreads - 1) {
+    info[0] = run;  // the last thread's running sum ends at the total
+    unsigned long long m = 0;
+    for (int w = 0; w < kScanThreads / 64; ++w) m = max(m, wmax[w]);
+    info[1] = m;
+  }
+}
+
+// keys[e] = hash >> sh (32 bits), vals[e] = lo32(hash) << 32 | i << kbits | k
+// for entry e = offs[i] + k of row i, k < len_i.
 __global__ __launch_bounds__(256) void index_fill_kernel(const uint64_t* __restrict__ sk,
-                                                         const uint32_t* __restrict__ lens, uint32_t n,
-                                                         uint32_t stride, uint32_t kbits, uint64_t* __restrict__ keys,
-                                                         uint32_t* __restrict__ vals) {
+                                                         const uint32_t* __restrict__ lens,
+                                                         const uint64_t* __restrict__ offs, uint32_t n,
+                                                         uint32_t stride, uint32_t kbits, uint32_t sh,
+                                                         uint32_t* __restrict__ keys, uint64_t* __restrict__ vals) {
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t len = lens[i];
     const uint64_t* row = sk + (uint64_t)i * stride;
-    for (uint32_t k = threadIdx.x; k < stride; k += 256) {
-      const uint64_t e = (uint64_t)i * stride + k;
-      keys[e] = k < len ? row[k] : ~0ull;
-      vals[e] = (i << kbits) | k;
+    const uint64_t o = offs[i];
+    for (uint32_t k = threadIdx.x; k < len; k += 256) {
+      const uint64_t h = row[k];
+      keys[o + k] = (uint32_t)(h >> sh);
+      vals[o + k] = (h << 32) | ((uint64_t)i << kbits) | k;
     }
   }
 }
 
-// Largest hash of any sketch (its last entry) -> *out (for the sort's bit
-// range: the radix sort skips the high bits that are zero in every key).
-__global__ __launch_bounds__(256) void index_max_kernel(const uint64_t* __restrict__ sk,
-                                                        const uint32_t* __restrict__ lens, uint32_t n, uint32_t stride,
-                                                        unsigned long long* __restrict__ out) {
-  unsigned long long m = 0;
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const uint32_t l = lens[i];
-    if (l) m = max(m, (unsigned long long)sk[(uint64_t)i * stride + l - 1]);
-  }
-  for (int o = 32; o > 0; o >>= 1) m = max(m, (unsigned long long)__shfl_xor(m, o));
-  if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
-}
-
-// Run starts write their run to every member's runinfo slot:
-// (start | g << 32) for g >= 2 (bit 63 set for the 2^64 - 1 run, whose
-// members may include padding), 0 for g = 1.  Runs longer than max_run set
-// *overflow (the host then uses the gate kernel).
-__global__ __launch_bounds__(256) void index_runs_kernel(const uint64_t* __restrict__ keys,
-                                                         const uint32_t* __restrict__ vals, uint64_t total,
+// Runs of equal keys: the thread at a run start owns it.  Every member of a
+// hash's run of g >= 2 gets runinfo = (start | g << 32) (runinfo is zeroed
+// beforehand, so g = 1 writes nothing).  A run whose members do not all
+// carry the same low hash word (two hashes with the same top bits: rare) is
+// then sorted in place by (low word, entry), split, and written again.  Runs
+// longer than max_run set *overflow (the host then uses the gate kernel).
+__global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restrict__ keys,
+                                                         uint64_t* __restrict__ vals, uint64_t total,
                                                          uint32_t stride, uint32_t kbits, uint32_t max_run,
-                                                         uint64_t* __restrict__ runinfo, uint32_t* __restrict__ overflow) {
+                                                         uint64_t* __restrict__ runinfo,
+                                                         uint32_t* __restrict__ overflow) {
   // (no device-wide event counter: one atomic per wave on one address
   // serialises at ~12 ns each, 1.9 ms at C3)
   const uint32_t kmask = (1u << kbits) - 1u;
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (uint64_t)gridDim.x * 256) {
-    const uint64_t key = keys[p];
+    const uint32_t key = keys[p];
     if (p > 0 && keys[p - 1] == key) continue;  // not a run start
     uint64_t e = p + 1;
     while (e < total && keys[e] == key && e - p <= max_run) ++e;
-    const uint64_t g = e - p;
-    if (g > max_run) {
+    if (e - p > max_run) {
       atomicOr(overflow, 1u);
       continue;
     }
-    const uint64_t info = g >= 2 ? (p | (g << 32) | (key == ~0ull ? (1ull << 63) : 0ull)) : 0ull;
+    if (e - p == 1) continue;
+    const uint32_t lo0 = (uint32_t)(vals[p] >> 32);
+    const uint64_t info = p | ((e - p) << 32);
+    bool mixed = false;
     for (uint64_t q = p; q < e; ++q) {
-      const uint32_t v = vals[q];
+      const uint64_t x = vals[q];
+      mixed |= (uint32_t)(x >> 32) != lo0;
+      const uint32_t v = (uint32_t)x;
       runinfo[(uint64_t)(v >> kbits) * stride + (v & kmask)] = info;
+    }
+    if (!mixed) continue;
+    for (uint64_t q = p + 1; q < e; ++q) {  // insertion sort by (low word, entry)
+      const uint64_t x = vals[q];
+      uint64_t w = q;
+      while (w > p && vals[w - 1] > x) {
+        vals[w] = vals[w - 1];
+        --w;
+      }
+      vals[w] = x;
+    }
+    for (uint64_t a = p; a < e;) {
+      const uint32_t lo = (uint32_t)(vals[a] >> 32);
+      uint64_t b = a + 1;
+      while (b < e && (uint32_t)(vals[b] >> 32) == lo) ++b;
+      const uint64_t sub = b - a >= 2 ? (a | ((b - a) << 32)) : 0ull;
+      for (uint64_t q = a; q < b; ++q) {
+        const uint32_t v = (uint32_t)vals[q];
+        runinfo[(uint64_t)(v >> kbits) * stride + (v & kmask)] = sub;
+      }
+      a = b;
     }
   }
 }
@@ -157,16 +219,14 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
     for (uint32_t k = tid; k < la; k += kRowThreads) {
       if (over) break;
       const uint64_t info = ri[k];
-      const uint32_t g = (uint32_t)(info >> 32) & 0x7FFFFFFFu;
+      const uint32_t g = (uint32_t)(info >> 32);
       if (g < 2) continue;
       const uint32_t st = (uint32_t)info;
-      const bool maxrun = (info >> 63) != 0;
       for (uint32_t q = st; q < st + g; ++q) {
-        const uint32_t v = a.vals[q];
+        const uint32_t v = (uint32_t)a.vals[q];
         const uint32_t j = v >> a.kbits;
         if (j < jlo || j >= jhi) continue;
         if (plog2 && part_of(j, plog2) != p) continue;
-        if (maxrun && (v & kmask) >= a.lens[j]) continue;  // padding, not the hash 2^64 - 1
         uint32_t h = (j * 0x85EBCA6Bu) >> (32 - kMapLog2);
         for (uint32_t probe = 0;; ++probe) {
           const uint32_t old = atomicCAS(&mkey[h], 0u, j + 1u);
@@ -215,22 +275,24 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
 }  // namespace
 
 hipError_t index_fill(const IndexBuild& b, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(b.flags, 0, 16, st);
+  hipError_t e = hipMemsetAsync(b.flags, 0, 4 * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(index_fill_kernel, dim3(std::min<uint32_t>(b.n, 16384)), dim3(256), 0, st, b.sketches, b.lens,
-                     b.n, b.stride, b.kbits, b.keys_in, b.vals_in);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(index_max_kernel, dim3(std::min<uint32_t>((b.n + 255) / 256, 1024)), dim3(256), 0, st,
-                     b.sketches, b.lens, b.n, b.stride, (unsigned long long*)(b.flags + 2));
+  hipLaunchKernelGGL(index_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, b.sketches, b.lens, b.n, b.stride,
+                     b.offs, (unsigned long long*)b.info);
   return hipGetLastError();
 }
 
-hipError_t index_build(const IndexBuild& b, uint32_t end_bit, hipStream_t st) {
-  const uint64_t total = (uint64_t)b.n * b.stride;
+hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_t end_bit, hipStream_t st) {
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(index_fill_kernel, dim3(std::min<uint32_t>(b.n, 16384)), dim3(256), 0, st, b.sketches, b.lens,
+                     b.offs, b.n, b.stride, b.kbits, sh, b.keys_in, b.vals_in);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   size_t bytes = b.sort_tmp_bytes;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out,
-                                                    (int)total, 0, (int)end_bit, st);
+  e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out,
+                                         (int)total, 0, (int)end_bit, st);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(b.runinfo, 0, (size_t)b.n * b.stride * sizeof(uint64_t), st);
   if (e != hipSuccess) return e;
   const uint64_t blocks = std::min<uint64_t>(65536, (total + 255) / 256);
   hipLaunchKernelGGL(index_runs_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, b.keys_out, b.vals_out, total,
@@ -240,8 +302,8 @@ hipError_t index_build(const IndexBuild& b, uint32_t end_bit, hipStream_t st) {
 
 size_t index_sort_tmp_bytes(uint64_t total) {
   size_t bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)total, 0, 64);
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)total, 0, 32);
   return bytes;
 }
 

@@ -491,3 +491,31 @@ def test_many_runs_index_and_run_table_errors(gpu_ctx):
     for r, msg in bad:
         with pytest.raises(ga.GalahGpuError, match=msg):
             gpu_ctx.sketch_device(d_words, r, n_genomes, d_out, d_lens)
+
+
+@pytest.mark.parametrize("top", [2**50, 2**64 - 1, 2**31])
+def test_index_kernel_shared_top_bits(monkeypatch, top):
+    """The index sorts by the top 32 significant bits of each hash and carries
+    the low word: hashes that differ only below those bits share a key and
+    must be split into their own runs (clusters of values within 2^12 of
+    each other, rows mixing them, the largest hash setting the key shift;
+    top = 2^31 leaves whole hashes as keys).  Equal to the oracle."""
+    rng = np.random.default_rng(31)
+    n, s = 400, 300
+    anchors = rng.integers(0, top // 2, 60, dtype=np.uint64)
+    pool = np.unique((anchors[:, None] + rng.integers(0, 4096, (60, 40)).astype(np.uint64)).reshape(-1))
+    sk = np.zeros((n, s), np.uint64)
+    lens = np.zeros(n, np.uint32)
+    for i in range(n):
+        take = pool[rng.random(len(pool)) < 0.12]
+        extra = rng.integers(0, top // 2, 30, dtype=np.uint64)
+        v = np.unique(np.concatenate([take, extra, [np.uint64(top)]] if i == 7 else [take, extra]))[:s]
+        sk[i, :len(v)] = v
+        lens[i] = len(v)
+    monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
+    for thr in (0.5, 0.9):
+        o = oracle.pairs(sk, lens.astype(np.int32), np.float32(thr))
+        exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+        with ga.Context(k=21, sketch_size=s) as ctx:
+            assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, thr
+        assert thr > 0.5 or len(exp) > 0
