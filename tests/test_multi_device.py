@@ -82,7 +82,12 @@ def test_precluster_shards_2k_synthetic_1_2_3_devices():
                 shards.append((d_words, runs, g1 - g0))
                 keep.append(d_words)
             pairs, ani = ctx.precluster_shards(shards, thr)
-            results.append((as_tuples(pairs), ani.tolist()))
+            # at 90% nearly every within-cluster pair passes (> 4096: the
+            # host merge's radix sort)
+            p90, a90 = ctx.precluster_shards(shards, ga.parse_percentage(90))
+            results.append((as_tuples(pairs), ani.tolist(), as_tuples(p90), a90.tolist()))
+            t90 = as_tuples(p90)
+            assert len(t90) > 4096 and t90 == sorted(t90) and all(i < j for i, j, _, _ in t90)
             if M == 1:
                 # the same genomes through the device-resident single-device path
                 d_words, runs, _ = shards[0]
@@ -106,6 +111,9 @@ def test_precluster_shards_2k_synthetic_1_2_3_devices():
                 exp = sorted((int(i), int(j), int(c), int(t)) for i, j, c, t, p in zip(ii, jj, oc, ot, opass) if p)
                 assert [x for x in ref if x[0] // cl == x[1] // cl] == exp
                 assert len(exp) > 100
+                opass90 = oracle.ani_array(oc, ot) >= np.float64(ga.parse_percentage(90))
+                exp90 = sorted((int(i), int(j), int(c), int(t)) for i, j, c, t, p in zip(ii, jj, oc, ot, opass90) if p)
+                assert [x for x in t90 if x[0] // cl == x[1] // cl] == exp90
     assert results[1] == results[0] and results[2] == results[0]
 
 
