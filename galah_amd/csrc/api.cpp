@@ -645,7 +645,7 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   a.tile_begin = tb;
   a.tile_end = te;
   a.runinfo = b.runinfo;
-  a.vals = b.vals_out;
+  a.vals = b.keys_in;  // the run pass leaves the run members' entries there
   a.cmin = d_cmin;
   a.sufmin = d_sufmin;
   a.tmax = 2 * c->s;

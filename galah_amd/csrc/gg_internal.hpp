@@ -189,7 +189,7 @@ struct IndexLaunch {
   uint64_t tile_begin;
   uint64_t tile_end;
   const uint64_t* runinfo;
-  const uint64_t* vals;  // hash order; low 32 bits: the entry (row << kbits | k)
+  const uint32_t* vals;  // entries (row << kbits | k) in hash order (those in runs of g >= 2)
   const uint32_t* cmin;
   const uint32_t* sufmin;
   uint32_t tmax;

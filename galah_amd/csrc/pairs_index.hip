@@ -115,36 +115,55 @@ __global__ __launch_bounds__(256) void index_fill_kernel(const uint64_t* __restr
 
 // Runs of equal keys: the thread at a run start owns it.  Every member of a
 // hash's run of g >= 2 gets runinfo = (start | g << 32) (runinfo is zeroed
-// beforehand, so g = 1 writes nothing).  A run whose members do not all
+// beforehand, so g = 1 writes nothing) and ents[q] = its entry (the pairs
+// kernel reads 4 bytes per run member instead of the 8 of vals).  A run whose members do not all
 // carry the same low hash word (two hashes with the same top bits: rare) is
 // then sorted in place by (low word, entry), split, and written again.  Runs
 // longer than max_run set *overflow (the host then uses the gate kernel).
 __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restrict__ keys,
                                                          uint64_t* __restrict__ vals, uint64_t total,
                                                          uint32_t stride, uint32_t kbits, uint32_t max_run,
-                                                         uint64_t* __restrict__ runinfo,
+                                                         uint64_t* __restrict__ runinfo, uint32_t* __restrict__ ents,
                                                          uint32_t* __restrict__ overflow) {
   // (no device-wide event counter: one atomic per wave on one address
   // serialises at ~12 ns each, 1.9 ms at C3)
   const uint32_t kmask = (1u << kbits) - 1u;
+  constexpr int W = 8;  // run members read in batches of W independent loads
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (uint64_t)gridDim.x * 256) {
     const uint32_t key = keys[p];
     if (p > 0 && keys[p - 1] == key) continue;  // not a run start
+    // run end: the next W - 1 keys at once (most runs are a cluster's few
+    // genomes), then one at a time
+    uint32_t kk[W - 1];
+#pragma unroll
+    for (int j = 1; j < W; ++j) kk[j - 1] = p + j < total ? keys[p + j] : ~key;
     uint64_t e = p + 1;
-    while (e < total && keys[e] == key && e - p <= max_run) ++e;
+#pragma unroll
+    for (int j = 1; j < W; ++j)
+      if (e == p + j && kk[j - 1] == key) e = p + j + 1;
+    if (e == p + W)
+      while (e < total && keys[e] == key && e - p <= max_run) ++e;
     if (e - p > max_run) {
       atomicOr(overflow, 1u);
       continue;
     }
-    if (e - p == 1) continue;
-    const uint32_t lo0 = (uint32_t)(vals[p] >> 32);
+    if (e - p == 1) continue;  // (no other row reads a singleton's entry)
     const uint64_t info = p | ((e - p) << 32);
+    uint32_t lo0 = 0;
     bool mixed = false;
-    for (uint64_t q = p; q < e; ++q) {
-      const uint64_t x = vals[q];
-      mixed |= (uint32_t)(x >> 32) != lo0;
-      const uint32_t v = (uint32_t)x;
-      runinfo[(uint64_t)(v >> kbits) * stride + (v & kmask)] = info;
+    for (uint64_t q0 = p; q0 < e; q0 += W) {
+      uint64_t x[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) x[j] = q0 + j < e ? vals[q0 + j] : 0ull;
+      if (q0 == p) lo0 = (uint32_t)(x[0] >> 32);
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        if (q0 + j >= e) break;
+        mixed |= (uint32_t)(x[j] >> 32) != lo0;
+        const uint32_t v = (uint32_t)x[j];
+        ents[q0 + j] = v;
+        runinfo[(uint64_t)(v >> kbits) * stride + (v & kmask)] = info;
+      }
     }
     if (!mixed) continue;
     for (uint64_t q = p + 1; q < e; ++q) {  // insertion sort by (low word, entry)
@@ -163,6 +182,7 @@ __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restr
       const uint64_t sub = b - a >= 2 ? (a | ((b - a) << 32)) : 0ull;
       for (uint64_t q = a; q < b; ++q) {
         const uint32_t v = (uint32_t)vals[q];
+        ents[q] = v;
         runinfo[(uint64_t)(v >> kbits) * stride + (v & kmask)] = sub;
       }
       a = b;
@@ -207,7 +227,6 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
   row_columns(i, a.n, a.nb, a.tile_begin, a.tile_end, jlo, jhi);
   const uint32_t la = a.lens[i];
   if (jlo >= jhi || la == 0) return;
-  const uint32_t kmask = (1u << a.kbits) - 1u;
   const uint64_t* ri = a.runinfo + (uint64_t)i * a.stride;
   const uint64_t* A = a.sketches + (uint64_t)i * a.stride;
   const uint64_t xa = A[la - 1];
@@ -223,7 +242,7 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
       if (g < 2) continue;
       const uint32_t st = (uint32_t)info;
       for (uint32_t q = st; q < st + g; ++q) {
-        const uint32_t v = (uint32_t)a.vals[q];
+        const uint32_t v = a.vals[q];
         const uint32_t j = v >> a.kbits;
         if (j < jlo || j >= jhi) continue;
         if (plog2 && part_of(j, plog2) != p) continue;
@@ -295,8 +314,9 @@ hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_
   e = hipMemsetAsync(b.runinfo, 0, (size_t)b.n * b.stride * sizeof(uint64_t), st);
   if (e != hipSuccess) return e;
   const uint64_t blocks = std::min<uint64_t>(65536, (total + 255) / 256);
+  // the entries of shared hashes land in keys_in (free after the sort)
   hipLaunchKernelGGL(index_runs_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, b.keys_out, b.vals_out, total,
-                     b.stride, b.kbits, b.max_run, b.runinfo, b.flags);
+                     b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in, b.flags);
   return hipGetLastError();
 }
 
