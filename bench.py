@@ -51,6 +51,9 @@ N_SIMD = 256 * 4       # 256 CUs x 4 SIMDs
 # records a fingerprint of K1's machine code; bench.py recomputes it from the
 # library it loads and flags the peak as stale when K1 has changed since.
 ISSUE_MODEL = os.path.join(ROOT, "profiles", "r02_k1_issue_model.json")
+# K2's per-kernel PMC summary (VALU issue share, LDS-array utilisation, fabric
+# GB/s against the gfx950 peaks): scripts/k2_pmc.sh + scripts/k2_pmc_model.py
+K2_PMC = os.path.join(ROOT, "profiles", "r02_k2_pmc.json")
 
 
 def parse():
@@ -122,7 +125,25 @@ def k1_fingerprint():
         return None
 
 
-def roofline(kst_sk, kst_pr, s, config_note):
+def k2_pmc(config):
+    """The K2 kernels' PMC summary for this config (one step of the same
+    workload, measured by scripts/k2_pmc.sh), or None."""
+    if not os.path.exists(K2_PMC):
+        return None
+    with open(K2_PMC) as f:
+        m = json.load(f)
+    c = m.get(config)
+    if not c:
+        return None
+    keep = ("ms", "bound", "bound_frac", "valu_frac_full", "lds_util", "lds_GBps", "hbm_read_GBps", "hbm_write_GBps",
+            "hbm_frac")
+    out = {k: {x: e[x] for x in keep if x in e} for k, e in c.items() if isinstance(e, dict) and k != "sketch_candidates"}
+    return {"source": "profiles/r02_k2_pmc.json (%s, one step)" % config, "kernels": out,
+            "peaks": "VALU: issue slots at 4.21 cycles per wave64 instruction per SIMD; LDS: array busy cycles per CU; "
+                     "HBM: 8 TB/s"}
+
+
+def roofline(kst_sk, kst_pr, s, config_note, config=None):
     model = None
     if os.path.exists(ISSUE_MODEL):
         with open(ISSUE_MODEL) as f:
@@ -157,6 +178,9 @@ def roofline(kst_sk, kst_pr, s, config_note):
           "note": "merge_priced_GBps = SURVEY 8(d)'s pricing (8 B x (|A|+|B|) per pair); neither K2 form merges: "
                   "the inverted index counts shared hashes from one sort of all sketch entries, the gate kernel "
                   "tests each column hash once against a row block's Bloom gate"}
+    pmc = k2_pmc(config) if config else None
+    if pmc:
+        k2["pmc"] = pmc
     dom = k1 if sk_ms * kst_sk["launches"] >= pr_ms * kst_pr["launches"] else k2
     roof = {"bound": dom.get("bound", "valu"), "achieved": round(dom["achieved"], 3),
             "peak": round(dom.get("peak", 0.0), 3), "unit": dom["unit"],
@@ -320,7 +344,7 @@ def run_lib(a, world, rank):
         ms_step = elapsed_max / a.steps * 1e3
         npairs = N * (N - 1) // 2
         note = ("per-launch figures are device 0's (%d of %d genomes)" % (shards[0][2], N)) if M > 1 else ""
-        roof = roofline(kst["sketch"], kst["pairs"], s, note)
+        roof = roofline(kst["sketch"], kst["pairs"], s, note, a.config if M == 1 and N == {"c3": 10000, "c5": 10000}.get(a.config) else None)
         downstream = None
         if M == 1 and found:
             t1 = time.perf_counter()
