@@ -150,6 +150,13 @@ SketchGeom sketch_geom(uint32_t s) {
   g.cap_log2 = 1;
   while ((1u << g.cap_log2) < 2 * g.sort_pow2) ++g.cap_log2;
   g.over = std::min(2.0, 0.8 * (double)g.limit / (double)s);
+  // GALAHGPU_TAU_OVER overrides the oversampling for A/B runs (any value
+  // gives the same sketches: too few candidates or an overflow only moves tau)
+  static const double over_env = [] {
+    const char* e = getenv("GALAHGPU_TAU_OVER");
+    return e && *e ? atof(e) : 0.0;
+  }();
+  if (over_env > 0.0) g.over = std::min(over_env, 0.95 * (double)g.limit / (double)s);
   return g;
 }
 

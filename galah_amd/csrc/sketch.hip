@@ -31,7 +31,10 @@
 namespace gg {
 namespace {
 
-constexpr int kGroup = 4;  // k-mers per tau-check branch (1 measured no faster, even at s = 10000)
+#ifndef GG_K1_GROUP
+#define GG_K1_GROUP 4
+#endif
+constexpr int kGroup = GG_K1_GROUP;  // k-mers per tau-check branch
 constexpr int kBlock = 256;
 // min waves per SIMD forced on the register allocator: 7 (72 VGPRs, 4 dwords
 // spilled at k = 21) beats the unconstrained 76 VGPRs / 6 waves with the
