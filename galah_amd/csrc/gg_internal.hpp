@@ -160,6 +160,33 @@ hipError_t launch_pairs_gate(const GateLaunch& a, hipStream_t st);
 
 // pairs_index.hip: the inverted-index pair kernel (default K2 when
 // eligible; see the file header).
+// parse.hip: one batch of raw FASTA text (files concatenated) -> 2-bit codes
+// and run starts; the host drives the passes and the per-block scans
+// (multi.cpp: parse_raw_batch).
+struct ParseLaunch {
+  const uint8_t* raw;
+  uint64_t n_bytes;
+  uint32_t n_blocks;
+  const uint32_t* blk_file;
+  const uint64_t* blk_start;
+  const uint64_t* blk_end;
+  const uint64_t* file_start;
+  uint64_t* blk_nl;      // pass 1 out
+  const uint64_t* pre_nl;
+  uint64_t* blk_bases;   // pass 2 out
+  uint64_t* blk_last;    // pass 2 out
+  const uint64_t* pre_last;
+  uint64_t* blk_runs;    // pass 3 out
+  const uint64_t* base_off;
+  const uint64_t* run_off;
+  uint8_t* codes;        // pass 4 out (packed positions)
+  uint64_t* starts;      // pass 4 out (run start positions)
+  uint64_t n_words;
+  uint32_t* words;       // pass 5 out
+};
+hipError_t parse_batch_pass(int pass, const ParseLaunch& p, hipStream_t st);
+uint32_t parse_block_bytes();
+
 struct IndexBuild {
   const uint64_t* sketches;
   const uint32_t* lens;
@@ -233,8 +260,11 @@ bool file_stamp(const char* path, FileStamp* out);
 int ingest_threads(int n_threads);
 class PackStream {
  public:
+  // raw: the workers only read (and gunzip) each file and keep its FASTA
+  // text for the device parser (parse.hip); FASTQ files are rewritten as
+  // FASTA records on the way.  Otherwise they pack on the host.
   PackStream(const char* const* paths, uint32_t n, int k, int n_threads, uint64_t budget_bytes,
-             bool stamp_files = false);
+             bool stamp_files = false, bool raw = false);
   ~PackStream();
   PackStream(const PackStream&) = delete;
   PackStream& operator=(const PackStream&) = delete;
@@ -242,6 +272,8 @@ class PackStream {
   // (base relative to word 0, genome field unused).  Valid until release(i).
   gg_status get(uint32_t i, const std::vector<uint32_t>** words, const std::vector<gg_run>** runs,
                 std::string* err);
+  // raw streams: genome i's FASTA text.  Valid until release(i).
+  gg_status get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err);
   // The file's size and mtime as stat'ed just before it was read (valid
   // after get(i) succeeded; the streams are built with stamp_files).
   FileStamp stamp(uint32_t i);

@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -221,6 +222,171 @@ gg_status pairs_with_ani(gg_ctx* c, const std::vector<gg_pair>& res, gg_pair** p
 // ---------------------------------------------------------------------------
 constexpr uint32_t kBatchGenomes = 32;          // genomes per K1 batch
 constexpr uint64_t kBatchWords = 64ull << 20;   // or 1 Gbases of packed words, whichever first
+constexpr uint64_t kBatchText = 1ull << 30;     // raw (device-parsed) batches: 1 GiB of FASTA text
+
+// memcpy on up to T threads (staging copies of a batch into pinned memory:
+// one thread moves ~10 GB/s, a batch of FASTA text is up to 1 GiB)
+void parallel_copy(void* dst, const void* src, size_t bytes, int T) {
+  constexpr size_t kPer = 8u << 20;
+  T = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, bytes / kPer));
+  if (T <= 1) {
+    if (bytes) memcpy(dst, src, bytes);
+    return;
+  }
+  std::vector<std::thread> th;
+  auto part = [&](int t) {
+    const size_t a = bytes * t / T, b = bytes * (t + 1) / T;
+    memcpy((uint8_t*)dst + a, (const uint8_t*)src + a, b - a);
+  };
+  for (int t = 1; t < T; ++t) th.emplace_back(part, t);
+  part(0);
+  for (auto& x : th) x.join();
+}
+
+// Where FASTA text becomes 2-bit runs: on the host threads (pack.cpp)
+// unless GALAHGPU_PARSE=device (parse.hip; the host threads then only read
+// and gunzip).  Measured on the MI355X box (profiles/r02_device_parse/, 128
+// x 3 Mbp gzip files): 16 threads 0.039 s host vs 0.087 s device, 1 thread
+// 0.494 vs 0.482 s -- the SSE packer runs ~2.5 Gbases/s per thread, gzip
+// decode dominates, and the device path moves 4x the bytes (text, not 2-bit
+// words) through host memory and PCIe, so the host packer stays the default.
+bool device_parse() {
+  const char* e = getenv("GALAHGPU_PARSE");
+  return e && strcmp(e, "device") == 0;
+}
+
+// One batch of FASTA text, already in device memory (d_text, files at
+// foff[0..nf]), parsed on the device: 2-bit words into *d_words (scratch of
+// m), runs of >= k bases (genome = file index in the batch, base = packed
+// position) into runs.  Synchronises m->stream.
+gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<uint64_t>& foff, uint32_t** d_words,
+                          uint64_t* n_words, std::vector<gg_run>& runs) {
+  hipStream_t st = m->stream;
+  const uint32_t nf = (uint32_t)foff.size() - 1;
+  const uint64_t bb = parse_block_bytes();
+  std::vector<uint32_t> bfile;
+  std::vector<uint64_t> bstart, bend;
+  for (uint32_t f = 0; f < nf; ++f)
+    for (uint64_t x = foff[f]; x < foff[f + 1]; x += bb) {
+      bfile.push_back(f);
+      bstart.push_back(x);
+      bend.push_back(std::min(foff[f + 1], x + bb));
+    }
+  const uint32_t nb = (uint32_t)bfile.size();
+  runs.clear();
+  ParseLaunch p{};
+  p.raw = d_text;
+  p.n_bytes = foff[nf];
+  p.n_blocks = nb;
+  uint64_t* blk;  // 9 arrays of nb u64: start, end, nl, pre_nl, bases, last, pre_last, runs, base_off; + run_off
+  GG_HIP(m, scratch_t(m, "parse_blk", (size_t)std::max(nb, 1u) * 10 + nf + 1, &blk));
+  uint32_t* d_bfile;
+  GG_HIP(m, scratch_t(m, "parse_bfile", std::max(nb, 1u), &d_bfile));
+  uint64_t* d_fstart = blk + (size_t)std::max(nb, 1u) * 10;
+  const size_t NB = std::max(nb, 1u);
+  p.blk_file = d_bfile;
+  p.blk_start = blk;
+  p.blk_end = blk + NB;
+  p.blk_nl = blk + 2 * NB;
+  p.pre_nl = blk + 3 * NB;
+  p.blk_bases = blk + 4 * NB;
+  p.blk_last = blk + 5 * NB;
+  p.pre_last = blk + 6 * NB;
+  p.blk_runs = blk + 7 * NB;
+  p.base_off = blk + 8 * NB;
+  p.run_off = blk + 9 * NB;
+  p.file_start = d_fstart;
+  std::vector<uint64_t> h(nb), h2(nb);
+  if (nb) {
+    GG_HIP(m, hipMemcpyAsync(d_bfile, bfile.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync((void*)p.blk_start, bstart.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync((void*)p.blk_end, bend.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  }
+  GG_HIP(m, hipMemcpyAsync(d_fstart, foff.data(), (nf + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  // pass 1 -> line-start prefix (last '\n' index + 1 before each block)
+  std::vector<uint64_t> fbases(nf, 0), gofs(nf + 1, 0);
+  uint64_t n_starts = 0;
+  if (nb) {
+    GG_HIP(m, parse_batch_pass(1, p, st));
+    GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_nl, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipStreamSynchronize(st));
+    uint64_t acc = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+      const uint64_t x = h[b];
+      h[b] = acc;
+      acc = std::max(acc, x);
+    }
+    GG_HIP(m, hipMemcpyAsync((void*)p.pre_nl, h.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    // pass 2 -> bases per block, last non-dropped byte before each block
+    GG_HIP(m, parse_batch_pass(2, p, st));
+    GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_bases, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipMemcpyAsync(h2.data(), p.blk_last, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipStreamSynchronize(st));
+    for (uint32_t b = 0; b < nb; ++b) fbases[bfile[b]] += h[b];
+    for (uint32_t f = 0; f < nf; ++f) gofs[f + 1] = gofs[f] + (fbases[f] + 15) / 16 * 16;  // genomes on words
+    {
+      std::vector<uint64_t> boff(nb);
+      uint64_t cur = 0;
+      uint32_t cf = ~0u;
+      for (uint32_t b = 0; b < nb; ++b) {
+        if (bfile[b] != cf) {
+          cf = bfile[b];
+          cur = gofs[cf];
+        }
+        boff[b] = cur;
+        cur += h[b];
+      }
+      GG_HIP(m, hipMemcpyAsync((void*)p.base_off, boff.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+      uint64_t last = 0;
+      for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t x = h2[b];
+        h2[b] = last;
+        if (x) last = x;
+      }
+      GG_HIP(m, hipMemcpyAsync((void*)p.pre_last, h2.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+      // pass 3 -> run starts per block
+      GG_HIP(m, parse_batch_pass(3, p, st));
+      GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_runs, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+      GG_HIP(m, hipStreamSynchronize(st));
+      for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t x = h[b];
+        h[b] = n_starts;
+        n_starts += x;
+      }
+      GG_HIP(m, hipMemcpyAsync((void*)p.run_off, h.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    }
+  }
+  const uint64_t total = gofs[nf];
+  *n_words = total / 16;
+  uint8_t* codes;
+  uint64_t* starts;
+  GG_HIP(m, scratch_t(m, "parse_codes", std::max<uint64_t>(total, 16), &codes));
+  GG_HIP(m, scratch_t(m, "parse_starts", std::max<uint64_t>(n_starts, 1), &starts));
+  GG_HIP(m, scratch_t(m, "stage_words", std::max<uint64_t>(*n_words, 1), d_words));
+  p.codes = codes;
+  p.starts = starts;
+  p.n_words = *n_words;
+  p.words = *d_words;
+  std::vector<uint64_t> hs(n_starts);
+  if (nb) {
+    GG_HIP(m, hipMemsetAsync(codes, 0, std::max<uint64_t>(total, 16), st));
+    GG_HIP(m, parse_batch_pass(4, p, st));
+    GG_HIP(m, parse_batch_pass(5, p, st));
+    if (n_starts) GG_HIP(m, hipMemcpyAsync(hs.data(), starts, n_starts * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipStreamSynchronize(st));
+  }
+  // runs: consecutive starts of one genome; a genome's last run ends at its
+  // last base; keep runs of >= k bases
+  uint32_t f = 0;
+  for (uint64_t r = 0; r < n_starts; ++r) {
+    const uint64_t a = hs[r];
+    while (f + 1 < nf && a >= gofs[f + 1]) ++f;
+    const uint64_t gend = gofs[f] + fbases[f];
+    const uint64_t e = (r + 1 < n_starts && hs[r + 1] < gend) ? hs[r + 1] : gend;
+    if (e - a >= (uint64_t)m->k) runs.push_back(gg_run{f, (uint32_t)(e - a), a});
+  }
+  return GG_OK;
+}
 
 // Sketches of paths[0..n) into every member's full array (rows[i]); spans
 // receives the rows each member sketched.  Genomes with a valid entry in
@@ -263,7 +429,10 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
   const uint32_t nm = (uint32_t)miss.size();
   // in-flight packed genomes: ~2 batches per member, at least 1 GiB
   const uint64_t budget = std::max<uint64_t>(1ull << 30, 2ull * M * kBatchWords * sizeof(uint32_t));
-  PackStream stream(miss.data(), nm, c->k, c->host_threads, budget, cache_dir != nullptr);
+  const bool raw = device_parse();
+  // staging copies per member: the host threads shared among the members
+  const int copy_threads = std::max(1, std::min(16, ingest_threads(c->host_threads)) / (int)M);
+  PackStream stream(miss.data(), nm, c->k, c->host_threads, budget, cache_dir != nullptr, raw);
   std::mutex cursor_mu;
   uint32_t cursor = 0;
   bool stop = false;        // a member failed: the others take no more batches
@@ -302,7 +471,48 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
       row_of.clear();
       uint64_t nw = 0;
       uint32_t g = 0;
-      for (uint32_t i = b0; i < b1; ++i, ++g) {
+      uint32_t* d_words = nullptr;
+      if (raw) {  // FASTA text -> device parser
+        std::vector<uint64_t> foff(1, 0);
+        for (uint32_t i = b0; i < b1; ++i) {
+          const std::vector<uint8_t>* tx;
+          std::string err;
+          const gg_status gs = stream.get_raw(i, &tx, &err);
+          if (gs != GG_OK) {
+            std::lock_guard<std::mutex> lk(cursor_mu);
+            if (!stop) file_error = true;
+            return fail(m, gs, err);
+          }
+          const uint64_t at = foff.back();
+          const uint64_t padded = (tx->size() + 15) / 16 * 16;  // next file on a 16-byte boundary
+          const size_t need = at + padded;
+          if (need > m->pinned_bytes) {  // grow, keeping what is staged
+            std::vector<uint8_t> keep((const uint8_t*)m->pinned, (const uint8_t*)m->pinned + at);
+            void* stage;
+            GG_HIP(m, pinned(m, std::max(need, std::min<size_t>(2 * need, kBatchText * 2)), &stage));
+            if (at) memcpy(stage, keep.data(), at);
+          }
+          parallel_copy((uint8_t*)m->pinned + at, tx->data(), tx->size(), copy_threads);
+          memset((uint8_t*)m->pinned + at + tx->size(), '\n', padded - tx->size());  // (parses as nothing)
+          foff.push_back(at + padded);
+          row_of.push_back(miss_at[i]);
+          stream.release(i);
+          if (foff.back() >= kBatchText && i + 1 < b1) {  // large genomes: cut the batch here
+            std::lock_guard<std::mutex> lk(cursor_mu);
+            if (cursor == b1) {
+              cursor = i + 1;
+              b1 = i + 1;
+            }
+          }
+        }
+        uint8_t* d_text;
+        GG_HIP(m, scratch_t(m, "stage_text", std::max<uint64_t>(foff.back(), 1), &d_text));
+        if (foff.back())
+          GG_HIP(m, hipMemcpyAsync(d_text, m->pinned, foff.back(), hipMemcpyHostToDevice, m->stream));
+        const gg_status ps = parse_raw_batch(m, d_text, foff, &d_words, &nw, runs);
+        if (ps != GG_OK) return ps;
+      }
+      for (uint32_t i = b0; !raw && i < b1; ++i, ++g) {
         const std::vector<uint32_t>* w;
         const std::vector<gg_run>* rr;
         std::string err;
@@ -334,11 +544,12 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
         }
       }
       const uint32_t ng = b1 - b0;
-      uint32_t* d_words;
       uint32_t* d_row_of;
-      GG_HIP(m, scratch_t(m, "stage_words", std::max<uint64_t>(nw, 1), &d_words));
+      if (!raw) {
+        GG_HIP(m, scratch_t(m, "stage_words", std::max<uint64_t>(nw, 1), &d_words));
+        if (nw) GG_HIP(m, hipMemcpyAsync(d_words, m->pinned, nw * sizeof(uint32_t), hipMemcpyHostToDevice, m->stream));
+      }
       GG_HIP(m, scratch_t(m, "row_of", ng, &d_row_of));
-      if (nw) GG_HIP(m, hipMemcpyAsync(d_words, m->pinned, nw * sizeof(uint32_t), hipMemcpyHostToDevice, m->stream));
       GG_HIP(m, hipMemcpyAsync(d_row_of, row_of.data(), ng * sizeof(uint32_t), hipMemcpyHostToDevice, m->stream));
       gg_status ks = sketch_core(m, d_words, nw, runs.data(), runs.size(), ng, r.sk, r.len, d_row_of, m->stream);
       if (ks != GG_OK) return ks;

@@ -75,6 +75,7 @@ __attribute__((target("sse4.1"))) inline bool pack16(const uint8_t* p, uint32_t*
 // Packs the runs of ONE genome; bases start at word 0 of its own buffer.
 struct GenomePacker {
   int k;
+  std::vector<uint8_t> text;  // raw streams: the FASTA text (parse.hip)
   std::vector<uint32_t> words;
   std::vector<gg_run> runs;  // base relative to this genome's first word
   uint64_t n_bases = 0;
@@ -335,6 +336,57 @@ gg_status pack_buffer(const uint8_t* d, size_t n, const char* name,
   return GG_OK;
 }
 
+// Raw streams: the text the device parser reads.  A file that starts with
+// '>' is FASTA to its end (pack_buffer splits records only at lines that
+// start with '>'), so it goes as is; one that starts with '@' is walked as
+// pack_buffer walks it and every record becomes ">\n" + its sequence bytes.
+gg_status raw_text(std::vector<uint8_t>& buf, const char* name, std::vector<uint8_t>& text, std::string& err) {
+  const size_t n = buf.size();
+  const uint8_t* d = buf.data();
+  if (n == 0 || (d[0] != '>' && d[0] != '@')) {
+    err = std::string("not a FASTA/FASTQ file: ") + name;
+    return GG_ERR_FORMAT;
+  }
+  if (d[0] == '>') {
+    text.swap(buf);
+    return GG_OK;
+  }
+  text.clear();
+  text.reserve(n / 2 + 16);
+  size_t i = 0;
+  while (i < n) {
+    const uint8_t tag = d[i];
+    if (tag != '>' && tag != '@') {
+      err = std::string("malformed record in ") + name;
+      return GG_ERR_FORMAT;
+    }
+    const uint8_t* nl = (const uint8_t*)memchr(d + i, '\n', n - i);
+    i = nl ? (size_t)(nl - d) + 1 : n;
+    size_t start = i, end;
+    if (tag == '>') {
+      while (i < n) {
+        if (d[i] == '>') break;
+        const uint8_t* e = (const uint8_t*)memchr(d + i, '\n', n - i);
+        i = e ? (size_t)(e - d) + 1 : n;
+      }
+      end = i;
+    } else {
+      const uint8_t* e = (const uint8_t*)memchr(d + i, '\n', n - i);
+      end = e ? (size_t)(e - d) : n;
+      i = e ? end + 1 : n;
+      for (int skip = 0; skip < 2 && i < n; ++skip) {
+        const uint8_t* q = (const uint8_t*)memchr(d + i, '\n', n - i);
+        i = q ? (size_t)(q - d) + 1 : n;
+      }
+    }
+    text.push_back('>');
+    text.push_back('\n');
+    text.insert(text.end(), d + start, d + end);
+    text.push_back('\n');
+  }
+  return GG_OK;
+}
+
 gg_packed* assemble(std::vector<std::unique_ptr<GenomePacker>>& gps) {
   const uint32_t ng = (uint32_t)gps.size();
   uint64_t n_words = 0, n_runs = 0;
@@ -400,6 +452,7 @@ struct PackStream::Impl {
   int k;
   uint64_t budget;
   bool stamping = false;
+  bool raw = false;
   std::vector<FileStamp> stamps;
   std::mutex mu;
   std::condition_variable cv_done;   // a genome finished packing
@@ -436,6 +489,8 @@ struct PackStream::Impl {
         e = "null path";
       } else if (!read_file(paths[i], buf, e)) {
         s = GG_ERR_IO;
+      } else if (raw) {
+        s = raw_text(buf, paths[i], gp->text, e);
       } else {
         s = pack_buffer(buf.data(), buf.size(), paths[i], *gp, e);
         gp->finish();
@@ -443,7 +498,7 @@ struct PackStream::Impl {
       if (buf.capacity() > (256u << 20)) std::vector<uint8_t>().swap(buf);  // do not pin a huge buffer
       {
         std::lock_guard<std::mutex> lk(mu);
-        inflight += gp->words.size() * sizeof(uint32_t) + gp->runs.size() * sizeof(gg_run);
+        inflight += gp->words.size() * sizeof(uint32_t) + gp->runs.size() * sizeof(gg_run) + gp->text.size();
         g[i] = std::move(gp);
         st[i] = s;
         err[i] = std::move(e);
@@ -455,10 +510,11 @@ struct PackStream::Impl {
 };
 
 PackStream::PackStream(const char* const* paths, uint32_t n, int k, int n_threads, uint64_t budget_bytes,
-                       bool stamp_files)
+                       bool stamp_files, bool raw)
     : p_(new Impl()) {
   Impl& m = *p_;
   m.stamping = stamp_files;
+  m.raw = raw;
   m.stamps.resize(stamp_files ? n : 0);
   m.paths = paths;
   m.n = n;
@@ -505,6 +561,22 @@ gg_status PackStream::get(uint32_t i, const std::vector<uint32_t>** words, const
   return GG_OK;
 }
 
+gg_status PackStream::get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err) {
+  Impl& m = *p_;
+  std::unique_lock<std::mutex> lk(m.mu);
+  m.cv_done.wait(lk, [&] { return m.state[i] >= 2 || (m.stop && m.state[i] == 0); });
+  if (m.state[i] < 2) {
+    if (err) *err = "ingest aborted";
+    return GG_ERR_INTERNAL;
+  }
+  if (m.st[i] != GG_OK) {
+    if (err) *err = m.err[i];
+    return m.st[i];
+  }
+  *text = &m.g[i]->text;
+  return GG_OK;
+}
+
 FileStamp PackStream::stamp(uint32_t i) {
   std::lock_guard<std::mutex> lk(p_->mu);
   return p_->stamping ? p_->stamps[i] : FileStamp{};
@@ -515,7 +587,7 @@ void PackStream::release(uint32_t i) {
   {
     std::lock_guard<std::mutex> lk(m.mu);
     if (m.state[i] != 2) return;
-    m.inflight -= m.g[i]->words.size() * sizeof(uint32_t) + m.g[i]->runs.size() * sizeof(gg_run);
+    m.inflight -= m.g[i]->words.size() * sizeof(uint32_t) + m.g[i]->runs.size() * sizeof(gg_run) + m.g[i]->text.size();
     m.g[i].reset();
     m.state[i] = 3;
     while (m.frontier < m.n && m.state[m.frontier] == 3) ++m.frontier;
