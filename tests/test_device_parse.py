@@ -127,3 +127,26 @@ def test_precluster_files_device_parse(golden, monkeypatch):
     with ga.Context(k=21, sketch_size=1000) as ctx:
         pairs, ani = ctx.precluster_files(golden["paths"], ga.parse_percentage(90))
     assert len(pairs) == 161
+
+
+def test_device_parse_three_members(tmp_path, monkeypatch):
+    """The device parser inside a 3-member context (batches dealt to the
+    members, each parsing on its own stream): same sketches as one member."""
+    rng = np.random.default_rng(47)
+    acgt = np.frombuffer(b"ACGTN", np.uint8)
+    files = []
+    for i in range(40):
+        seq = acgt[rng.integers(0, 4010, int(rng.integers(1000, 60000))) // 1000].tobytes()
+        p = tmp_path / ("m%02d.fa" % i)
+        p.write_bytes(b">m\n" + wrap(seq, 80))
+        files.append(str(p))
+    monkeypatch.setenv("GALAHGPU_PARSE", "device")
+    with ga.Context(k=21, sketch_size=500) as ctx:
+        sk1, l1, _ = ctx.sketch_files(files)
+    with ga.Context(k=21, sketch_size=500, devices=[0, 0, 0]) as ctx:
+        sk3, l3, _ = ctx.sketch_files(files)
+    assert (l1 == l3).all() and (sk1 == sk3).all()
+    monkeypatch.setenv("GALAHGPU_PARSE", "host")
+    with ga.Context(k=21, sketch_size=500) as ctx:
+        skh, lh, _ = ctx.sketch_files(files)
+    assert (lh == l1).all() and (skh == sk1).all()
