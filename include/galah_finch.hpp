@@ -70,13 +70,19 @@ inline float parse_percentage(float value) {
 }
 
 // src/finch.rs:26-75 on the GPU: sketch (K1), all pairs (K2), keep ani >= min_ani.
+// devices: HIP ordinals (empty: every visible GPU, or GALAHGPU_DEVICES, as
+// galah's one distances() call would use them); threads: galah's --threads
+// for file ingest (<= 0: the process's CPUs).
 inline SortedPairGenomeDistanceCache finch_distances(const std::vector<std::string>& paths,
                                                      float min_ani, size_t num_kmers,
-                                                     uint8_t kmer_length, int device = -1) {
+                                                     uint8_t kmer_length, const std::vector<int>& devices = {},
+                                                     int threads = 0) {
   gg_status st = GG_OK;
-  gg_ctx* ctx = gg_create(kmer_length, (uint32_t)num_kmers, 0, device, &st);
+  gg_ctx* ctx = gg_create_multi(kmer_length, (uint32_t)num_kmers, 0, devices.empty() ? nullptr : devices.data(),
+                                (uint32_t)devices.size(), &st);
   if (!ctx)
     throw std::runtime_error(std::string("Failed to sketch genomes with finch: ") + gg_thread_last_error());
+  if (threads > 0) gg_set_host_threads(ctx, threads);
   std::vector<const char*> c_paths;
   for (const auto& p : paths) c_paths.push_back(p.c_str());
   gg_pair* pairs = nullptr;
