@@ -357,7 +357,7 @@ def run_lib(a, world, rank):
                           round(t_tr * 1e3, 3), "preclusters": int(len(offsets) - 1),
                           "largest": int(np.diff(offsets).max()) if N else 0}
         cpu = None
-        if world == 1 and M == 1 and not a.no_cpu_baseline and a.config in ("c2", "c3"):
+        if world == 1 and M == 1 and not a.no_cpu_baseline and a.config in ("c2", "c3", "c4"):
             d_words, runs, _ = shards[0]
             d_sk = torch.zeros((N, s), dtype=torch.int64, device="cuda:%d" % devs[0])
             d_len = torch.zeros(N, dtype=torch.int32, device="cuda:%d" % devs[0])
