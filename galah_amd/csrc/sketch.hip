@@ -42,6 +42,28 @@ constexpr int kBlock = 256;
 #ifndef GG_K1_MIN_WAVES
 #define GG_K1_MIN_WAVES 7
 #endif
+// canonical code: high word as v_min_u32 of the two high words (1) instead of
+// a second v_cndmask on the 64-bit compare (0)
+#ifndef GG_K1_MINHI
+#define GG_K1_MINHI 0
+#endif
+// tau prefilter: high words of the last fmix64 multiplies as v_mul_hi_u32 +
+// two v_mul_lo_u32 (1; the full products only in the candidate branch) or as
+// the full 64-bit products (0)
+#ifndef GG_K1_MULHI
+#define GG_K1_MULHI 1
+#endif
+// k2 group-4b+2 entry read as one ds_read_b128 (1; its unused 4th dword kept
+// live by an empty asm) instead of the ds_read_b64 + ds_read_b32 the
+// compiler splits it into (0)
+#ifndef GG_K1_K2A128
+#define GG_K1_K2A128 1
+#endif
+// candidate branch: the exact hash of each k-mer of the group under its own
+// high-word test (1) or of all of them once the group's test passes (0)
+#ifndef GG_K1_INNER
+#define GG_K1_INNER 1
+#endif
 // candidates through the per-wave LDS queue (1) or inserted where they arise (0)
 #ifndef GG_K1_QUEUE
 #define GG_K1_QUEUE 1
@@ -84,6 +106,20 @@ __device__ __forceinline__ uint64_t fmix64_pre(uint64_t k) {
   return k;
 }
 __device__ __forceinline__ uint64_t fmix_last(uint64_t k) { return k ^ (k >> 33); }
+
+// fmix64 up to its second multiply: fmix64_pre(k) = fmix64_mid(k) * kFmixC2
+constexpr uint64_t kFmixC2 = 0xc4ceb9fe1a85ec53ull;
+__device__ __forceinline__ uint64_t fmix64_mid(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  return k ^ (k >> 33);
+}
+// high word of y * kFmixC2 (mod 2^64) without the low word: one v_mul_hi_u32
+// and two v_mul_lo_u32 instead of a v_mad_u64_u32 and two v_mul_lo_u32
+__device__ __forceinline__ uint32_t hi_times_c2(uint64_t y) {
+  const uint32_t lo = (uint32_t)y, hi = (uint32_t)(y >> 32);
+  return __umulhi(lo, (uint32_t)kFmixC2) + lo * (uint32_t)(kFmixC2 >> 32) + hi * (uint32_t)kFmixC2;
+}
 
 // h * 5 + c with one v_lshl_add_u64 (hipcc otherwise lowers the multiply by
 // 5 to v_mad_u64_u32 sequences).
@@ -160,7 +196,12 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
     const uint64_t* bt = tab + b * S::BLK_U64;
     const ulonglong2 e0 = *(const ulonglong2*)(bt + S::K1A + 2 * group_byte(hi, lo, 4 * b));
     const uint2 e1 = *(const uint2*)(bt + S::K1B + group_byte(hi, lo, 4 * b + 1));
+#if GG_K1_K2A128
+    const ulonglong2 e2q = *(const ulonglong2*)(bt + S::K2A + 2 * group_byte(hi, lo, 4 * b + 2));
+    const uint4 e2 = make_uint4((uint32_t)e2q.x, (uint32_t)(e2q.x >> 32), (uint32_t)e2q.y, (uint32_t)(e2q.y >> 32));
+#else
     const uint4 e2 = *(const uint4*)(bt + S::K2A + 2 * group_byte(hi, lo, 4 * b + 2));
+#endif
     const uint32_t t3 = ((const uint32_t*)(bt + S::K2B))[group_byte(hi, lo, 4 * b + 3)];
     // rotl(k1 * c1, 31) * c2
     const uint32_t v = ((uint32_t)e0.y + e1.y) >> 1;
@@ -171,6 +212,9 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
     // 2 hi(x) + bit 31 of lo(x) = 2 hi(x) + bit 31 of lo(T2), so
     // rotl(x, 33) * c1 = [T2 * (c1 << 33) + (lo(T2) >> 31) * c1] + hi(x) * 2 c1,
     // the bracket a table entry P of group 4b+2, hi(x) = hi(T2) + hi(T3)
+#if GG_K1_K2A128
+    asm volatile("" ::"v"(e2.w));
+#endif
     const uint32_t hx = e2.z + t3;
     uint64_t k2 = (uint64_t)hx * (uint32_t)(c1 << 1) + (((uint64_t)e2.y << 32) | e2.x);
     k2 += (uint64_t)(hx * (uint32_t)((c1 << 1) >> 32)) << 32;
@@ -200,8 +244,13 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
   h2 ^= (uint64_t)K;
   h1 += h2;
   h2 += h1;
+#if GG_K1_MULHI
+  f1 = fmix64_mid(h1);  // the caller finishes with kFmixC2 (hi_times_c2 / full)
+  f2 = fmix64_mid(h2);
+#else
   f1 = fmix64_pre(h1);
   f2 = fmix64_pre(h2);
+#endif
 }
 
 // ASCII bytes of `nbases` bases of an MSB-first code of `width` bases
@@ -456,12 +505,29 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
         const uint64_t fwd = window64<K>(F, FP, i);
         const int t0 = 64 - K - i;  // reverse complement of k-mer i starts here
         const uint64_t rev = window64<K>(R, RP, t0);
+#if GG_K1_MINHI
+        // min(fwd, rev): its high word is the smaller high word whatever the
+        // low words are; only the low word needs the 64-bit compare
+        uint32_t chi;
+        asm("v_min_u32 %0, %1, %2" : "=v"(chi) : "v"((uint32_t)(fwd >> 32)), "v"((uint32_t)(rev >> 32)));
+        const uint32_t clo = fwd < rev ? (uint32_t)fwd : (uint32_t)rev;
+        hash_parts<K>(((uint64_t)chi << 32) | clo, mtab, seed, f1[j], f2[j]);
+#else
         hash_parts<K>(fwd < rev ? fwd : rev, mtab, seed, f1[j], f2[j]);
+#endif
       }
+#if GG_K1_MULHI
+      uint32_t hs[kGroup];  // S + 1 per k-mer
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) hs[j] = hi_times_c2(f1[j]) + hi_times_c2(f2[j]) + 1u;
+#else
+      uint32_t hs[kGroup];
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) hs[j] = (uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u;
+#endif
       bool any = false;
 #pragma unroll
-      for (int j = 0; j < kGroup; ++j)
-        any |= (uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr;
+      for (int j = 0; j < kGroup; ++j) any |= hs[j] <= thr;
       if (any) {
 #if GG_K1_QUEUE
         // (a lane of the wave has a k-mer whose high-word sum can reach
@@ -469,17 +535,34 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
         // the candidates
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
+#if GG_K1_INNER
+          // one k-mer of the group passes in one lane, typically: the exact
+          // hash only under its own test (the wave skips the others)
+          if (hs[j] <= thr && (uint32_t)(g * kGroup + j) < cnt) {
+#if GG_K1_MULHI
+            const uint64_t hv = fmix_last(f1[j] * kFmixC2) + fmix_last(f2[j] * kFmixC2);
+#else
+            const uint64_t hv = fmix_last(f1[j]) + fmix_last(f2[j]);
+#endif
+            if (hv <= tau) queue_push(q, hv, slot, a.table, a.cap_log2, a.flags);
+          }
+#else
+#if GG_K1_MULHI
+          const uint64_t hv = fmix_last(f1[j] * kFmixC2) + fmix_last(f2[j] * kFmixC2);
+#else
           const uint64_t hv = fmix_last(f1[j]) + fmix_last(f2[j]);
-          if (((uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr) &&
+#endif
+          if (hs[j] <= thr &&
               (uint32_t)(g * kGroup + j) < cnt && hv <= tau)
             queue_push(q, hv, slot, a.table, a.cap_log2, a.flags);
+#endif
         }
 #else
         // finish the exact test per candidate k-mer and insert it now
         uint32_t pending = 0;
 #pragma unroll
         for (int j = 0; j < kGroup; ++j)
-          pending |= (((uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u <= thr) &
+          pending |= ((hs[j] <= thr) &
                       ((uint32_t)(g * kGroup + j) < cnt)) ? (1u << j) : 0u;
         while (pending) {
           const int j = __builtin_ctz(pending);
@@ -490,7 +573,11 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
             a1 = (j == x) ? f1[x] : a1;
             a2 = (j == x) ? f2[x] : a2;
           }
+#if GG_K1_MULHI
+          const uint64_t hv = fmix_last(a1 * kFmixC2) + fmix_last(a2 * kFmixC2);
+#else
           const uint64_t hv = fmix_last(a1) + fmix_last(a2);
+#endif
           if (hv <= tau)
             insert_candidate(a.table + ((uint64_t)slot << a.cap_log2), (1u << a.cap_log2) - 1u, a.flags + slot, hv);
         }

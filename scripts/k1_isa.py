@@ -100,7 +100,7 @@ def fingerprint(listing):
 
 
 DUAL_OPS = re.compile(r"^v_(add_u32|sub_u32|subrev_u32|xor_b32|and_b32|or_b32|lshrrev_b32|mov_b32|add_f32|"
-                      r"sub_f32|mul_f32|max_u32|min_u32|max_f32|min_f32)(_e32)?$")
+                      r"sub_f32|mul_f32|max_f32|min_f32)(_e32)?$")
 WIDE_OPS = re.compile(r"^v_(mad_u64_u32|mad_i64_i32|lshl_add_u64|lshlrev_b64|lshrrev_b64|ashrrev_i64|"
                       r"pk_\w+|cmp\w*_u64|cmp\w*_i64|cmpx\w*_u64)(_e32|_e64)?$")
 

@@ -85,13 +85,29 @@ constexpr int kChains = 16;
   X(56, "pk_mul_lo_u16 v,v", A32("v_pk_mul_lo_u16 %0, %0, %2"))                            \
   X(57, "lshlrev_b32 inl,v e64", A32("v_lshlrev_b32_e64 %0, 3, %0"))                       \
   X(58, "lshlrev_b16 inl,v", A32("v_lshlrev_b16 %0, 3, %0"))                               \
-  X(59, "add_lshl_u32 v,v,inl", A32("v_add_lshl_u32 %0, %0, %2, 3"))
+  X(59, "add_lshl_u32 v,v,inl", A32("v_add_lshl_u32 %0, %0, %2, 3"))                     \
+  X(60, "mul_lo_u32 v,s", A32("v_mul_lo_u32 %0, %0, %1"))                                  \
+  X(61, "mul_hi_u32 v,s", A32("v_mul_hi_u32 %0, %0, %1"))                                  \
+  X(62, "mad_u64_u32 v,s,v64", A64("v_mad_u64_u32 %0, vcc, %3, %1, %0"))                   \
+  X(63, "lshl_add_u64 v64,0,s64", A64S("v_lshl_add_u64 %0, %0, 0, %1"))                    \
+  X(64, "lshl_add_u64 v64,0,v64", A64V("v_lshl_add_u64 %0, %0, 0, %1"))                    \
+  X(65, "mad_u64_u32 v,v,0", A64("v_mad_u64_u32 %0, vcc, %3, %3, 0"))                      \
+  X(66, "min_u32 v,v", A32("v_min_u32 %0, %2, %0"))                                        \
+  X(67, "cmp_lt_u64_e64 + 2 cndmask_e64 (3)", A64C("v_cmp_lt_u64_e64 %3, %0, %4\n v_cndmask_b32_e64 %1, %1, %5, %3\n v_cndmask_b32_e64 %2, %2, %6, %3")) \
+  X(68, "min_f64 v64,v64", A64V("v_min_f64 %0, %0, %1"))                                   \
+  X(69, "mad_u64_u32 v,v,s64", A64SY("v_mad_u64_u32 %0, vcc, %2, %2, %1"))                  \
+  X(70, "mul_hi_u32 v,v,+mul_lo v,v (2)", A64P("v_mul_hi_u32 %0, %0, %3\n v_mul_lo_u32 %1, %1, %3")) \
+  X(71, "mad_u64_u32 v,v(vgpr c),v64", A64("v_mad_u64_u32 %0, vcc, %3, %2, %0"))
 
 // 32-bit chains r[q]; 64-bit chains w[q]; y: a VGPR, c: an SGPR
 #define A32(S) asm volatile(S : "+v"(r[q]) : "s"(c), "v"(y));
 #define A64(S) asm volatile(S : "+v"(w[q]) : "s"(c), "v"(y), "v"(y) : "vcc");
 #define A64P(S) asm volatile(S : "+v"(lo[q]), "+v"(hi[q]) : "s"(c), "v"(y) : "vcc");
 #define A32M(S) asm volatile(S : "+v"(r[q]) : "s"(c), "v"(y), "s"(mask));
+#define A64S(S) asm volatile(S : "+v"(w[q]) : "s"(mask) : "vcc");
+#define A64SY(S) asm volatile(S : "+v"(w[q]) : "s"(mask), "v"(y) : "vcc");
+#define A64V(S) asm volatile(S : "+v"(w[q]) : "v"(wy) : "vcc");
+#define A64C(S) { uint64_t sm_; asm volatile(S : "+v"(w[q]), "+v"(lo[q]), "+v"(hi[q]), "=&s"(sm_) : "v"(wy), "v"(y), "v"(y)); }
 #define A1(S) { if (q == 0) asm volatile(S : "+v"(r[q]) : "s"(c), "v"(y)); }
 #define A64Q(S) asm volatile(S : "+v"(w[q]), "+v"(lo[q]), "+v"(hi[q]) : "v"(wy), "v"(y), "v"(y) : "vcc");
 #define MIX(S1, S2)                                            \
@@ -152,7 +168,7 @@ int run(uint32_t* d_out, int n_cu, int wps) {
   CHK(hipEventSynchronize(b));
   float ms = 0;
   CHK(hipEventElapsedTime(&ms, a, b));
-  const double per = (V == 24 || V == 33 || V == 53) ? 2.0 : V == 55 ? 3.0 : V == 54 ? 1.0 / kChains : 1.0;
+  const double per = (V == 24 || V == 33 || V == 53 || V == 70) ? 2.0 : (V == 55 || V == 67) ? 3.0 : V == 54 ? 1.0 / kChains : 1.0;
   const double instr = per * kIters * kChains * wps;  // wave-instructions per SIMD
   std::printf("{\"variant\": %d, \"name\": \"%s\", \"waves_per_simd\": %d, \"ms_per_launch\": %.4f, "
               "\"cycles_per_instr_at_2.4GHz\": %.3f}\n",
