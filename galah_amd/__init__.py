@@ -291,6 +291,7 @@ class Packed:
 
     def __init__(self, ptr):
         self._p = ptr
+        self._free = _L.gg_packed_free  # kept: module globals may be gone at interpreter shutdown
         p = ptr.contents
         self.n_words = p.n_words
         self.n_bases = p.n_bases
@@ -304,7 +305,7 @@ class Packed:
 
     def free(self):
         if self._p:
-            _L.gg_packed_free(self._p)
+            self._free(self._p)
             self._p = None
 
     def __del__(self):
