@@ -64,6 +64,11 @@ constexpr int kBlock = 256;
 #ifndef GG_K1_INNER
 #define GG_K1_INNER 1
 #endif
+// k2 word's high half through v_mul_lo_u32 + v_add_u32 (1) or as the
+// compiler fuses it, v_mov + v_mad_u64_u32 (0)
+#ifndef GG_K1_K2HI
+#define GG_K1_K2HI 0
+#endif
 // candidates through the per-wave LDS queue (1) or inserted where they arise (0)
 #ifndef GG_K1_QUEUE
 #define GG_K1_QUEUE 1
@@ -216,8 +221,17 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
     asm volatile("" ::"v"(e2.w));
 #endif
     const uint32_t hx = e2.z + t3;
+#if GG_K1_K2HI
+    // high word as v_mul_lo_u32 + v_add_u32 (the compiler otherwise builds a
+    // 64-bit addend with a v_mov and a second v_mad_u64_u32)
+    const uint64_t k2p = (uint64_t)hx * (uint32_t)(c1 << 1) + (((uint64_t)e2.y << 32) | e2.x);
+    uint32_t k2m;
+    asm("v_mul_lo_u32 %0, %1, %2" : "=v"(k2m) : "v"(hx), "s"((uint32_t)((c1 << 1) >> 32)));
+    const uint64_t k2 = ((uint64_t)((uint32_t)(k2p >> 32) + k2m) << 32) | (uint32_t)k2p;
+#else
     uint64_t k2 = (uint64_t)hx * (uint32_t)(c1 << 1) + (((uint64_t)e2.y << 32) | e2.x);
     k2 += (uint64_t)(hx * (uint32_t)((c1 << 1) >> 32)) << 32;
+#endif
     h1 ^= k1;
     h1 = rotl64<27>(h1); h1 += h2; h1 = times5_plus(h1, 0x52dce729);
     h2 ^= k2;
