@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--dir", default=None)
     ap.add_argument("--repeat", default="1,4")
     ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--cache", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
     if a.child:
         return child(a)
@@ -79,6 +80,13 @@ def main():
             raise SystemExit(r.stderr)
         runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
     out["precluster_files_gz"] = runs
+    # the sketch cache: a cold call (sketches and stores
+    # every genome) then a warm one (every genome read from the cache)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", listing, "--repeat", "1",
+                        "--threads", str(a.threads), "--cache"], capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise SystemExit(r.stderr)
+    out["precluster_files_gz_cache"] = json.loads(r.stdout.strip().splitlines()[-1])
     out["precluster_files_gz_s"] = runs[0]["s"]
     out["pairs_found"] = runs[0]["pairs"]
     out["precluster_over_pack_gz"] = round(runs[0]["s"] / out["pack_gz_s"], 3)
@@ -92,6 +100,19 @@ def child(a):
     with open(a.child) as f:
         paths = [x for x in f.read().split("\n") if x] * int(a.repeat)
     rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    if a.cache:
+        cache = tempfile.mkdtemp(prefix="gg_cache_")
+        with ga.Context(k=21, sketch_size=1000, host_threads=a.threads) as ctx:
+            ctx.precluster_files(paths[:8], ga.parse_percentage(95))  # warm-up, no cache
+            res = {"genomes": len(paths)}
+            for leg in ("cold", "warm"):
+                t0 = time.perf_counter()
+                pairs, ani = ctx.precluster_files(paths, ga.parse_percentage(95), cache_dir=cache)
+                res[leg + "_s"] = round(time.perf_counter() - t0, 3)
+                res[leg + "_cached"] = int(ctx.last_cached)
+                res[leg + "_pairs"] = int(len(pairs))
+        print(json.dumps(res), flush=True)
+        return
     with ga.Context(k=21, sketch_size=1000, host_threads=a.threads) as ctx:
         ctx.precluster_files(paths[:8], ga.parse_percentage(95))  # device and library warm-up
         rss1 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
