@@ -59,8 +59,8 @@ K2_PMC = os.path.join(ROOT, "profiles", "r02_k2_pmc.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--mode", default="lib", choices=["lib", "dist"],
                     help="lib (default): one library call drives every GPU; dist: one process per GPU, "
                          "RCCL all-gather (galah_amd/sharding.py)")
