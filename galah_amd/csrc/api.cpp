@@ -613,13 +613,47 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   b.sort_tmp_bytes = index_sort_tmp_bytes(total);
   GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
   GG_HIP(c, scratch_t(c, "idx_flags", 4, &b.flags));
+  // rows of the tile rows that intersect [tb, te)
+  uint64_t I0 = UINT64_MAX, I1 = 0, t = 0;
+  for (uint64_t I = 0; I < nb && t < te; ++I) {
+    const uint64_t first = t, last = t + (nb - I);
+    t = last;
+    if (std::max(first, tb) >= std::min(last, te)) continue;
+    I0 = std::min(I0, I);
+    I1 = std::max(I1, I + 1);
+  }
+  if (I0 == UINT64_MAX) {  // no tile here: nothing to index or emit
+    *used = true;
+    return GG_OK;
+  }
+  const uint32_t r0 = (uint32_t)(I0 * GG_PAIR_TILE), r1 = (uint32_t)std::min<uint64_t>(n, I1 * GG_PAIR_TILE);
+  // A device that evaluates only some rows (a multi-device call) indexes only
+  // the entries whose hash may occur in them (GALAHGPU_INDEX_RANGE=0: every
+  // entry, as a single device does).
+  static const bool range_on = [] {
+    const char* e = getenv("GALAHGPU_INDEX_RANGE");
+    return !(e && *e == '0');
+  }();
+  // (a range of more than ~40% of the rows keeps most entries anyway: the
+  // filter would cost more than the smaller sort saves)
+  if (range_on && (r0 > 0 || r1 < n) && 5ull * (r1 - r0) <= 2ull * n) {
+    uint32_t lg = 20;
+    while (lg < 30 && (1ull << lg) < 16ull * (r1 - r0) * c->s) ++lg;
+    b.bloom_log2 = lg;
+    b.r0 = r0;
+    b.r1 = r1;
+    GG_HIP(c, scratch_t(c, "idx_bloom", (size_t)1 << (lg - 5), &b.bloom));
+  }
   uint64_t info[2] = {0, 0};
+  uint32_t kept = 0;
   GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_fill(b, st); }));
   GG_HIP(c, hipMemcpyAsync(info, b.info, sizeof info, hipMemcpyDeviceToHost, st));
+  if (b.bloom) GG_HIP(c, hipMemcpyAsync(&kept, b.flags + 1, sizeof kept, hipMemcpyDeviceToHost, st));
   GG_HIP(c, hipStreamSynchronize(st));
   // keys = the top 32 significant bits of each hash (the low 32 bits travel
-  // with the entry): shift by the bits of the largest hash beyond 32
-  const uint64_t n_entries = info[0], maxh = info[1];
+  // with the entry): shift by the bits of the largest hash beyond 32 (the
+  // row-range fill computed the same shift on the device)
+  const uint64_t n_entries = b.bloom ? kept : info[0], maxh = info[1];
   uint32_t bits = 0;
   while (bits < 64 && (maxh >> bits) != 0) ++bits;
   const uint32_t sh = bits > 32 ? bits - 32 : 0;
@@ -630,24 +664,14 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   GG_HIP(c, hipStreamSynchronize(st));
   if (flags[0]) return GG_OK;  // a run longer than kMaxRun
-  // rows of the tile rows that intersect [tb, te)
-  uint64_t I0 = UINT64_MAX, I1 = 0, t = 0;
-  for (uint64_t I = 0; I < nb && t < te; ++I) {
-    const uint64_t first = t, last = t + (nb - I);
-    t = last;
-    if (std::max(first, tb) >= std::min(last, te)) continue;
-    I0 = std::min(I0, I);
-    I1 = std::max(I1, I + 1);
-  }
   *used = true;
-  if (I0 == UINT64_MAX) return GG_OK;
   IndexLaunch a;
   a.sketches = d_sk;
   a.lens = d_lens;
   a.n = n;
   a.stride = c->s;
   a.kbits = kbits;
-  a.row0 = (uint32_t)(I0 * GG_PAIR_TILE);
+  a.row0 = r0;
   a.nb = nb;
   a.tile_begin = tb;
   a.tile_end = te;
@@ -659,8 +683,7 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   a.out = d_out;
   a.out_cap = cap;
   a.count = (unsigned long long*)d_count;
-  const uint32_t rows = (uint32_t)(std::min<uint64_t>(n, I1 * GG_PAIR_TILE) - a.row0);
-  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_index_pairs(a, rows, st); }));
+  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_index_pairs(a, r1 - r0, st); }));
   return GG_OK;
 }
 

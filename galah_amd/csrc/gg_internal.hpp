@@ -204,6 +204,14 @@ struct IndexBuild {
   void* sort_tmp;
   size_t sort_tmp_bytes;
   uint32_t* flags;     // [4]: overflow
+  // Row-range index (a device that evaluates only rows [r0, r1) of a
+  // multi-device call): bloom != null keeps just the entries whose hash may
+  // occur in those rows (a Bloom filter of the rows' hashes: no false
+  // negatives, so every run of such a hash is complete), compacted by
+  // index_fill, their count in flags[1].
+  uint32_t* bloom = nullptr;  // [1 << (bloom_log2 - 5)] words
+  uint32_t bloom_log2 = 0;
+  uint32_t r0 = 0, r1 = 0;
 };
 struct IndexLaunch {
   const uint64_t* sketches;
@@ -227,6 +235,8 @@ struct IndexLaunch {
 // Row offsets, the entry count and the largest hash (info[0], info[1]);
 // then, with the key shift and the sort's bit range, the keys, the sort and
 // the run pass (overflow: flags[0]).
+// (row-range index: then the Bloom filter over rows [r0, r1) and the kept
+// entries, already keyed: index_build sorts them)
 hipError_t index_fill(const IndexBuild& b, hipStream_t st);
 hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_t end_bit, hipStream_t st);
 size_t index_sort_tmp_bytes(uint64_t total);

@@ -16,8 +16,10 @@
 //               peers run on seven links at once; a ring all-gather would use
 //               two of them)
 //   3. pairs    device d runs K2 over part d of the upper-triangle tiles
-//               (gg_pair_partition: equal pair counts); passing pairs come
-//               back sparse
+//               (equal numbers of tile rows for the inverted index, which
+//               indexes only the entries its rows may share; equal pair
+//               counts, gg_pair_partition, for the gate kernel); passing
+//               pairs come back sparse
 //   4. merge    concatenate, sort by (i, j) (SortedPairGenomeDistanceCache
 //               order), f32 ANI per pair (src/finch.rs:56-70)
 //
@@ -171,9 +173,22 @@ gg_status gather_pairs_merge(gg_ctx* c, const std::vector<gg_ctx*>& ms, const st
   c->phase_ms[GG_PHASE_REPLICATE] = ms_since(t0);
   t0 = Clock::now();
   std::vector<std::vector<gg_pair>> part(M);
+  // Which tiles each member evaluates.  When K2 takes the inverted index
+  // (min_ani > 0: a pair needs a shared hash), a member's cost is mostly
+  // indexing the entries its rows may share (pairs_index.hip's row-range
+  // index), so the members get equal numbers of tile rows; otherwise (the
+  // gate kernel) equal numbers of pairs (gg_pair_partition).
+  const uint64_t nb = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
+  const bool by_rows = M > 1 && min_ani > 0.0f && !(min_ani != min_ani);
+  auto row_tile = [&](uint64_t I) { return I * nb - I * (I - 1) / 2; };  // first tile of tile row I
   gg_status st = on_members(c, ms, [&](size_t i, gg_ctx* m) {
     uint64_t tb = 0, te = 0;
-    gg_pair_partition(n, (uint32_t)M, (uint32_t)i, &tb, &te);
+    if (by_rows) {
+      tb = row_tile(nb * i / M);
+      te = row_tile(nb * (i + 1) / M);
+    } else {
+      gg_pair_partition(n, (uint32_t)M, (uint32_t)i, &tb, &te);
+    }
     return pairs_range_to_host(m, rows[i].sk, rows[i].len, n, tb, te, min_ani, part[i], m->stream);
   });
   if (st != GG_OK) return st;

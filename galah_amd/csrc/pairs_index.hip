@@ -113,6 +113,96 @@ __global__ __launch_bounds__(256) void index_fill_kernel(const uint64_t* __restr
   }
 }
 
+// Row-range index.  A blocked Bloom filter of the hashes of rows [r0, r1):
+// one 32-bit word per hash, two bits in it, so a test is one load (the
+// filter holds ~16 bits per row entry: ~2% false positives, which only add
+// entries to the sort).
+__device__ __forceinline__ void bloom_probe(uint64_t h, uint32_t log2b, uint32_t& word, uint32_t& mask) {
+  const uint64_t x = (h + 0x632BE59BD9B4E019ull) * 0x9E3779B97F4A7C15ull;
+  word = (uint32_t)(x >> (64 - (log2b - 5)));
+  mask = (1u << ((uint32_t)(x >> 20) & 31u)) | (1u << ((uint32_t)(x >> 26) & 31u));
+}
+
+__global__ __launch_bounds__(256) void bloom_build_kernel(const uint64_t* __restrict__ sk,
+                                                          const uint32_t* __restrict__ lens, uint32_t r0,
+                                                          uint32_t r1, uint32_t stride, uint32_t* __restrict__ bloom,
+                                                          uint32_t log2b) {
+  for (uint32_t i = r0 + blockIdx.x; i < r1; i += gridDim.x) {
+    const uint32_t len = lens[i];
+    const uint64_t* row = sk + (uint64_t)i * stride;
+    for (uint32_t k = threadIdx.x; k < len; k += 256) {
+      uint32_t w, m;
+      bloom_probe(row[k], log2b, w, m);
+      atomicOr(&bloom[w], m);
+    }
+  }
+}
+
+__device__ __forceinline__ bool bloom_test(const uint32_t* __restrict__ bloom, uint32_t log2b, uint64_t h) {
+  uint32_t w, m;
+  bloom_probe(h, log2b, w, m);
+  return (bloom[w] & m) == m;
+}
+
+// The kept entries, compacted: rows [r0, r1) keep all of theirs, other rows
+// the entries that pass the filter.  Workgroup w owns a contiguous slice of
+// rows: it counts its kept entries, reserves their space with one atomic on
+// *kept, and writes them in row order (a wave-ballot prefix per 256-entry
+// chunk).  The key shift comes from the largest hash (info[1], written by
+// index_scan_kernel before this launch), as the host computes it.
+__global__ __launch_bounds__(256) void index_fill_range_kernel(
+    const uint64_t* __restrict__ sk, const uint32_t* __restrict__ lens, uint32_t n, uint32_t stride, uint32_t kbits,
+    const uint32_t* __restrict__ bloom, uint32_t log2b, uint32_t r0, uint32_t r1,
+    const unsigned long long* __restrict__ info, uint32_t* __restrict__ kept, uint32_t* __restrict__ keys,
+    uint64_t* __restrict__ vals) {
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t base_s;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t i0 = (uint32_t)((uint64_t)n * blockIdx.x / gridDim.x);
+  const uint32_t i1 = (uint32_t)((uint64_t)n * (blockIdx.x + 1) / gridDim.x);
+  const unsigned long long maxh = info[1];
+  const uint32_t bits = maxh ? 64u - (uint32_t)__builtin_clzll(maxh) : 0u;
+  const uint32_t sh = bits > 32 ? bits - 32 : 0u;
+  uint32_t c = 0;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t len = lens[i];
+    if (i >= r0 && i < r1) {
+      if (threadIdx.x == 0) c += len;
+      continue;
+    }
+    const uint64_t* row = sk + (uint64_t)i * stride;
+    for (uint32_t k = threadIdx.x; k < len; k += 256) c += bloom_test(bloom, log2b, row[k]) ? 1u : 0u;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if (lane == 0) wsum[wave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) base_s = atomicAdd(kept, wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+  __syncthreads();
+  uint64_t o = base_s;
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t len = lens[i];
+    const uint64_t* row = sk + (uint64_t)i * stride;
+    const bool all = i >= r0 && i < r1;
+    for (uint32_t k0 = 0; k0 < len; k0 += 256) {
+      const uint32_t k = k0 + threadIdx.x;
+      const uint64_t h = k < len ? row[k] : 0ull;
+      const bool keep = k < len && (all || bloom_test(bloom, log2b, h));
+      const uint64_t m = __ballot(keep);
+      const uint32_t before = __popcll(m & ((1ull << lane) - 1ull));
+      __syncthreads();  // (the previous chunk's readers of wsum are done)
+      if (lane == 0) wsum[wave] = __popcll(m);
+      __syncthreads();
+      uint32_t base = 0;
+      for (uint32_t w = 0; w < wave; ++w) base += wsum[w];
+      if (keep) {
+        keys[o + base + before] = (uint32_t)(h >> sh);
+        vals[o + base + before] = (h << 32) | ((uint64_t)i << kbits) | k;
+      }
+      o += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    }
+  }
+}
+
 // Runs of equal keys: the thread at a run start owns it.  Every member of a
 // hash's run of g >= 2 gets runinfo = (start | g << 32) (runinfo is zeroed
 // beforehand, so g = 1 writes nothing) and ents[q] = its entry (the pairs
@@ -298,20 +388,38 @@ hipError_t index_fill(const IndexBuild& b, hipStream_t st) {
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(index_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, b.sketches, b.lens, b.n, b.stride,
                      b.offs, (unsigned long long*)b.info);
+  e = hipGetLastError();
+  if (e != hipSuccess || !b.bloom) return e;
+  // row-range index: filter, then the kept entries (their count -> flags[1])
+  e = hipMemsetAsync(b.bloom, 0, ((size_t)1 << b.bloom_log2) / 8, st);
+  if (e != hipSuccess) return e;
+  if (b.r1 > b.r0)
+    hipLaunchKernelGGL(bloom_build_kernel, dim3(std::min<uint32_t>(b.r1 - b.r0, 16384)), dim3(256), 0, st,
+                       b.sketches, b.lens, b.r0, b.r1, b.stride, b.bloom, b.bloom_log2);
+  hipLaunchKernelGGL(index_fill_range_kernel, dim3(std::max(1u, std::min<uint32_t>(b.n, 4096))), dim3(256), 0, st,
+                     b.sketches, b.lens, b.n, b.stride, b.kbits, b.bloom, b.bloom_log2, b.r0, b.r1,
+                     (const unsigned long long*)b.info, b.flags + 1, b.keys_in, b.vals_in);
   return hipGetLastError();
 }
 
 hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_t end_bit, hipStream_t st) {
   if (total == 0) return hipSuccess;
-  hipLaunchKernelGGL(index_fill_kernel, dim3(std::min<uint32_t>(b.n, 16384)), dim3(256), 0, st, b.sketches, b.lens,
-                     b.offs, b.n, b.stride, b.kbits, sh, b.keys_in, b.vals_in);
+  if (!b.bloom)  // (the row-range index filled its kept entries in index_fill)
+    hipLaunchKernelGGL(index_fill_kernel, dim3(std::min<uint32_t>(b.n, 16384)), dim3(256), 0, st, b.sketches,
+                       b.lens, b.offs, b.n, b.stride, b.kbits, sh, b.keys_in, b.vals_in);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t bytes = b.sort_tmp_bytes;
   e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out,
                                          (int)total, 0, (int)end_bit, st);
   if (e != hipSuccess) return e;
-  e = hipMemsetAsync(b.runinfo, 0, (size_t)b.n * b.stride * sizeof(uint64_t), st);
+  // runinfo of the evaluated rows (all rows, or [r0, r1) for the row-range
+  // index: other rows' slots are written by the run pass but never read)
+  if (b.bloom)
+    e = hipMemsetAsync(b.runinfo + (size_t)b.r0 * b.stride, 0, (size_t)(b.r1 - b.r0) * b.stride * sizeof(uint64_t),
+                       st);
+  else
+    e = hipMemsetAsync(b.runinfo, 0, (size_t)b.n * b.stride * sizeof(uint64_t), st);
   if (e != hipSuccess) return e;
   const uint64_t blocks = std::min<uint64_t>(65536, (total + 255) / 256);
   // the entries of shared hashes land in keys_in (free after the sort)

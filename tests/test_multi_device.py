@@ -185,3 +185,20 @@ def test_many_small_files_stream_in_batches(tmp_path):
             for g in range(len(paths)):
                 assert (sk[g][:lens[g]] == exp_sk[g][:lens[g]]).all()
                 assert (sk[g][lens[g]:] == 0).all()
+
+
+@pytest.mark.parametrize("min_ani", [0.5, 0.9])
+def test_row_range_index_partners_across_members(min_ani):
+    """Inverted-index K2 split over 2, 3 and 5 members, each indexing only the
+    entries whose hash may occur in its own rows (a Bloom filter of them):
+    cluster members are 11 rows apart, so almost every pair's partner row
+    belongs to another member's range.  Equal to one device and to the oracle."""
+    rng = np.random.default_rng(23)
+    n = 800
+    sk, lens = random_sketch_set(rng, n, 1000, 11)
+    o = oracle.pairs(sk, lens.astype(np.int32), np.float32(min_ani))
+    exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+    assert len(exp) > 1000
+    for devs in ([0], [0, 0], [0, 0, 0], [0] * 5):
+        with ga.Context(k=21, sketch_size=1000, devices=devs) as ctx:
+            assert as_tuples(ctx.pairs(sk, lens, np.float32(min_ani))) == exp, devs
