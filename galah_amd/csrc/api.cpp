@@ -922,6 +922,8 @@ void gg_destroy(gg_ctx* ctx) {
   }
   for (hipEvent_t e : ctx->spare_events) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  for (hipStream_t ps : ctx->peer_streams)
+    if (ps) (void)hipStreamDestroy(ps);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   delete ctx;
 }

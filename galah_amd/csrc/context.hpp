@@ -47,6 +47,9 @@ struct gg_ctx {
   std::vector<hipEvent_t> spare_events;
   // multi-device context: the members (owned)
   std::vector<gg_ctx*> devs;
+  // a member's copy streams, one per peer it gathers rows from (created on
+  // first use), so the copies from different peers run at once
+  std::vector<hipStream_t> peer_streams;
   // host threads for file ingest (<= 0: gg_pack_files' default)
   int host_threads = 0;
   // wall-clock phases of the last fused call (GG_PHASE_*)

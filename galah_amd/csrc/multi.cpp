@@ -100,25 +100,35 @@ void spans_of(std::vector<uint32_t>& rows, uint32_t owner, std::vector<RowSpan>&
   }
 }
 
-// Member mi copies every span it does not own from the owner's array.
+// Member mi copies every span it does not own from the owner's array.  The
+// copies from each owner go on a stream of their own: in one stream they
+// would run one after the other, and each peer is a different xGMI link (at
+// 8 devices, C3's 10 MB per peer, C4's 100 MB).
 gg_status replicate(gg_ctx* m, size_t mi, const std::vector<gg_ctx*>& ms, const std::vector<Rows>& rows,
                     const std::vector<RowSpan>& spans) {
   const size_t s = m->s;
+  if (m->peer_streams.size() < ms.size()) m->peer_streams.resize(ms.size(), nullptr);
+  std::vector<char> used(ms.size(), 0);
   for (const RowSpan& sp : spans) {
     if (sp.owner == mi) continue;
+    hipStream_t& ps = m->peer_streams[sp.owner];
+    if (!ps) GG_HIP(m, hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
+    used[sp.owner] = 1;
     const gg_ctx* o = ms[sp.owner];
     uint64_t* dsk = rows[mi].sk + (size_t)sp.row0 * s;
     const uint64_t* ssk = rows[sp.owner].sk + (size_t)sp.row0 * s;
     uint32_t* dl = rows[mi].len + sp.row0;
     const uint32_t* sl = rows[sp.owner].len + sp.row0;
     if (o->device == m->device) {
-      GG_HIP(m, hipMemcpyAsync(dsk, ssk, (size_t)sp.rows * s * sizeof(uint64_t), hipMemcpyDeviceToDevice, m->stream));
-      GG_HIP(m, hipMemcpyAsync(dl, sl, sp.rows * sizeof(uint32_t), hipMemcpyDeviceToDevice, m->stream));
+      GG_HIP(m, hipMemcpyAsync(dsk, ssk, (size_t)sp.rows * s * sizeof(uint64_t), hipMemcpyDeviceToDevice, ps));
+      GG_HIP(m, hipMemcpyAsync(dl, sl, sp.rows * sizeof(uint32_t), hipMemcpyDeviceToDevice, ps));
     } else {
-      GG_HIP(m, hipMemcpyPeerAsync(dsk, m->device, ssk, o->device, (size_t)sp.rows * s * sizeof(uint64_t), m->stream));
-      GG_HIP(m, hipMemcpyPeerAsync(dl, m->device, sl, o->device, sp.rows * sizeof(uint32_t), m->stream));
+      GG_HIP(m, hipMemcpyPeerAsync(dsk, m->device, ssk, o->device, (size_t)sp.rows * s * sizeof(uint64_t), ps));
+      GG_HIP(m, hipMemcpyPeerAsync(dl, m->device, sl, o->device, sp.rows * sizeof(uint32_t), ps));
     }
   }
+  for (size_t o = 0; o < ms.size(); ++o)
+    if (used[o]) GG_HIP(m, hipStreamSynchronize(m->peer_streams[o]));
   GG_HIP(m, hipStreamSynchronize(m->stream));
   return GG_OK;
 }
