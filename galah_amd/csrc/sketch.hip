@@ -69,9 +69,18 @@ constexpr int kBlock = 256;
 #ifndef GG_K1_K2HI
 #define GG_K1_K2HI 0
 #endif
+// k-mers that pass the high-word prefilter go to the LDS queue with their
+// finaliser states and the drain finishes the exact test (1), instead of the
+// exact test in the candidate branch (0); needs GG_K1_MULHI and GG_K1_QUEUE
+#ifndef GG_K1_DEFER
+#define GG_K1_DEFER 1
+#endif
 // candidates through the per-wave LDS queue (1) or inserted where they arise (0)
 #ifndef GG_K1_QUEUE
 #define GG_K1_QUEUE 1
+#endif
+#if GG_K1_DEFER && !(GG_K1_MULHI && GG_K1_QUEUE)
+#error "GG_K1_DEFER needs GG_K1_MULHI and GG_K1_QUEUE"
 #endif
 
 // 64-bit rotate left by a compile-time amount as two v_alignbit_b32
@@ -356,11 +365,38 @@ __device__ __forceinline__ void insert_candidate(uint64_t* __restrict__ tab,
 constexpr uint32_t kQueue = 64;
 constexpr uint32_t kQueueDrain = 32;
 struct CandQueue {
+#if GG_K1_DEFER
+  uint64_t f1[kQueue], f2[kQueue];  // fmix64_mid of h1 / h2: the exact test runs at the drain
+#else
   uint64_t h[kQueue];
+#endif
   uint32_t slot[kQueue];
   uint32_t head, tail, claim;
 };
 
+#if GG_K1_DEFER
+__device__ __forceinline__ uint64_t exact_hash(uint64_t f1, uint64_t f2) {
+  return fmix_last(f1 * kFmixC2) + fmix_last(f2 * kFmixC2);
+}
+
+// A k-mer whose high-word sum passed the prefilter: queued with its two
+// finaliser states; the drain finishes the hash and inserts it if <= tau.
+__device__ __forceinline__ void queue_push_mid(CandQueue& q, uint64_t f1, uint64_t f2, uint32_t slot,
+                                               const uint64_t* __restrict__ tau, uint64_t* __restrict__ table,
+                                               uint32_t cap_log2, uint32_t* __restrict__ flags) {
+  const uint32_t pos = atomicAdd(&q.tail, 1u);
+  if (pos - __atomic_load_n(&q.head, __ATOMIC_RELAXED) < kQueue) {
+    q.f1[pos & (kQueue - 1)] = f1;
+    q.f2[pos & (kQueue - 1)] = f2;
+    q.slot[pos & (kQueue - 1)] = slot;
+  } else {  // ring full: finish and insert now
+    const uint64_t hv = exact_hash(f1, f2);
+    if (hv <= tau[slot]) insert_candidate(table + ((uint64_t)slot << cap_log2), (1u << cap_log2) - 1u, flags + slot, hv);
+  }
+}
+#endif
+
+#if !GG_K1_DEFER
 __device__ __forceinline__ void queue_push(CandQueue& q, uint64_t hv, uint32_t slot, uint64_t* __restrict__ table,
                                            uint32_t cap_log2, uint32_t* __restrict__ flags) {
   const uint32_t pos = atomicAdd(&q.tail, 1u);
@@ -371,11 +407,13 @@ __device__ __forceinline__ void queue_push(CandQueue& q, uint64_t hv, uint32_t s
     insert_candidate(table + ((uint64_t)slot << cap_log2), (1u << cap_log2) - 1u, flags + slot, hv);
   }
 }
+#endif
 
 // Insert the queued candidates with the lanes that are active (all of them
 // at the end of the kernel).  Positions past head + kQueue were inserted by
 // their pushes.
-__device__ __forceinline__ void queue_drain(CandQueue& q, uint64_t* __restrict__ table, uint32_t cap_log2,
+__device__ __forceinline__ void queue_drain(CandQueue& q, const uint64_t* __restrict__ tau,
+                                            uint64_t* __restrict__ table, uint32_t cap_log2,
                                             uint32_t* __restrict__ flags, uint32_t min_pending) {
   const uint32_t head = __atomic_load_n(&q.head, __ATOMIC_RELAXED);
   const uint32_t tail = __atomic_load_n(&q.tail, __ATOMIC_RELAXED);
@@ -387,7 +425,13 @@ __device__ __forceinline__ void queue_drain(CandQueue& q, uint64_t* __restrict__
     if (e >= end) break;
     const uint32_t x = e & (kQueue - 1);
     const uint32_t sl = q.slot[x];
+#if GG_K1_DEFER
+    const uint64_t hv = exact_hash(q.f1[x], q.f2[x]);
+    if (hv <= tau[sl]) insert_candidate(table + ((uint64_t)sl << cap_log2), cap_mask, flags + sl, hv);
+#else
+    (void)tau;
     insert_candidate(table + ((uint64_t)sl << cap_log2), cap_mask, flags + sl, q.h[x]);
+#endif
   }
   // every active lane is past its last claim here (lockstep): reopen the ring
   __atomic_store_n(&q.head, tail, __ATOMIC_RELAXED);
@@ -549,7 +593,10 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
         // the candidates
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
-#if GG_K1_INNER
+#if GG_K1_DEFER
+          if (hs[j] <= thr && (uint32_t)(g * kGroup + j) < cnt)
+            queue_push_mid(q, f1[j], f2[j], slot, a.tau, a.table, a.cap_log2, a.flags);
+#elif GG_K1_INNER
           // one k-mer of the group passes in one lane, typically: the exact
           // hash only under its own test (the wave skips the others)
           if (hs[j] <= thr && (uint32_t)(g * kGroup + j) < cnt) {
@@ -598,9 +645,9 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
 #endif
       }
     }
-    queue_drain(q, a.table, a.cap_log2, a.flags, kQueueDrain);
+    queue_drain(q, a.tau, a.table, a.cap_log2, a.flags, kQueueDrain);
   }
-  queue_drain(q, a.table, a.cap_log2, a.flags, 1);  // every lane of the wave is back
+  queue_drain(q, a.tau, a.table, a.cap_log2, a.flags, 1);  // every lane of the wave is back
 }
 
 // One workgroup per genome slot: gather the set into LDS, sort it, keep the
