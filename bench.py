@@ -495,7 +495,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    line = run_lib(a, world, rank) if a.mode == "lib" else run_dist(a, world, rank, local)
+    mode = a.mode
+    if mode == "lib" and world > 1 and not a.devices and torch.cuda.device_count() < world:
+        # a launcher that shows each rank only its own GPU: one process per
+        # GPU with the RCCL all-gather instead of one process driving all
+        mode = "dist"
+    line = run_lib(a, world, rank) if mode == "lib" else run_dist(a, world, rank, local)
     if rank == 0 and line is not None:
         print(json.dumps(line), flush=True)
 
