@@ -75,6 +75,11 @@ constexpr int kBlock = 256;
 #ifndef GG_K1_DEFER
 #define GG_K1_DEFER 1
 #endif
+// with the deferred test: the passing lanes of a wave reserve their queue
+// positions with one LDS atomic (ballot + rank) (1) or one each (0)
+#ifndef GG_K1_WAVEPUSH
+#define GG_K1_WAVEPUSH 0
+#endif
 // candidates through the per-wave LDS queue (1) or inserted where they arise (0)
 #ifndef GG_K1_QUEUE
 #define GG_K1_QUEUE 1
@@ -409,6 +414,32 @@ __device__ __forceinline__ void queue_push(CandQueue& q, uint64_t hv, uint32_t s
 }
 #endif
 
+#if GG_K1_DEFER && GG_K1_WAVEPUSH
+// queue_push_mid for every lane of the wave whose k-mer passed (m = the
+// wave's ballot, uniform): one lane reserves the positions, each passing lane
+// takes base + its rank among them (one LDS atomic per wave instead of one
+// serialised atomic per passing lane).
+__device__ __forceinline__ void queue_push_wave(CandQueue& q, uint64_t m, bool pass, uint64_t f1, uint64_t f2,
+                                                uint32_t slot, const uint64_t* __restrict__ tau,
+                                                uint64_t* __restrict__ table, uint32_t cap_log2,
+                                                uint32_t* __restrict__ flags) {
+  const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+  uint32_t base = 0;
+  if (__lane_id() == leader) base = atomicAdd(&q.tail, (uint32_t)__popcll(m));
+  base = __builtin_amdgcn_readlane(base, leader);
+  if (!pass) return;
+  const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  if (pos - __atomic_load_n(&q.head, __ATOMIC_RELAXED) < kQueue) {
+    q.f1[pos & (kQueue - 1)] = f1;
+    q.f2[pos & (kQueue - 1)] = f2;
+    q.slot[pos & (kQueue - 1)] = slot;
+  } else {  // ring full: finish and insert now
+    const uint64_t hv = exact_hash(f1, f2);
+    if (hv <= tau[slot]) insert_candidate(table + ((uint64_t)slot << cap_log2), (1u << cap_log2) - 1u, flags + slot, hv);
+  }
+}
+#endif
+
 // Insert the queued candidates with the lanes that are active (all of them
 // at the end of the kernel).  Positions past head + kQueue were inserted by
 // their pushes.
@@ -593,7 +624,11 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
         // the candidates
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
-#if GG_K1_DEFER
+#if GG_K1_DEFER && GG_K1_WAVEPUSH
+          const bool pass = hs[j] <= thr && (uint32_t)(g * kGroup + j) < cnt;
+          const uint64_t m = __ballot(pass);
+          if (m) queue_push_wave(q, m, pass, f1[j], f2[j], slot, a.tau, a.table, a.cap_log2, a.flags);
+#elif GG_K1_DEFER
           if (hs[j] <= thr && (uint32_t)(g * kGroup + j) < cnt)
             queue_push_mid(q, f1[j], f2[j], slot, a.tau, a.table, a.cap_log2, a.flags);
 #elif GG_K1_INNER
