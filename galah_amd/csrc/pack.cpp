@@ -51,10 +51,11 @@ struct ByteClass {
 };
 const ByteClass kClass;
 
-// 16 bytes that are all A/C/G/T/U in either case -> their 2-bit codes
-// (A0 C1 G2 T3, U as T), first byte in bits 31..30; false otherwise.
-// ((c >> 1) ^ (c >> 2)) & 3 maps exactly those ten letters to their codes.
-__attribute__((target("sse4.1"))) inline bool pack16(const uint8_t* p, uint32_t* word) {
+// 16 bytes -> their 2-bit codes (A0 C1 G2 T3, U as T; first byte in bits
+// 31..30) and the mask of the bytes that are A/C/G/T/U in either case (bit b
+// = byte b; codes of other bytes are garbage).  ((c >> 1) ^ (c >> 2)) & 3
+// maps exactly those ten letters to their codes.
+__attribute__((target("sse4.1"))) inline uint32_t pack16(const uint8_t* p, uint32_t* word) {
   const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
   const __m128i v = _mm_or_si128(c, _mm_set1_epi8(0x20));  // lower case
   __m128i ok = _mm_cmpeq_epi8(v, _mm_set1_epi8('a'));
@@ -62,14 +63,13 @@ __attribute__((target("sse4.1"))) inline bool pack16(const uint8_t* p, uint32_t*
   ok = _mm_or_si128(ok, _mm_cmpeq_epi8(v, _mm_set1_epi8('g')));
   ok = _mm_or_si128(ok, _mm_cmpeq_epi8(v, _mm_set1_epi8('t')));
   ok = _mm_or_si128(ok, _mm_cmpeq_epi8(v, _mm_set1_epi8('u')));
-  if (_mm_movemask_epi8(ok) != 0xFFFF) return false;
   const __m128i code = _mm_and_si128(_mm_xor_si128(_mm_srli_epi16(c, 1), _mm_srli_epi16(c, 2)), _mm_set1_epi8(3));
   // pairs -> 4-bit, quads -> 8-bit (base 0 most significant)
   const __m128i q2 = _mm_maddubs_epi16(code, _mm_set1_epi16(0x0104));  // 4 * even + odd
   const __m128i q4 = _mm_madd_epi16(q2, _mm_set1_epi32(0x00010010));   // 16 * lo + hi
   const __m128i b = _mm_packus_epi16(_mm_packus_epi32(q4, q4), _mm_setzero_si128());
   *word = __builtin_bswap32((uint32_t)_mm_cvtsi128_si32(b));
-  return true;
+  return (uint32_t)_mm_movemask_epi8(ok);
 }
 
 // Packs the runs of ONE genome; bases start at word 0 of its own buffer.
@@ -119,6 +119,31 @@ struct GenomePacker {
     }
   }
 
+  // The first j (1..15) bases of word (MSB-first 2-bit codes; the rest of
+  // word is ignored).
+  inline void push_n(uint32_t word, uint32_t j) {
+    if (!in_run) {
+      in_run = true;
+      run_start = n_bases;
+    }
+    word &= ~0u << (32 - 2 * j);
+    if (fill == 0) {
+      cur = word;
+      fill = j;
+    } else {
+      cur |= word >> (2 * fill);
+      const uint32_t nf = fill + j;
+      if (nf >= 16) {
+        words.push_back(cur);
+        cur = nf > 16 ? word << (32 - 2 * fill) : 0u;
+        fill = nf - 16;
+      } else {
+        fill = nf;
+      }
+    }
+    n_bases += j;
+  }
+
   // 16 bases at once (word = their MSB-first 2-bit codes).
   inline void push16(uint32_t word) {
     if (!in_run) {
@@ -134,14 +159,28 @@ struct GenomePacker {
     n_bases += 16;
   }
 
-  // One record's sequence bytes (may contain line breaks).
+  // One record's sequence bytes (may contain line breaks).  16 bytes at a
+  // time: all bases (the common case) in one step; otherwise the bases
+  // before the first other byte in one step, then that byte (a line break
+  // of a 60-column file costs one step, not one per byte up to it).
   void add_sequence(const uint8_t* p, size_t n) {
     size_t i = 0;
     while (i < n) {
       uint32_t word;
-      if (i + 16 <= n && pack16(p + i, &word)) {  // the common case: 16 bases
-        push16(word);
-        i += 16;
+      if (i + 16 <= n) {
+        const uint32_t m = pack16(p + i, &word);
+        if (m == 0xFFFFu) {
+          push16(word);
+          i += 16;
+          continue;
+        }
+        const uint32_t j = (uint32_t)__builtin_ctz(~m);  // leading bases
+        if (j) {
+          push_n(word, j);
+          i += j;
+        }
+        if (kClass.t[p[i]] == kBreak) end_run();  // (else whitespace: skipped)
+        ++i;
         continue;
       }
       const uint8_t c = kClass.t[p[i]];

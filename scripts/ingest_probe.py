@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--dir", default=None)
     ap.add_argument("--repeat", default="1,4")
+    ap.add_argument("--line", type=int, default=80, help="FASTA line width")
+    ap.add_argument("--reuse", action="store_true", help="keep files already in --dir")
     ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cache", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args()
@@ -47,21 +49,23 @@ def main():
         seq = root.copy()
         mut = rng.random(a.len) < 0.02 * (i % 4)
         seq[mut] = acgt[rng.integers(0, 4, int(mut.sum()))]
-        lines = seq[: a.len // 80 * 80].reshape(-1, 80)
+        lines = seq[: a.len // a.line * a.line].reshape(-1, a.line)
         body = b"\n".join(bytes(x) for x in lines)
         data = b">genome_%d synthetic\n" % i + body + b"\n"
         for kind in ("plain", "gz"):
             p = os.path.join(d, "g%05d.fna%s" % (i, ".gz" if kind == "gz" else ""))
+            paths[kind].append(p)
+            if a.reuse and os.path.exists(p):  # (the same seeded files from an earlier run)
+                continue
             if kind == "gz":
                 with gzip.open(p, "wb", compresslevel=6) as f:
                     f.write(data)
             else:
                 with open(p, "wb") as f:
                     f.write(data)
-            paths[kind].append(p)
     gen_s = time.perf_counter() - t0
-    out = {"files": a.files, "genome_len": a.len, "threads": a.threads, "generate_s": round(gen_s, 2)}
-    bases = a.files * (a.len // 80 * 80)
+    out = {"files": a.files, "genome_len": a.len, "line": a.line, "threads": a.threads, "generate_s": round(gen_s, 2)}
+    bases = a.files * (a.len // a.line * a.line)
     for kind in ("plain", "gz"):
         t0 = time.perf_counter()
         pk = ga.pack_files(paths[kind], threads=a.threads)

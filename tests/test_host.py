@@ -289,3 +289,43 @@ def test_packer_multi_member_gzip_and_decoders(tmp_path, monkeypatch):
             "assert (a.words == b.words).all() and (a.runs == b.runs).all()" % (ROOT, str(plain), str(gz)))
     env = dict(os.environ, GALAHGPU_NO_LIBDEFLATE="1")
     subprocess.run([sys.executable, "-c", code], check=True, env=env)
+
+
+def reference_runs(seq, k=21):
+    """needletail normalize(false) + the "all k bytes in ACGT" window test,
+    restated: the maximal A/C/G/T stretches of length >= k (upper case, U as
+    T, whitespace dropped without breaking)."""
+    out, cur = [], bytearray()
+    for ch in seq:
+        c = chr(ch)
+        if c in " \t\r\n":
+            continue
+        c = c.upper().replace("U", "T")
+        if c in "ACGT":
+            cur.append(ord(c))
+            continue
+        if len(cur) >= k:
+            out.append(bytes(cur))
+        cur = bytearray()
+    if len(cur) >= k:
+        out.append(bytes(cur))
+    return out
+
+
+@pytest.mark.parametrize("width", [1, 7, 15, 16, 17, 31, 33, 59, 60, 61, 64, 70, 79, 80, 81, 127])
+def test_packer_line_widths_exact_runs(tmp_path, width):
+    """Wrapped FASTA at every line width around the packer's 16-byte steps
+    (LF and CRLF, lower case, U, IUPAC and N breaks): the packed runs are
+    exactly the reference's A/C/G/T stretches, base for base."""
+    rng = np.random.default_rng(width)
+    body = bytearray(rng.choice(np.frombuffer(b"ACGTacgtU", np.uint8), size=4000,
+                                p=[.24, .24, .24, .24, .01, .01, .01, .004, .006]).tobytes())
+    for x in rng.integers(0, len(body), 6):
+        body[x] = ord("N") if x % 2 else ord("R")
+    eol = b"\r\n" if width % 2 else b"\n"
+    text = b">r1 test\n" + eol.join(bytes(body[i:i + width]) for i in range(0, len(body), width)) + eol
+    p = tmp_path / ("w%d.fa" % width)
+    p.write_bytes(text)
+    pk = ga.pack_files([str(p)], k=21)
+    assert packed_records(pk)[0] == reference_runs(bytes(body))
+    pk.free()
