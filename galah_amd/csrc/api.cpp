@@ -260,16 +260,16 @@ gg_status index_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t n_
   for (int t = 0; t < T; ++t) coff[t + 1] = coff[t] + csum[t];
   ix.rs[n_runs] = coff[T];
   ix.nk.assign(n_genomes, 0);
-  parallel_chunks(n_runs, T, [&](int t, uint64_t b, uint64_t e) {
+  // segment starts (prefix within each run chunk) and k-mers per genome are
+  // independent: one team of threads does both
+  parallel_chunks((uint64_t)T, T, [&](int t, uint64_t, uint64_t) {
     uint64_t acc = coff[t];
-    for (uint64_t r = b; r < e; ++r) {
+    for (uint64_t r = n_runs * t / T, e = n_runs * (t + 1) / T; r < e; ++r) {
       const uint64_t v = ix.rs[r];
       ix.rs[r] = acc;
       acc += v;
     }
-  });
-  parallel_chunks(n_genomes, T, [&](int, uint64_t b, uint64_t e) {
-    for (uint64_t g = b; g < e; ++g) {
+    for (uint64_t g = (uint64_t)n_genomes * t / T, e = (uint64_t)n_genomes * (t + 1) / T; g < e; ++g) {
       uint64_t nk = 0;
       for (uint64_t r = ix.gr[g]; r < ix.gr[g + 1]; ++r) nk += runs[r].len - k + 1;
       ix.nk[g] = nk;
