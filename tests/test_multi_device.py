@@ -202,3 +202,30 @@ def test_row_range_index_partners_across_members(min_ani):
     for devs in ([0], [0, 0], [0, 0, 0], [0] * 5):
         with ga.Context(k=21, sketch_size=1000, devices=devs) as ctx:
             assert as_tuples(ctx.pairs(sk, lens, np.float32(min_ani))) == exp, devs
+
+
+def test_precluster_shards_mixed_lengths_s10000_1_vs_3_devices():
+    """C5's shape at reduced scale: 900 genomes of 0.2-2 Mbp with N runs,
+    s = 10000, sharded over 1 and 3 members (K1 per member, replication of
+    80 KB rows, the row-range index at s = 10000): identical pairs and ANI."""
+    torch = torch_dev()
+    n, cl, s = 900, 10, 10000
+    thr = ga.parse_percentage(95)
+    results = []
+    for devs in ([0], [0, 0, 0]):
+        with ga.Context(k=21, sketch_size=s, devices=devs) as ctx:
+            M = ctx.device_count
+            cuts = [n * m // M for m in range(M + 1)]
+            shards, keep = [], []
+            for m in range(M):
+                g0, g1 = cuts[m], cuts[m + 1]
+                lens_bp = ga.synth_mixed_lengths(g1 - g0, 200000, 2000000, cl, 7, first_genome=g0)
+                d_words = torch.empty(max(1, int(lens_bp.sum()) // 16), dtype=torch.int32, device="cuda")
+                runs = ctx.member(m).synth_mixed_device(lens_bp, cl, 0.07, 1e-4, 8, d_words, first_genome=g0)
+                torch.cuda.synchronize()
+                shards.append((d_words, runs, g1 - g0))
+                keep.append(d_words)
+            pairs, ani = ctx.precluster_shards(shards, thr)
+            results.append((as_tuples(pairs), ani.tolist()))
+    assert len(results[0][0]) > 500
+    assert results[1] == results[0]
