@@ -280,6 +280,32 @@ gg_status index_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t n_
 
 }  // namespace
 
+gg_status check_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t n_genomes, uint64_t n_words) {
+  if (n_runs && !runs) return fail(c, GG_ERR_INVALID_ARG, "null run table");
+  const int T = n_runs >= (1u << 18) ? std::max(1, std::min(16, ingest_threads(c->host_threads))) : 1;
+  const uint32_t k = (uint32_t)c->k;
+  std::vector<uint64_t> bad(T, ~0ull);
+  parallel_chunks(n_runs, T, [&](int t, uint64_t b, uint64_t e) {
+    for (uint64_t r = b; r < e; ++r) {
+      const gg_run& x = runs[r];
+      const uint32_t prev = r ? runs[r - 1].genome : 0u;
+      if (x.genome >= n_genomes || x.genome < prev || x.len < k || x.base + x.len > n_words * 16ull ||
+          x.base + x.len < x.base) {
+        bad[t] = r;
+        return;
+      }
+    }
+  });
+  const uint64_t first_bad = *std::min_element(bad.begin(), bad.end());
+  if (first_bad == ~0ull) return GG_OK;
+  const gg_run& x = runs[first_bad];
+  const uint32_t prev = first_bad ? runs[first_bad - 1].genome : 0u;
+  if (x.genome >= n_genomes || x.genome < prev)
+    return fail(c, GG_ERR_INVALID_ARG, "runs must be grouped by non-decreasing genome < n_genomes");
+  if (x.len < k) return fail(c, GG_ERR_INVALID_ARG, "run shorter than k");
+  return fail(c, GG_ERR_INVALID_ARG, "run extends past the packed words");
+}
+
 // GALAHGPU_HOST_PROFILE=1: per-stage host wall times of sketch_core on stderr
 struct HostProf {
   bool on;
@@ -585,9 +611,10 @@ gg_status pairs_gate(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
 
 // Inverted-index K2 (pairs_index.hip) over tiles [tb, te).  *used = false
 // when the index path does not apply (a hash shared by more than kMaxRun
-// sketches); nothing has been emitted then and the caller runs the gate
-// kernel.  Eligibility (no pass without a shared hash, sizes) is the
-// caller's.
+// sketches, or a row whose partners overflow the LDS map at 2^16 partner
+// classes); the output count is then as before the call and the caller runs
+// the gate kernel.  Eligibility (no pass without a shared hash, sizes) is
+// the caller's.
 gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n, uint64_t nb,
                       uint64_t tb, uint64_t te, const uint32_t* d_cmin, const uint32_t* d_sufmin, gg_pair* d_out,
                       uint64_t cap, uint64_t* d_count, uint64_t work, hipStream_t st, bool* used) {
@@ -683,7 +710,24 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   a.out = d_out;
   a.out_cap = cap;
   a.count = (unsigned long long*)d_count;
+  // GALAHGPU_INDEX_MAX_SPLIT (tests): fewer partner classes per row, so the
+  // overflow fallback below can be reached on small inputs
+  {
+    const char* e = getenv("GALAHGPU_INDEX_MAX_SPLIT");
+    a.max_split_log2 = e && *e ? (uint32_t)std::min(16, std::max(0, atoi(e))) : 16u;
+  }
+  a.overflow = b.flags + 2;  // (zeroed by index_fill)
+  // the output count before this launch: restored if a row overflows
+  uint64_t* d_count0;
+  GG_HIP(c, scratch_t(c, "idx_count0", 1, &d_count0));
+  GG_HIP(c, hipMemcpyAsync(d_count0, d_count, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
   GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_index_pairs(a, r1 - r0, st); }));
+  GG_HIP(c, hipMemcpyAsync(flags, b.flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  GG_HIP(c, hipStreamSynchronize(st));
+  if (flags[0]) {  // a row's partners did not fit the LDS map: drop what this launch emitted
+    GG_HIP(c, hipMemcpyAsync(d_count, d_count0, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
+    *used = false;
+  }
   return GG_OK;
 }
 

@@ -82,6 +82,10 @@ hipError_t scratch_t(gg_ctx* c, const char* key, size_t count, T** out) {
 // Grow-only pinned host buffer of the context (contents not preserved).
 hipError_t pinned(gg_ctx* c, size_t bytes, void** out);
 
+// The run-table checks sketch_core applies (genome < n_genomes and
+// non-decreasing, len >= k, base + len <= 16 n_words), for callers that
+// read the table before sketch_core does (gg_sketch splits it by genome).
+gg_status check_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t n_genomes, uint64_t n_words);
 // K1 over device-resident packed words; runs are host metadata with genome
 // indices in [0, n_genomes).  Row g of d_out / entry g of d_lens receive
 // genome g, or genome g goes to row d_row_of[g] when d_row_of (device, n_genomes

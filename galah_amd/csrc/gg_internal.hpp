@@ -231,6 +231,8 @@ struct IndexLaunch {
   gg_pair* out;
   uint64_t out_cap;
   unsigned long long* count;
+  uint32_t max_split_log2;  // a row's partners split into at most 2^this classes (16)
+  uint32_t* overflow;       // set when a row's partners overflow the LDS map at the last split
 };
 // Row offsets, the entry count and the largest hash (info[0], info[1]);
 // then, with the key shift and the sort's bit range, the keys, the sort and

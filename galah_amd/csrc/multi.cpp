@@ -119,13 +119,10 @@ gg_status replicate(gg_ctx* m, size_t mi, const std::vector<gg_ctx*>& ms, const 
     const uint64_t* ssk = rows[sp.owner].sk + (size_t)sp.row0 * s;
     uint32_t* dl = rows[mi].len + sp.row0;
     const uint32_t* sl = rows[sp.owner].len + sp.row0;
-    if (o->device == m->device) {
-      GG_HIP(m, hipMemcpyAsync(dsk, ssk, (size_t)sp.rows * s * sizeof(uint64_t), hipMemcpyDeviceToDevice, ps));
-      GG_HIP(m, hipMemcpyAsync(dl, sl, sp.rows * sizeof(uint32_t), hipMemcpyDeviceToDevice, ps));
-    } else {
-      GG_HIP(m, hipMemcpyPeerAsync(dsk, m->device, ssk, o->device, (size_t)sp.rows * s * sizeof(uint64_t), ps));
-      GG_HIP(m, hipMemcpyPeerAsync(dl, m->device, sl, o->device, sp.rows * sizeof(uint32_t), ps));
-    }
+    // one call for every member pair, same device included (a peer copy with
+    // src == dst device is legal), so the one-GPU tests run the node's code
+    GG_HIP(m, hipMemcpyPeerAsync(dsk, m->device, ssk, o->device, (size_t)sp.rows * s * sizeof(uint64_t), ps));
+    GG_HIP(m, hipMemcpyPeerAsync(dl, m->device, sl, o->device, sp.rows * sizeof(uint32_t), ps));
   }
   for (size_t o = 0; o < ms.size(); ++o)
     if (used[o]) GG_HIP(m, hipStreamSynchronize(m->peer_streams[o]));
@@ -641,6 +638,17 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
   return GG_OK;
 }
 
+// Direct access from device a to device b's memory: true when a == b (a
+// device always reaches its own memory) or when the peer link is enabled.
+bool enable_peer(int a, int b) {
+  if (a == b) return true;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can || hipSetDevice(a) != hipSuccess) return false;
+  const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+  return e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
+}
+
 // Contiguous genome ranges with about equal k-mer counts, one per member.
 std::vector<uint32_t> balance_genomes(const gg_run* runs, uint64_t n_runs, uint32_t n_genomes, int k, size_t M) {
   std::vector<uint64_t> per(n_genomes + 1, 0);
@@ -726,17 +734,11 @@ gg_ctx* gg_create_multi(int kmer_length, uint32_t sketch_size, uint64_t hash_see
     c->devs.push_back(m);
   }
   c->device = list[0];
-  // direct xGMI peer access between every pair of distinct devices (a copy
-  // between devices without it is staged through the host)
+  // direct xGMI peer access between every pair of members (a copy between
+  // devices without it is staged through the host); the same loop runs for
+  // repeated ordinals, where it is a no-op
   for (int a : list)
-    for (int b : list) {
-      if (a == b) continue;
-      int can = 0;
-      if (hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can && hipSetDevice(a) == hipSuccess) {
-        const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
-        if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
-      }
-    }
+    for (int b : list) (void)enable_peer(a, b);
   (void)hipSetDevice(list[0]);
   *status = GG_OK;
   return c;
@@ -774,6 +776,10 @@ gg_status gg_sketch(gg_ctx* ctx, const gg_packed* packed, uint64_t* out_hashes, 
   if (ng == 0) return GG_OK;
   const std::vector<gg_ctx*> ms = members(ctx);
   const size_t s = ctx->s;
+  // the run table is split by genome below, before sketch_core sees it
+  gg_status vs = check_runs(ctx, packed->runs, packed->n_runs, ng, packed->n_words);
+  if (vs != GG_OK) return vs;
+  if (packed->n_runs && !packed->words) return fail(ctx, GG_ERR_INVALID_ARG, "gg_sketch: null packed words");
   // contiguous genome ranges of about equal k-mer counts; each member copies
   // the packed words its range spans and sketches it
   const std::vector<uint32_t> cut = balance_genomes(packed->runs, packed->n_runs, ng, ctx->k, ms.size());
@@ -787,9 +793,12 @@ gg_status gg_sketch(gg_ctx* ctx, const gg_packed* packed, uint64_t* out_hashes, 
     const gg_run* re = std::lower_bound(rb, rend, g1,
                                         [](const gg_run& r, uint32_t g) { return r.genome < g; });
     uint64_t w0 = 0, w1 = 0;
-    if (rb != re) {
-      w0 = rb->base / 16;
-      for (const gg_run* r = rb; r != re; ++r) w1 = std::max<uint64_t>(w1, (r->base + r->len + 15) / 16);
+    if (rb != re) {  // the words the range's runs touch (bases need not rise with the genome)
+      w0 = ~0ull;
+      for (const gg_run* r = rb; r != re; ++r) {
+        w0 = std::min<uint64_t>(w0, r->base / 16);
+        w1 = std::max<uint64_t>(w1, (r->base + r->len + 15) / 16);
+      }
     }
     std::vector<gg_run> runs(rb, re);
     for (gg_run& r : runs) {

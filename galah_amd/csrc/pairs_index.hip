@@ -356,11 +356,17 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
       }
     }
     __syncthreads();
-    if (over && plog2 < 16) {  // too many partners for one map: split them in twice as many classes
-      ++plog2;
-      p = 0;
-      __syncthreads();
-      continue;
+    if (over) {
+      if (plog2 < a.max_split_log2) {  // too many partners for one map: split them in twice as many classes
+        ++plog2;
+        p = 0;
+        __syncthreads();
+        continue;
+      }
+      // still too many in one class: the counts would be incomplete, so emit
+      // nothing; the host discards this launch's output and runs the gate kernel
+      if (tid == 0) atomicOr(a.overflow, 1u);
+      return;
     }
     for (uint32_t x = tid; x < kMap; x += kRowThreads) {
       const uint32_t key = mkey[x];

@@ -31,61 +31,13 @@
 namespace gg {
 namespace {
 
-#ifndef GG_K1_GROUP
-#define GG_K1_GROUP 4
-#endif
-constexpr int kGroup = GG_K1_GROUP;  // k-mers per tau-check branch
+constexpr int kGroup = 4;  // k-mers per tau-check branch (1 or 2: within noise, profiles/r02_k1_group_defer_ab/)
 constexpr int kBlock = 256;
 // min waves per SIMD forced on the register allocator: 7 (72 VGPRs, 4 dwords
 // spilled at k = 21) beats the unconstrained 76 VGPRs / 6 waves with the
 // candidate queue (C3 K1 49.3 -> 49.1 ms, C5 78.7 -> 77.9 ms)
 #ifndef GG_K1_MIN_WAVES
 #define GG_K1_MIN_WAVES 7
-#endif
-// canonical code: high word as v_min_u32 of the two high words (1) instead of
-// a second v_cndmask on the 64-bit compare (0)
-#ifndef GG_K1_MINHI
-#define GG_K1_MINHI 0
-#endif
-// tau prefilter: high words of the last fmix64 multiplies as v_mul_hi_u32 +
-// two v_mul_lo_u32 (1; the full products only in the candidate branch) or as
-// the full 64-bit products (0)
-#ifndef GG_K1_MULHI
-#define GG_K1_MULHI 1
-#endif
-// k2 group-4b+2 entry read as one ds_read_b128 (1; its unused 4th dword kept
-// live by an empty asm) instead of the ds_read_b64 + ds_read_b32 the
-// compiler splits it into (0)
-#ifndef GG_K1_K2A128
-#define GG_K1_K2A128 1
-#endif
-// candidate branch: the exact hash of each k-mer of the group under its own
-// high-word test (1) or of all of them once the group's test passes (0)
-#ifndef GG_K1_INNER
-#define GG_K1_INNER 1
-#endif
-// k2 word's high half through v_mul_lo_u32 + v_add_u32 (1) or as the
-// compiler fuses it, v_mov + v_mad_u64_u32 (0)
-#ifndef GG_K1_K2HI
-#define GG_K1_K2HI 0
-#endif
-// k-mers that pass the high-word prefilter go to the LDS queue with their
-// finaliser states and the drain finishes the exact test (1), instead of the
-// exact test in the candidate branch (0); needs GG_K1_MULHI and GG_K1_QUEUE
-#ifndef GG_K1_DEFER
-#define GG_K1_DEFER 1
-#endif
-// with the deferred test: the passing lanes of a wave reserve their queue
-// positions with one LDS atomic (ballot + rank) (1) or one each (0)
-#ifndef GG_K1_WAVEPUSH
-#define GG_K1_WAVEPUSH 0
-#endif
-// candidates through the per-wave LDS queue (1) or inserted where they arise (0)
-#ifndef GG_K1_QUEUE
-#define GG_K1_QUEUE 1
-#endif
-#if GG_K1_DEFER && !(GG_K1_MULHI && GG_K1_QUEUE)
-#error "GG_K1_DEFER needs GG_K1_MULHI and GG_K1_QUEUE"
 #endif
 
 // 64-bit rotate left by a compile-time amount as two v_alignbit_b32
@@ -115,15 +67,6 @@ __device__ __forceinline__ uint64_t add_rotl31(uint64_t x, uint64_t y) {
   return out;
 }
 
-// fmix64 without its final k ^= k >> 33, which leaves the high word alone
-// (see the tau prefilter in sketch_candidates_kernel).
-__device__ __forceinline__ uint64_t fmix64_pre(uint64_t k) {
-  k ^= k >> 33;
-  k *= 0xff51afd7ed558ccdull;
-  k ^= k >> 33;
-  k *= 0xc4ceb9fe1a85ec53ull;
-  return k;
-}
 __device__ __forceinline__ uint64_t fmix_last(uint64_t k) { return k ^ (k >> 33); }
 
 // fmix64 up to its second multiply: fmix64_pre(k) = fmix64_mid(k) * kFmixC2
@@ -215,12 +158,8 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
     const uint64_t* bt = tab + b * S::BLK_U64;
     const ulonglong2 e0 = *(const ulonglong2*)(bt + S::K1A + 2 * group_byte(hi, lo, 4 * b));
     const uint2 e1 = *(const uint2*)(bt + S::K1B + group_byte(hi, lo, 4 * b + 1));
-#if GG_K1_K2A128
     const ulonglong2 e2q = *(const ulonglong2*)(bt + S::K2A + 2 * group_byte(hi, lo, 4 * b + 2));
     const uint4 e2 = make_uint4((uint32_t)e2q.x, (uint32_t)(e2q.x >> 32), (uint32_t)e2q.y, (uint32_t)(e2q.y >> 32));
-#else
-    const uint4 e2 = *(const uint4*)(bt + S::K2A + 2 * group_byte(hi, lo, 4 * b + 2));
-#endif
     const uint32_t t3 = ((const uint32_t*)(bt + S::K2B))[group_byte(hi, lo, 4 * b + 3)];
     // rotl(k1 * c1, 31) * c2
     const uint32_t v = ((uint32_t)e0.y + e1.y) >> 1;
@@ -231,21 +170,10 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
     // 2 hi(x) + bit 31 of lo(x) = 2 hi(x) + bit 31 of lo(T2), so
     // rotl(x, 33) * c1 = [T2 * (c1 << 33) + (lo(T2) >> 31) * c1] + hi(x) * 2 c1,
     // the bracket a table entry P of group 4b+2, hi(x) = hi(T2) + hi(T3)
-#if GG_K1_K2A128
     asm volatile("" ::"v"(e2.w));
-#endif
     const uint32_t hx = e2.z + t3;
-#if GG_K1_K2HI
-    // high word as v_mul_lo_u32 + v_add_u32 (the compiler otherwise builds a
-    // 64-bit addend with a v_mov and a second v_mad_u64_u32)
-    const uint64_t k2p = (uint64_t)hx * (uint32_t)(c1 << 1) + (((uint64_t)e2.y << 32) | e2.x);
-    uint32_t k2m;
-    asm("v_mul_lo_u32 %0, %1, %2" : "=v"(k2m) : "v"(hx), "s"((uint32_t)((c1 << 1) >> 32)));
-    const uint64_t k2 = ((uint64_t)((uint32_t)(k2p >> 32) + k2m) << 32) | (uint32_t)k2p;
-#else
     uint64_t k2 = (uint64_t)hx * (uint32_t)(c1 << 1) + (((uint64_t)e2.y << 32) | e2.x);
     k2 += (uint64_t)(hx * (uint32_t)((c1 << 1) >> 32)) << 32;
-#endif
     h1 ^= k1;
     h1 = rotl64<27>(h1); h1 += h2; h1 = times5_plus(h1, 0x52dce729);
     h2 ^= k2;
@@ -272,13 +200,8 @@ __device__ __forceinline__ void hash_parts(uint64_t code, const uint64_t* __rest
   h2 ^= (uint64_t)K;
   h1 += h2;
   h2 += h1;
-#if GG_K1_MULHI
   f1 = fmix64_mid(h1);  // the caller finishes with kFmixC2 (hi_times_c2 / full)
   f2 = fmix64_mid(h2);
-#else
-  f1 = fmix64_pre(h1);
-  f2 = fmix64_pre(h2);
-#endif
 }
 
 // ASCII bytes of `nbases` bases of an MSB-first code of `width` bases
@@ -370,16 +293,11 @@ __device__ __forceinline__ void insert_candidate(uint64_t* __restrict__ tab,
 constexpr uint32_t kQueue = 64;
 constexpr uint32_t kQueueDrain = 32;
 struct CandQueue {
-#if GG_K1_DEFER
   uint64_t f1[kQueue], f2[kQueue];  // fmix64_mid of h1 / h2: the exact test runs at the drain
-#else
-  uint64_t h[kQueue];
-#endif
   uint32_t slot[kQueue];
   uint32_t head, tail, claim;
 };
 
-#if GG_K1_DEFER
 __device__ __forceinline__ uint64_t exact_hash(uint64_t f1, uint64_t f2) {
   return fmix_last(f1 * kFmixC2) + fmix_last(f2 * kFmixC2);
 }
@@ -399,46 +317,6 @@ __device__ __forceinline__ void queue_push_mid(CandQueue& q, uint64_t f1, uint64
     if (hv <= tau[slot]) insert_candidate(table + ((uint64_t)slot << cap_log2), (1u << cap_log2) - 1u, flags + slot, hv);
   }
 }
-#endif
-
-#if !GG_K1_DEFER
-__device__ __forceinline__ void queue_push(CandQueue& q, uint64_t hv, uint32_t slot, uint64_t* __restrict__ table,
-                                           uint32_t cap_log2, uint32_t* __restrict__ flags) {
-  const uint32_t pos = atomicAdd(&q.tail, 1u);
-  if (pos - __atomic_load_n(&q.head, __ATOMIC_RELAXED) < kQueue) {
-    q.h[pos & (kQueue - 1)] = hv;
-    q.slot[pos & (kQueue - 1)] = slot;
-  } else {  // ring full: insert now
-    insert_candidate(table + ((uint64_t)slot << cap_log2), (1u << cap_log2) - 1u, flags + slot, hv);
-  }
-}
-#endif
-
-#if GG_K1_DEFER && GG_K1_WAVEPUSH
-// queue_push_mid for every lane of the wave whose k-mer passed (m = the
-// wave's ballot, uniform): one lane reserves the positions, each passing lane
-// takes base + its rank among them (one LDS atomic per wave instead of one
-// serialised atomic per passing lane).
-__device__ __forceinline__ void queue_push_wave(CandQueue& q, uint64_t m, bool pass, uint64_t f1, uint64_t f2,
-                                                uint32_t slot, const uint64_t* __restrict__ tau,
-                                                uint64_t* __restrict__ table, uint32_t cap_log2,
-                                                uint32_t* __restrict__ flags) {
-  const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
-  uint32_t base = 0;
-  if (__lane_id() == leader) base = atomicAdd(&q.tail, (uint32_t)__popcll(m));
-  base = __builtin_amdgcn_readlane(base, leader);
-  if (!pass) return;
-  const uint32_t pos = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  if (pos - __atomic_load_n(&q.head, __ATOMIC_RELAXED) < kQueue) {
-    q.f1[pos & (kQueue - 1)] = f1;
-    q.f2[pos & (kQueue - 1)] = f2;
-    q.slot[pos & (kQueue - 1)] = slot;
-  } else {  // ring full: finish and insert now
-    const uint64_t hv = exact_hash(f1, f2);
-    if (hv <= tau[slot]) insert_candidate(table + ((uint64_t)slot << cap_log2), (1u << cap_log2) - 1u, flags + slot, hv);
-  }
-}
-#endif
 
 // Insert the queued candidates with the lanes that are active (all of them
 // at the end of the kernel).  Positions past head + kQueue were inserted by
@@ -456,13 +334,8 @@ __device__ __forceinline__ void queue_drain(CandQueue& q, const uint64_t* __rest
     if (e >= end) break;
     const uint32_t x = e & (kQueue - 1);
     const uint32_t sl = q.slot[x];
-#if GG_K1_DEFER
     const uint64_t hv = exact_hash(q.f1[x], q.f2[x]);
     if (hv <= tau[sl]) insert_candidate(table + ((uint64_t)sl << cap_log2), cap_mask, flags + sl, hv);
-#else
-    (void)tau;
-    insert_candidate(table + ((uint64_t)sl << cap_log2), cap_mask, flags + sl, q.h[x]);
-#endif
   }
   // every active lane is past its last claim here (lockstep): reopen the ring
   __atomic_store_n(&q.head, tail, __ATOMIC_RELAXED);
@@ -594,90 +467,23 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
         const uint64_t fwd = window64<K>(F, FP, i);
         const int t0 = 64 - K - i;  // reverse complement of k-mer i starts here
         const uint64_t rev = window64<K>(R, RP, t0);
-#if GG_K1_MINHI
-        // min(fwd, rev): its high word is the smaller high word whatever the
-        // low words are; only the low word needs the 64-bit compare
-        uint32_t chi;
-        asm("v_min_u32 %0, %1, %2" : "=v"(chi) : "v"((uint32_t)(fwd >> 32)), "v"((uint32_t)(rev >> 32)));
-        const uint32_t clo = fwd < rev ? (uint32_t)fwd : (uint32_t)rev;
-        hash_parts<K>(((uint64_t)chi << 32) | clo, mtab, seed, f1[j], f2[j]);
-#else
         hash_parts<K>(fwd < rev ? fwd : rev, mtab, seed, f1[j], f2[j]);
-#endif
       }
-#if GG_K1_MULHI
       uint32_t hs[kGroup];  // S + 1 per k-mer
 #pragma unroll
       for (int j = 0; j < kGroup; ++j) hs[j] = hi_times_c2(f1[j]) + hi_times_c2(f2[j]) + 1u;
-#else
-      uint32_t hs[kGroup];
-#pragma unroll
-      for (int j = 0; j < kGroup; ++j) hs[j] = (uint32_t)(f1[j] >> 32) + (uint32_t)(f2[j] >> 32) + 1u;
-#endif
       bool any = false;
 #pragma unroll
       for (int j = 0; j < kGroup; ++j) any |= hs[j] <= thr;
       if (any) {
-#if GG_K1_QUEUE
         // (a lane of the wave has a k-mer whose high-word sum can reach
         // tau): finish the exact test for the group's k-mers and queue
         // the candidates
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
-#if GG_K1_DEFER && GG_K1_WAVEPUSH
-          const bool pass = hs[j] <= thr && (uint32_t)(g * kGroup + j) < cnt;
-          const uint64_t m = __ballot(pass);
-          if (m) queue_push_wave(q, m, pass, f1[j], f2[j], slot, a.tau, a.table, a.cap_log2, a.flags);
-#elif GG_K1_DEFER
           if (hs[j] <= thr && (uint32_t)(g * kGroup + j) < cnt)
             queue_push_mid(q, f1[j], f2[j], slot, a.tau, a.table, a.cap_log2, a.flags);
-#elif GG_K1_INNER
-          // one k-mer of the group passes in one lane, typically: the exact
-          // hash only under its own test (the wave skips the others)
-          if (hs[j] <= thr && (uint32_t)(g * kGroup + j) < cnt) {
-#if GG_K1_MULHI
-            const uint64_t hv = fmix_last(f1[j] * kFmixC2) + fmix_last(f2[j] * kFmixC2);
-#else
-            const uint64_t hv = fmix_last(f1[j]) + fmix_last(f2[j]);
-#endif
-            if (hv <= tau) queue_push(q, hv, slot, a.table, a.cap_log2, a.flags);
-          }
-#else
-#if GG_K1_MULHI
-          const uint64_t hv = fmix_last(f1[j] * kFmixC2) + fmix_last(f2[j] * kFmixC2);
-#else
-          const uint64_t hv = fmix_last(f1[j]) + fmix_last(f2[j]);
-#endif
-          if (hs[j] <= thr &&
-              (uint32_t)(g * kGroup + j) < cnt && hv <= tau)
-            queue_push(q, hv, slot, a.table, a.cap_log2, a.flags);
-#endif
         }
-#else
-        // finish the exact test per candidate k-mer and insert it now
-        uint32_t pending = 0;
-#pragma unroll
-        for (int j = 0; j < kGroup; ++j)
-          pending |= ((hs[j] <= thr) &
-                      ((uint32_t)(g * kGroup + j) < cnt)) ? (1u << j) : 0u;
-        while (pending) {
-          const int j = __builtin_ctz(pending);
-          pending &= pending - 1;
-          uint64_t a1 = f1[0], a2 = f2[0];
-#pragma unroll
-          for (int x = 1; x < kGroup; ++x) {
-            a1 = (j == x) ? f1[x] : a1;
-            a2 = (j == x) ? f2[x] : a2;
-          }
-#if GG_K1_MULHI
-          const uint64_t hv = fmix_last(a1 * kFmixC2) + fmix_last(a2 * kFmixC2);
-#else
-          const uint64_t hv = fmix_last(a1) + fmix_last(a2);
-#endif
-          if (hv <= tau)
-            insert_candidate(a.table + ((uint64_t)slot << a.cap_log2), (1u << a.cap_log2) - 1u, a.flags + slot, hv);
-        }
-#endif
       }
     }
     queue_drain(q, a.tau, a.table, a.cap_log2, a.flags, kQueueDrain);

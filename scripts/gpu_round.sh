@@ -1,46 +1,63 @@
 #!/bin/bash
-# One gpurun call: parity tests, smoke, benches.  Stops at the first crash,
-# abort or time limit (exit codes other than 0/1 from pytest, any non-zero
-# from the others); plain test failures (pytest exit 1) still let the
-# bench run so its numbers come back with the failure log.
+# One gpurun call: any sequence of stages, each under its own time limit.
+#   STAGES="tests smoke bench" OUT=r3a scripts/gpu_round.sh
+# Logs go to gpurun_out/$OUT/<stage>.log.  The call stops at the first crash,
+# abort or time limit (any non-zero exit; pytest's plain test failures, exit 1,
+# still let later stages run so their numbers come back with the failure log).
+# Stages that take extra arguments read them from the environment:
+#   BENCH_ARGS   extra bench.py arguments for bench* stages
+#   ALT_LIB      alternate libgalahgpu.so for benchalt (GALAHGPU_LIB)
+#   TESTS        pytest selection for the tests stage (default: tests -m gpu)
+#   PMC_ARGS     bench.py arguments for the pmc stage (default: one C3 step)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-STAGES="${STAGES:-tests smoke bench1k bench}"
+OUT="gpurun_out/${OUT:-run}"
+mkdir -p "$OUT"
+STAGES="${STAGES:-tests smoke bench}"
 run() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
   echo "== $name ($(date +%T))"
-  timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
   echo "== $name rc=$rc"
-  tail -n 5 "gpurun_out/$name.log"
+  tail -n 4 "$OUT/$name.log"
   return $rc
+}
+bench() {  # name limit args...
+  local name=$1 lim=$2; shift 2
+  run "$name" "$lim" python3 -u bench.py "$@" $BENCH_ARGS || exit $?
+  tail -n 1 "$OUT/$name.log" > "$OUT/$name.json"
 }
 for st in $STAGES; do
   case $st in
     tests)
-      run gpu_tests 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread
+      run gpu_tests 900 python3 -u -m pytest ${TESTS:-tests -m gpu} -v --timeout 300 --timeout-method thread
       rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     smoke)
-      run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
-    bench1k)
-      run bench_1k 300 python -u bench.py --genomes 1000 --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
-    bench)
-      run bench 600 python -u bench.py --steps 3 --warmup 1 || exit $? ;;
-    benchalt)  # same bench against an alternate build (GALAHGPU_LIB)
-      GALAHGPU_LIB="${ALT_LIB:?}" run bench_alt 600 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
-    bench2r)
-      run bench_2rank_gloo 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 2 --warmup 1 --genomes 2000 --dist-backend gloo || exit $? ;;
-    k2)
-      run k2_probe 300 python -u scripts/k2_probe.py || exit $? ;;
-    pmc_k2)
-      run pmc_k2 900 bash scripts/pmc.sh gpurun_out/pmc_k2 pairs_table -- python3 -u scripts/k2_probe.py --reps 1 || exit $? ;;
-    pmc_k1)
-      run pmc_k1 900 bash scripts/pmc.sh gpurun_out/pmc_k1 sketch_candidates -- python3 -u scripts/k2_probe.py --reps 1 || exit $? ;;
-    counters)
-      run counters 120 rocprofv3 -L || exit $? ;;
-    prof)
-      run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $? ;;
+      run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
+    bench)       bench bench_c3 600 --steps 20 --warmup 5 ;;
+    bench_nocpu) bench bench_c3 300 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    bench_c2)    bench bench_c2 300 --config c2 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    bench_c4)    bench bench_c4 600 --config c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
+    bench_c5)    bench bench_c5 300 --config c5 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    bench_files) bench bench_files 600 --files --steps 3 --warmup 1 --no-cpu-baseline ;;
+    benchalt)  # the C3 and C5 benches against an alternate build
+      GALAHGPU_LIB="${ALT_LIB:?}" bench bench_alt_c3 300 --steps 20 --warmup 5 --no-cpu-baseline
+      GALAHGPU_LIB="${ALT_LIB:?}" bench bench_alt_c5 300 --config c5 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    bench2r)  # the driver's launch shape on one GPU (two members of GPU 0)
+      run bench_2rank 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29511 bench.py --gpus 2 --devices 0,0 --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
+    prof)  # kernel trace + stats of the C3 bench (per-kernel averages for profiles/)
+      run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c3 -- \
+        python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $? ;;
+    prof_c5)
+      run prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c5 -- \
+        python3 -u bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
+    pmc)  # PMC passes at HEAD (scripts/pmc_head.sh)
+      run pmc 900 bash scripts/pmc_head.sh "$OUT/pmc" ${PMC_ARGS:-} || exit $? ;;
+    ubench)
+      run ubench 300 ./scripts/ubench_dual || exit $? ;;
+    *) echo "unknown stage $st"; exit 2 ;;
   esac
 done
 exit 0

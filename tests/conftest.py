@@ -17,6 +17,19 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device")
 
 
+# The default paths at the BASELINE configs and the multi-device path run
+# first, so that a GPU run cut short (pytest -x, a box lost mid-run) still
+# carries evidence for them; the rest keeps its file order.
+_FIRST = ("test_full_size.py", "test_multi_device.py")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    def rank(item):
+        name = os.path.basename(str(item.fspath))
+        return _FIRST.index(name) if name in _FIRST else len(_FIRST)
+    items[:] = [it for _, it in sorted(enumerate(items), key=lambda p: (rank(p[1]), p[0]))]
+
+
 def golden_names():
     with np.load(os.path.join(GOLD, "sketches_k21_s1000.npz")) as z:
         return [str(x) for x in z["names"]]

@@ -426,6 +426,14 @@ def test_index_kernel_many_partners_and_long_runs(monkeypatch):
             monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", kern)
             with ga.Context(k=21, sketch_size=s) as ctx:
                 assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, (thr, kern)
+        # row 0's partners still overflowing the map at the last split: the
+        # index launch's output is dropped and the gate kernel runs instead
+        monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
+        for split in ("0", "1"):
+            monkeypatch.setenv("GALAHGPU_INDEX_MAX_SPLIT", split)
+            with ga.Context(k=21, sketch_size=s) as ctx:
+                assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, (thr, split)
+        monkeypatch.delenv("GALAHGPU_INDEX_MAX_SPLIT")
     # 5,000 sketches that all hold one hash: a run of 5,000 > the run limit
     n = 5000
     s = 40
@@ -491,6 +499,69 @@ def test_many_runs_index_and_run_table_errors(gpu_ctx):
     for r, msg in bad:
         with pytest.raises(ga.GalahGpuError, match=msg):
             gpu_ctx.sketch_device(d_words, r, n_genomes, d_out, d_lens)
+
+
+class HostPacked:
+    """A caller-built gg_packed (host words + run table) for Context.sketch."""
+
+    def __init__(self, words, runs, n_genomes):
+        self.words = np.ascontiguousarray(words, dtype=np.uint32)
+        self.runs = np.ascontiguousarray(runs, dtype=ga.RUN_DTYPE)
+        self.kmers = np.zeros(max(n_genomes, 1), np.uint64)
+        p = ga._Packed()
+        p.words = self.words.ctypes.data_as(ga.ctypes.POINTER(ga.ctypes.c_uint32))
+        p.n_words = len(self.words)
+        p.n_bases = len(self.words) * 16
+        p.runs = self.runs.ctypes.data_as(ga.ctypes.POINTER(ga._Run))
+        p.n_runs = len(self.runs)
+        p.n_genomes = n_genomes
+        p.genome_kmers = self.kmers.ctypes.data_as(ga.ctypes.POINTER(ga.ctypes.c_uint64))
+        self._struct = p
+        self._p = ga.ctypes.pointer(p)
+        self.n_genomes = n_genomes
+
+
+def test_host_sketch_run_table_checked_before_split():
+    """gg_sketch (host buffers) splits the run table by genome among the
+    members before K1 sees it: every bad table fails with the run-table error
+    on 1 and 2 members, and a valid table whose bases do not rise with the
+    genome (genome 0 packed after genome 1) gives the oracle's sketches."""
+    rng = np.random.default_rng(78)
+    n_words = 1 << 14
+    words = rng.integers(0, 2**32, n_words, dtype=np.uint64).astype(np.uint32)
+    n_genomes = 6
+    runs = np.zeros(12, ga.RUN_DTYPE)
+    runs["genome"] = np.repeat(np.arange(n_genomes), 2)
+    runs["len"] = rng.integers(21, 5000, 12)
+    # genome g's two runs inside block (n_genomes - 1 - g): bases fall as g rises
+    blk = n_words * 16 // n_genomes
+    for r in range(12):
+        g = r // 2
+        runs["base"][r] = (n_genomes - 1 - g) * blk + (r % 2) * 6000
+    bad = []
+    r1 = runs.copy()
+    r1["genome"][3] = n_genomes + 5
+    bad.append((r1, "non-decreasing genome"))
+    r2 = runs.copy()
+    r2["genome"][4], r2["genome"][5] = 3, 1
+    bad.append((r2, "non-decreasing genome"))
+    r3 = runs.copy()
+    r3["len"][7] = 20
+    bad.append((r3, "shorter than k"))
+    r4 = runs.copy()
+    r4["base"][11] = n_words * 16 - 10
+    bad.append((r4, "past the packed words"))
+    for devs in ([0], [0, 0]):
+        with ga.Context(k=21, sketch_size=1000, devices=devs) as ctx:
+            for r, msg in bad:
+                with pytest.raises(ga.GalahGpuError, match=msg):
+                    ctx.sketch(HostPacked(words, r, n_genomes))
+            sk, lens = ctx.sketch(HostPacked(words, runs, n_genomes))
+            for g in range(n_genomes):
+                sel = runs[runs["genome"] == g]
+                recs = [unpack_run(words, int(x["base"]), int(x["len"])) for x in sel]
+                exp = oracle.sketch_records(recs)
+                assert lens[g] == len(exp) and (sk[g][:lens[g]] == exp).all(), (devs, g)
 
 
 @pytest.mark.parametrize("top", [2**50, 2**64 - 1, 2**31])

@@ -82,6 +82,11 @@ def test_precluster_shards_2k_synthetic_1_2_3_devices():
                 shards.append((d_words, runs, g1 - g0))
                 keep.append(d_words)
             pairs, ani = ctx.precluster_shards(shards, thr)
+            if M > 1:
+                # every member copied the other members' rows with
+                # hipMemcpyPeerAsync (multi.cpp replicate: the node's call,
+                # here with src == dst device)
+                assert ctx.phase_times()["replicate"] > 0
             # at 90% nearly every within-cluster pair passes (> 4096: the
             # host merge's radix sort)
             p90, a90 = ctx.precluster_shards(shards, ga.parse_percentage(90))
