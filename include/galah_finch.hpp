@@ -12,11 +12,13 @@
 // src/finch.rs:50); here the same message is thrown as std::runtime_error.
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
 #include <map>
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -69,37 +71,70 @@ inline float parse_percentage(float value) {
   return out;
 }
 
-// src/finch.rs:26-75 on the GPU: sketch (K1), all pairs (K2), keep ani >= min_ani.
-// devices: HIP ordinals (empty: every visible GPU, or GALAHGPU_DEVICES, as
-// galah's one distances() call would use them); threads: galah's --threads
-// for file ingest (<= 0: the process's CPUs).
-inline SortedPairGenomeDistanceCache finch_distances(const std::vector<std::string>& paths,
-                                                     float min_ani, size_t num_kmers,
-                                                     uint8_t kmer_length, const std::vector<int>& devices = {},
-                                                     int threads = 0) {
-  gg_status st = GG_OK;
-  gg_ctx* ctx = gg_create_multi(kmer_length, (uint32_t)num_kmers, 0, devices.empty() ? nullptr : devices.data(),
-                                (uint32_t)devices.size(), &st);
+// rayon's global pool, which galah builds with --threads threads
+// (CAP:408-412, default 1); finch_distances reads its size the way the Rust
+// body in INTEGRATION.md calls rayon::current_num_threads().  0 = unset: the
+// machine's CPUs, rayon's own default.
+inline int& rayon_pool_slot() {
+  static int n = 0;
+  return n;
+}
+inline void set_num_threads(int n) { rayon_pool_slot() = n > 0 ? n : 0; }
+inline int current_num_threads() {
+  const int n = rayon_pool_slot();
+  return n > 0 ? n : (int)std::max(1u, std::thread::hardware_concurrency());
+}
+
+namespace detail {
+// sketch + all pairs + threshold on an existing context; takes ownership of ctx
+inline SortedPairGenomeDistanceCache distances_on(gg_ctx* ctx, const std::vector<std::string>& paths, float min_ani) {
   if (!ctx)
     throw std::runtime_error(std::string("Failed to sketch genomes with finch: ") + gg_thread_last_error());
-  if (threads > 0) gg_set_host_threads(ctx, threads);
+  gg_set_host_threads(ctx, current_num_threads());
   std::vector<const char*> c_paths;
   for (const auto& p : paths) c_paths.push_back(p.c_str());
   gg_pair* pairs = nullptr;
   float* ani = nullptr;
   uint64_t n = 0;
-  st = gg_precluster_files(ctx, c_paths.data(), (uint32_t)c_paths.size(), min_ani, &pairs, &ani, &n);
+  const gg_status st = gg_precluster_files(ctx, c_paths.data(), (uint32_t)c_paths.size(), min_ani, &pairs, &ani, &n);
   if (st != GG_OK) {
     std::string msg = gg_last_error(ctx);
     gg_destroy(ctx);
-    throw std::runtime_error("Failed to sketch genomes with finch: " + msg);
+    throw std::runtime_error("Failed to sketch genomes with finch: " + msg);  // src/finch.rs:50
   }
   SortedPairGenomeDistanceCache cache;
-  for (uint64_t i = 0; i < n; ++i) cache.insert({pairs[i].i, pairs[i].j}, ani[i]);
+  for (uint64_t i = 0; i < n; ++i) cache.insert({pairs[i].i, pairs[i].j}, ani[i]);  // src/finch.rs:70
   gg_free(pairs);
   gg_free(ani);
   gg_destroy(ctx);
   return cache;
+}
+}  // namespace detail
+
+// src/finch.rs:26-75 on the GPU, same arguments: sketch (K1), all pairs (K2),
+// keep ani >= min_ani.  Every visible GPU (or GALAHGPU_DEVICES), as galah's
+// one distances() call would use them; file ingest on current_num_threads().
+inline SortedPairGenomeDistanceCache finch_distances(const std::vector<std::string>& paths, float min_ani,
+                                                     size_t num_kmers, uint8_t kmer_length) {
+  gg_status st = GG_OK;
+  return detail::distances_on(gg_create_multi(kmer_length, (uint32_t)num_kmers, 0, nullptr, 0, &st), paths, min_ani);
+}
+
+// The same on one HIP device (ordinal; -1 = the current device).
+inline SortedPairGenomeDistanceCache finch_distances(const std::vector<std::string>& paths, float min_ani,
+                                                     size_t num_kmers, uint8_t kmer_length, int device) {
+  gg_status st = GG_OK;
+  return detail::distances_on(gg_create(kmer_length, (uint32_t)num_kmers, 0, device, &st), paths, min_ani);
+}
+
+// The same on a list of HIP ordinals (repeats allowed: several members on one GPU).
+inline SortedPairGenomeDistanceCache finch_distances_on(const std::vector<int>& devices,
+                                                        const std::vector<std::string>& paths, float min_ani,
+                                                        size_t num_kmers, uint8_t kmer_length) {
+  gg_status st = GG_OK;
+  return detail::distances_on(
+      gg_create_multi(kmer_length, (uint32_t)num_kmers, 0, devices.data(), (uint32_t)devices.size(), &st), paths,
+      min_ani);
 }
 
 // src/finch.rs:4-24

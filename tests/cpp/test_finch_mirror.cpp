@@ -53,6 +53,10 @@ static void test_parse_percentage() {
 
 static void test_hello_world(const std::string& dir) {
   const std::vector<std::string> paths = {dir + "/set1/1mbp.fna.gz", dir + "/set1/500kb.fna.gz"};
+  // galah builds rayon's global pool from --threads before clustering
+  // (CAP:408-412); distances() reads its size
+  galah::set_num_threads(2);
+  CHECK(galah::current_num_threads() == 2);
   galah::FinchPreclusterer p(0.9f, 1000, 21);
   CHECK(std::strcmp(p.method_name(), "finch") == 0);
   auto d1 = p.distances(paths);
@@ -61,6 +65,10 @@ static void test_hello_world(const std::string& dir) {
   CHECK(d1 == e1);
   auto d2 = galah::finch_distances(paths, 0.99f, 1000, 21);
   CHECK(d2.size() == 0);
+  // one device by ordinal, and two members of device 0
+  CHECK(galah::finch_distances(paths, 0.9f, 1000, 21, 0) == e1);
+  CHECK(galah::finch_distances_on({0, 0}, paths, 0.9f, 1000, 21) == e1);
+  galah::set_num_threads(0);
   bool threw = false;
   try {
     galah::finch_distances({dir + "/does_not_exist.fna"}, 0.9f, 1000, 21);
