@@ -79,6 +79,11 @@ def parse():
                     help="lib mode: comma-separated HIP ordinals (repeats allowed, e.g. 0,0 to run the sharded "
                          "path on one GPU); default: 0..gpus-1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--files", dest="files", action="store_true", default=None,
+                    help="add the ingest-inclusive leg (C2's genomes as gzip FASTA files through "
+                         "gg_precluster_files); on by default for the one-GPU C3 headline")
+    ap.add_argument("--no-files", dest="files", action="store_false")
+    ap.add_argument("--files-genomes", type=int, default=1000, help="genomes in the files leg (C2: 1000)")
     ap.add_argument("--cpu-budget-s", type=float, default=24.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="dist mode: gloo stages collectives through host memory (ranks sharing one GPU)")
@@ -160,18 +165,26 @@ def roofline(kst_sk, kst_pr, s, config_note, config=None):
     k1["hbm_frac"] = k1["hbm_achieved_GBps"] / HBM_PEAK_GBS
     if model:
         fp = k1_fingerprint()
-        k1["peak"] = model["peak_gkmer_per_s"]
         k1["peak_model"] = model["note"]
         k1["valu_per_wave_kmer"] = model["valu_per_wave_kmer"]
         k1["floor_cycles_per_wave_kmer"] = model["floor_cycles_per_wave_kmer"]
         k1["traffic_bytes_per_kmer_pmc"] = model.get("hbm_bytes_per_kmer_pmc")
         k1["peak_stale"] = (fp is None or fp != model.get("k1_fingerprint"))
-        k1["frac"] = k1_gkmer / model["peak_gkmer_per_s"]
-        # the same instructions if every one of them dual-issued (2.3 cycles,
-        # MI355X_MICROARCH.md's "2 cycles per wave64 VALU"): the headroom a
-        # cheaper instruction mix could reach
-        all_dual = N_SIMD * CLK_GHZ * 64 / (model["valu_per_wave_kmer"] * model["class_cost_cycles"]["dual"])
-        k1["frac_vs_all_dual_issue"] = k1_gkmer / all_dual
+        # three fractions of one kernel:
+        #  frac_vs_guide_valu  K1's VALU instructions at MI355X_MICROARCH.md's
+        #                      "2 cycles per wave64 VALU" (:54, :473): the
+        #                      headline fraction
+        #  frac_issue_model    the same instructions at the issue cost of
+        #                      their class measured on this chip (2.3 / 4.2 /
+        #                      5.0 cycles, scripts/ubench_dual.hip)
+        #  hbm_frac            0.25 B per k-mer against 8 TB/s
+        guide = N_SIMD * CLK_GHZ * 64 / (model["valu_per_wave_kmer"] * 2.0)
+        k1["peak_guide_valu"] = guide
+        k1["frac_vs_guide_valu"] = k1_gkmer / guide
+        k1["peak_issue_model"] = model["peak_gkmer_per_s"]
+        k1["frac_issue_model"] = k1_gkmer / model["peak_gkmer_per_s"]
+        k1["peak"] = guide
+        k1["frac"] = k1["frac_vs_guide_valu"]
     k2 = {"kernel": "K2: index_pairs_kernel (+ fill, radix sort, runs) or pairs_gate_kernel", "unit": "Gpair/s",
           "achieved": pairs / (pr_ms * 1e-3) / 1e9 if pr_ms > 0 else 0.0, "avg_ms": pr_ms, "work_per_launch": pairs,
           "merge_priced_GBps": pairs * 16.0 * s / (pr_ms * 1e-3) / 1e9 if pr_ms > 0 else 0.0,
@@ -185,15 +198,19 @@ def roofline(kst_sk, kst_pr, s, config_note, config=None):
     roof = {"bound": dom.get("bound", "valu"), "achieved": round(dom["achieved"], 3),
             "peak": round(dom.get("peak", 0.0), 3), "unit": dom["unit"],
             "frac": round(dom.get("frac", 0.0), 4),
+            "frac_vs_guide_valu": round(dom["frac_vs_guide_valu"], 4) if "frac_vs_guide_valu" in dom else None,
+            "frac_issue_model": round(dom["frac_issue_model"], 4) if "frac_issue_model" in dom else None,
+            "hbm_frac": round(dom["hbm_frac"], 4) if "hbm_frac" in dom else None,
             "traffic": (round(2 * model["hbm_bytes_per_kmer_pmc"] * kmers) if (model and dom is k1
                         and model.get("hbm_bytes_per_kmer_pmc")) else None),
             "kernel": dom["kernel"], "avg_launch_ms": round(dom["avg_ms"], 4),
-            "note": ("K1 is bound by VALU issue: peak = 1024 SIMDs x %.1f GHz x 64 k-mers / floor cycles per wave of "
-                     "64 k-mers; floor = K1's VALU instructions per wave-k-mer (PMC at HEAD) at the issue cost of "
-                     "their class measured on this chip (dual-issued simple ops ~2.3 cycles, others ~4.2, 64-bit "
-                     "~5.0; profiles/r02_k1_issue_model.json); traffic = HBM bytes per launch from the PMC pass: "
-                     "FETCH_SIZE x 2 (the gfx950 factor, calibrated for 4-, 8- and 16-B loads by "
-                     "scripts/ubench_fetch.hip: profiles/r02_pmc_head/fetch) per k-mer x k-mers; %s"
+            "note": ("K1 is bound by VALU issue, not HBM (hbm_frac: 0.25 B per k-mer at 8 TB/s). peak = 1024 SIMDs x "
+                     "%.1f GHz x 64 k-mers / (K1's VALU instructions per wave-k-mer, PMC at HEAD, x 2 cycles: "
+                     "MI355X_MICROARCH.md's wave64 VALU issue); frac_issue_model prices the same instructions at the "
+                     "issue cost of their class measured on this chip (simple 32-bit ~2.3 cycles, other 32-bit ~4.2, "
+                     "64-bit ~5.0; profiles/r02_k1_issue_model.json, DESIGN §4); traffic = HBM bytes per launch "
+                     "from the PMC pass: FETCH_SIZE x 2 (the gfx950 factor, calibrated for 4-, 8- and 16-B loads by "
+                     "scripts/ubench_fetch.hip) per k-mer x k-mers; %s"
                      % (CLK_GHZ, config_note)),
             "kernels": [{kk: (round(v, 5) if isinstance(v, float) else v) for kk, v in x.items()} for x in (k1, k2)]}
     return roof
@@ -278,6 +295,92 @@ def cpu_baseline(sample_words, glen, sk_all, lens_all, k, s, min_ani, n_total, b
         "pair_rate_all_cores": pair_rate_all,
         "value_all_core_pairs": npairs / t_total_all,
     }
+
+
+# ---------------------------------------------------------------------------
+# ingest-inclusive leg: real gzip FASTA files through gg_precluster_files
+# ---------------------------------------------------------------------------
+def files_leg(a, device, steps):
+    """C2's genomes (1k x 3 Mbp, clusters of 10) written as gzip FASTA (80
+    columns, level 6) to local disk OUTSIDE the timed region, then
+    gg_precluster_files over the paths (what galah's distances() calls:
+    src/finch.rs:47-73) timed end to end: read + gunzip + parse + 2-bit pack
+    on the host threads, H2D, K1, K2, merge.  Files are in the page cache
+    (written just before).  Beside it: pure read + libdeflate gunzip of the
+    same files on the same threads (scripts/gunzip_probe), the floor any
+    host ingest of these files sits on."""
+    import concurrent.futures as cf
+    import shutil
+    import tempfile
+    import zlib
+
+    n, glen, T = a.files_genomes, 3000000, cpu_threads()
+    out = {"workload": "C2: %d synthetic genomes x %d bp as gzip FASTA (80 columns, zlib level 6), "
+                       "k=21, s=1000, min_ani=%s" % (n, glen, float(ga.parse_percentage(a.min_ani))),
+           "host_threads": T}
+    d = tempfile.mkdtemp(prefix="gg_files_", dir=os.environ.get("TMPDIR") or "/tmp")
+    try:
+        t0 = time.perf_counter()
+        with ga.Context(k=21, sketch_size=1000, seed=0, device=device) as ctx:
+            d_words = torch.empty(n * glen // 16, dtype=torch.int32, device="cuda:%d" % device)
+            ctx.synth_device(n, glen, a.cluster, a.max_sub, a.seed, d_words)
+            torch.cuda.synchronize(device)
+            words = d_words.cpu().numpy().view(np.uint32)
+            del d_words
+        acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+        shifts = (np.uint32(30) - 2 * np.arange(16, dtype=np.uint32))[None, :]
+        nl = np.full((glen // 80, 1), ord("\n"), np.uint8)
+
+        def write(g):
+            w = words[g * glen // 16:(g + 1) * glen // 16]
+            seq = acgt[((w[:, None] >> shifts) & np.uint32(3)).reshape(-1)]
+            body = np.concatenate([seq[: glen // 80 * 80].reshape(-1, 80), nl], axis=1).tobytes()
+            text = b">genome_%d synthetic C2\n" % g + body + (bytes(seq[glen // 80 * 80:]) + b"\n" if glen % 80 else b"")
+            c = zlib.compressobj(6, zlib.DEFLATED, 31)
+            p = os.path.join(d, "g%05d.fna.gz" % g)
+            with open(p, "wb") as f:
+                f.write(c.compress(text) + c.flush())
+            return p
+
+        with cf.ThreadPoolExecutor(T) as ex:
+            paths = list(ex.map(write, range(n)))
+        del words
+        out["write_s"] = round(time.perf_counter() - t0, 2)
+        out["gz_bytes"] = int(sum(os.path.getsize(p) for p in paths))
+        print("[bench] files leg: wrote %d gzip FASTA files (%.2f GB) in %.1f s" % (n, out["gz_bytes"] / 1e9,
+              out["write_s"]), file=sys.stderr, flush=True)
+        thr = ga.parse_percentage(a.min_ani)
+        with ga.Context(k=21, sketch_size=1000, seed=0, device=device, host_threads=T) as ctx:
+            ctx.precluster_files(paths[:16], thr)  # warm-up (device, library, threads)
+            times, found, ph = [], 0, {p: 0.0 for p in ga.PHASES}
+            for _ in range(max(1, steps)):
+                t1 = time.perf_counter()
+                pairs, _ani = ctx.precluster_files(paths, thr)
+                times.append(time.perf_counter() - t1)
+                found = len(pairs)
+                for p, v in ctx.phase_times().items():
+                    ph[p] += v
+        t = float(np.median(times))
+        bases = n * glen
+        out.update({"steps": len(times), "s_per_call_median": round(t, 4), "s_per_call": [round(x, 4) for x in times],
+                    "gbases_per_s": round(bases / t / 1e9, 3), "genome_pairs_per_s": round(n * (n - 1) / 2 / t, 1),
+                    "pairs_found": int(found),
+                    "phase_ms": {p: round(v / len(times), 2) for p, v in ph.items()}})
+        probe = os.path.join(ROOT, "scripts", "gunzip_probe")
+        if os.path.exists(probe):
+            r = subprocess.run([probe, str(T)] + paths, capture_output=True, text=True, timeout=300)
+            if r.returncode == 0:
+                dec = json.loads(r.stdout.strip().splitlines()[-1])
+                out["pure_decode_s"] = dec["decode_s"]
+                out["pure_decode_gbases_per_s"] = round(bases / dec["decode_s"] / 1e9, 3)
+                out["ratio_to_pure_decode"] = round(t / dec["decode_s"], 3)
+            else:
+                out["pure_decode_error"] = r.stderr[-300:]
+        out["note"] = ("kernel-only headline vs this: the same path from gzip files on %d host threads; galah's "
+                       "distances() starts from these paths (src/finch.rs:47)" % T)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -367,6 +470,14 @@ def run_lib(a, world, rank):
             sample = d_words[: n_sample * a.genome_len // 16].cpu().numpy().view(np.uint32)
             cpu = cpu_baseline(sample, a.genome_len, d_sk.cpu().numpy().view(np.uint64),
                                d_len.cpu().numpy().view(np.uint32), a.k, s, min_ani, N, a.cpu_budget_s)
+            del d_sk, d_len
+        files = None
+        want_files = a.files if a.files is not None else (a.config == "c3")
+        if world == 1 and M == 1 and want_files:
+            try:
+                files = files_leg(a, devs[0], 3)
+            except Exception as e:  # the headline stands without it
+                files = {"error": "%s: %s" % (type(e).__name__, e)}
         line = {
             "metric": "precluster genome-pairs/sec at 10k genomes (s=1000) + sketch Gbases/s",
             "value": round(npairs / (elapsed_max / a.steps), 1), "unit": "genome-pairs/s", "n_gpus": n_dev,
@@ -383,6 +494,7 @@ def run_lib(a, world, rank):
             "roofline": roof,
             "cpu_baseline": cpu,
             "downstream": downstream,
+            "files": files,
         }
         ctx.close()
     if world > 1:
