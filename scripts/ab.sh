@@ -10,9 +10,9 @@ GALAHGPU_LIB=$ALT timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --tim
 tail -2 gpurun_out/ab_tests.log
 for r in 1 2; do
   echo "== bench A"
-  timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab_a$r.log 2>&1 || exit 1
+  timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-files > gpurun_out/ab_a$r.log 2>&1 || exit 1
   python -c "import json,sys; d=json.loads(open('gpurun_out/ab_a$r.log').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['phase_ms'], d['roofline']['kernels'][0]['avg_ms'], d['roofline']['kernels'][1]['avg_ms'])"
   echo "== bench B"
-  GALAHGPU_LIB=$ALT timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab_b$r.log 2>&1 || exit 1
+  GALAHGPU_LIB=$ALT timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-files > gpurun_out/ab_b$r.log 2>&1 || exit 1
   python -c "import json,sys; d=json.loads(open('gpurun_out/ab_b$r.log').read().strip().splitlines()[-1]); print(d['ms_per_step'], d['phase_ms'], d['roofline']['kernels'][0]['avg_ms'], d['roofline']['kernels'][1]['avg_ms'])"
 done

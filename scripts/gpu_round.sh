@@ -5,7 +5,7 @@
 # abort or time limit (any non-zero exit; pytest's plain test failures, exit 1,
 # still let later stages run so their numbers come back with the failure log).
 # Stages that take extra arguments read them from the environment:
-#   BENCH_ARGS   extra bench.py arguments for bench* stages
+#   BENCH_ARGS   extra bench.py arguments for bench* stages (the C3 stage runs the files leg unless --no-files)
 #   ALT_LIB      alternate libgalahgpu.so for benchalt (GALAHGPU_LIB)
 #   TESTS        pytest selection for the tests stage (default: tests -m gpu)
 #   PMC_ARGS     bench.py arguments for the pmc stage (default: one C3 step)
@@ -36,7 +36,7 @@ for st in $STAGES; do
     smoke)
       run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)       bench bench_c3 600 --steps 20 --warmup 5 ;;
-    bench_nocpu) bench bench_c3 300 --steps 20 --warmup 5 --no-cpu-baseline ;;
+    bench_nocpu) bench bench_c3 300 --steps 20 --warmup 5 --no-cpu-baseline --no-files ;;
     bench_c2)    bench bench_c2 300 --config c2 --steps 10 --warmup 2 --no-cpu-baseline ;;
     bench_c4)    bench bench_c4 600 --config c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench_c5)    bench bench_c5 300 --config c5 --steps 10 --warmup 2 --no-cpu-baseline ;;
@@ -49,7 +49,7 @@ for st in $STAGES; do
         --master-port 29511 bench.py --gpus 2 --devices 0,0 --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
     prof)  # kernel trace + stats of the C3 bench (per-kernel averages for profiles/)
       run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c3 -- \
-        python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline || exit $? ;;
+        python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-files || exit $? ;;
     prof_c5)
       run prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c5 -- \
         python3 -u bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;

@@ -17,7 +17,7 @@ i=0
 for s in "${sets[@]}"; do
   i=$((i+1))
   echo "== pmc pass $i: $s"
-  timeout -s KILL 240 rocprofv3 --pmc $s --kernel-include-regex "$rx" --output-format csv -d "$out/p$i" -o p$i -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline "$@" > "$out/p$i.log" 2>&1
+  timeout -s KILL 240 rocprofv3 --pmc $s --kernel-include-regex "$rx" --output-format csv -d "$out/p$i" -o p$i -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-files "$@" > "$out/p$i.log" 2>&1
   rc=$?
   echo "rc=$rc"; tail -n 1 "$out/p$i.log"
   [ $rc -eq 0 ] || exit $rc
