@@ -210,75 +210,18 @@ void parallel_chunks(uint64_t n, int T, F&& f) {
   for (auto& x : th) x.join();
 }
 
-// One parallel pass over the caller's run table: checks it (grouped by
-// non-decreasing genome < n_genomes, every run >= k bases and inside the
-// packed words), and lays out what K1 needs: the first run of every genome,
-// every genome's k-mer count (for its initial tau) and the start of every
-// run's K1 segments (ceil(k-mers / seg) per run, exclusive prefix; entry
-// n_runs = the total).  C5's 3.6M runs: 11 ms in four serial loops before.
-struct RunIndex {
-  std::vector<uint64_t> gr;  // [n_genomes + 1]
-  std::vector<uint64_t> nk;  // [n_genomes]
-  std::vector<uint64_t> rs;  // [n_runs + 1]
-};
-
-gg_status index_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t n_genomes, uint64_t n_words,
-                     uint32_t seg, RunIndex& ix) {
-  const int T = n_runs >= (1u << 18) ? std::max(1, std::min(16, ingest_threads(c->host_threads))) : 1;
-  const uint32_t k = (uint32_t)c->k;
-  ix.gr.assign((size_t)n_genomes + 1, ~0ull);
-  ix.rs.resize(n_runs + 1);
-  std::vector<uint64_t> bad(T, ~0ull), csum(T, 0);
-  parallel_chunks(n_runs, T, [&](int t, uint64_t b, uint64_t e) {
-    uint64_t segs = 0;
-    for (uint64_t r = b; r < e; ++r) {
-      const gg_run& x = runs[r];
-      const uint32_t prev = r ? runs[r - 1].genome : 0u;
-      if (x.genome >= n_genomes || x.genome < prev || x.len < k || x.base + x.len > n_words * 16ull) {
-        bad[t] = r;
-        return;
-      }
-      if (r == 0 || x.genome != prev) ix.gr[x.genome] = r;
-      ix.rs[r] = (x.len - k + 1 + seg - 1) / seg;
-      segs += ix.rs[r];
-    }
-    csum[t] = segs;
-  });
-  const uint64_t first_bad = *std::min_element(bad.begin(), bad.end());
-  if (first_bad != ~0ull) {
-    const gg_run& x = runs[first_bad];
-    const uint32_t prev = first_bad ? runs[first_bad - 1].genome : 0u;
-    if (x.genome >= n_genomes || x.genome < prev)
-      return fail(c, GG_ERR_INVALID_ARG, "runs must be grouped by non-decreasing genome < n_genomes");
-    if (x.len < k) return fail(c, GG_ERR_INVALID_ARG, "run shorter than k");
-    return fail(c, GG_ERR_INVALID_ARG, "run extends past the packed words");
-  }
-  ix.gr[n_genomes] = n_runs;
-  for (uint32_t g = n_genomes; g-- > 0;)  // genomes without runs start where the next one does
-    if (ix.gr[g] == ~0ull) ix.gr[g] = ix.gr[g + 1];
-  std::vector<uint64_t> coff(T + 1, 0);
-  for (int t = 0; t < T; ++t) coff[t + 1] = coff[t] + csum[t];
-  ix.rs[n_runs] = coff[T];
-  ix.nk.assign(n_genomes, 0);
-  // segment starts (prefix within each run chunk) and k-mers per genome are
-  // independent: one team of threads does both
-  parallel_chunks((uint64_t)T, T, [&](int t, uint64_t, uint64_t) {
-    uint64_t acc = coff[t];
-    for (uint64_t r = n_runs * t / T, e = n_runs * (t + 1) / T; r < e; ++r) {
-      const uint64_t v = ix.rs[r];
-      ix.rs[r] = acc;
-      acc += v;
-    }
-    for (uint64_t g = (uint64_t)n_genomes * t / T, e = (uint64_t)n_genomes * (t + 1) / T; g < e; ++g) {
-      uint64_t nk = 0;
-      for (uint64_t r = ix.gr[g]; r < ix.gr[g + 1]; ++r) nk += runs[r].len - k + 1;
-      ix.nk[g] = nk;
-    }
-  });
-  return GG_OK;
-}
-
 }  // namespace
+
+// The status and message for the first bad run of a table (check_runs, and
+// the device check in sketch_core).
+gg_status run_error(gg_ctx* c, const gg_run* runs, uint64_t first_bad, uint32_t n_genomes) {
+  const gg_run& x = runs[first_bad];
+  const uint32_t prev = first_bad ? runs[first_bad - 1].genome : 0u;
+  if (x.genome >= n_genomes || x.genome < prev)
+    return fail(c, GG_ERR_INVALID_ARG, "runs must be grouped by non-decreasing genome < n_genomes");
+  if (x.len < (uint32_t)c->k) return fail(c, GG_ERR_INVALID_ARG, "run shorter than k");
+  return fail(c, GG_ERR_INVALID_ARG, "run extends past the packed words");
+}
 
 gg_status check_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t n_genomes, uint64_t n_words) {
   if (n_runs && !runs) return fail(c, GG_ERR_INVALID_ARG, "null run table");
@@ -298,12 +241,7 @@ gg_status check_runs(gg_ctx* c, const gg_run* runs, uint64_t n_runs, uint32_t n_
   });
   const uint64_t first_bad = *std::min_element(bad.begin(), bad.end());
   if (first_bad == ~0ull) return GG_OK;
-  const gg_run& x = runs[first_bad];
-  const uint32_t prev = first_bad ? runs[first_bad - 1].genome : 0u;
-  if (x.genome >= n_genomes || x.genome < prev)
-    return fail(c, GG_ERR_INVALID_ARG, "runs must be grouped by non-decreasing genome < n_genomes");
-  if (x.len < k) return fail(c, GG_ERR_INVALID_ARG, "run shorter than k");
-  return fail(c, GG_ERR_INVALID_ARG, "run extends past the packed words");
+  return run_error(c, runs, first_bad, n_genomes);
 }
 
 // GALAHGPU_HOST_PROFILE=1: per-stage host wall times of sketch_core on stderr
@@ -328,16 +266,12 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
     return GG_OK;
   }
   const uint32_t seg = (uint32_t)sketch_segment_len(c->k);
-  RunIndex ix;
-  gg_status vs = index_runs(c, runs, n_runs, n_genomes, n_words, seg, ix);
-  if (vs != GG_OK) return vs;
-  hp.mark("index runs");
+  if (n_runs && !runs) return fail(c, GG_ERR_INVALID_ARG, "null run table");
   const SketchGeom geom = sketch_geom(c->s);
   const uint64_t cap = 1ull << geom.cap_log2;
   // genomes per batch: tables limited to ~4 GiB
   const uint32_t max_batch = (uint32_t)std::max<uint64_t>(
       1, std::min<uint64_t>(n_genomes, (4ull << 30) / (cap * sizeof(uint64_t))));
-  const std::vector<uint64_t>& gr = ix.gr;
 
   int n_cu = 256;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);
@@ -363,6 +297,56 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   GG_HIP(c, scratch_t(c, "slot_genome", max_batch, &d_slot_genome));
   GG_HIP(c, scratch_t(c, "tau", max_batch, &d_tau));
 
+  // batch 0's candidate sets are cleared on `stream` while the run table
+  // uploads on the copy stream (C5: 2.6 GB of sets, 58 MB of runs)
+  const uint32_t nb0 = std::min(n_genomes, max_batch);
+  GG_HIP(c, hipMemsetAsync(d_table, 0xFF, (size_t)nb0 * cap * sizeof(uint64_t), st));
+  GG_HIP(c, hipMemsetAsync(d_flags, 0, nb0 * sizeof(uint32_t), st));
+  if (!c->copy_stream) {
+    GG_HIP(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    GG_HIP(c, hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming));
+  }
+  // the run table goes to the device once and is checked and indexed there
+  // (runindex.hip); the host keeps per genome its first run, k-mer count and
+  // first segment
+  gg_run* d_all_runs;
+  uint64_t *d_ix, *d_rs, *d_sc;
+  void* d_ix_tmp;
+  const size_t ng1 = (size_t)n_genomes + 1;
+  GG_HIP(c, scratch_t(c, "runs_all", std::max<uint64_t>(n_runs, 1), &d_all_runs));
+  GG_HIP(c, scratch_t(c, "run_sstart", n_runs + 1, &d_rs));
+  GG_HIP(c, scratch_t(c, "run_segs", n_runs + 1, &d_sc));
+  GG_HIP(c, scratch_t(c, "run_index", 1 + 3 * ng1, &d_ix));  // bad, gr, grs, nk
+  const size_t ix_tmp = run_index_tmp_bytes(n_runs);
+  GG_HIP(c, scratch(c, "run_index_tmp", std::max<size_t>(ix_tmp, 16), &d_ix_tmp));
+  if (n_runs)
+    GG_HIP(c, hipMemcpyAsync(d_all_runs, runs, n_runs * sizeof(gg_run), hipMemcpyHostToDevice, c->copy_stream));
+  GG_HIP(c, hipEventRecord(c->copy_done, c->copy_stream));
+  GG_HIP(c, hipStreamWaitEvent(st, c->copy_done, 0));
+  RunIndexDev xd;
+  xd.runs = d_all_runs;
+  xd.n_runs = n_runs;
+  xd.n_genomes = n_genomes;
+  xd.n_words = n_words;
+  xd.k = c->k;
+  xd.seg = seg;
+  xd.bad = d_ix;
+  xd.sc = d_sc;
+  xd.rs = d_rs;
+  xd.gr = d_ix + 1;
+  xd.grs = d_ix + 1 + ng1;
+  xd.nk = d_ix + 1 + 2 * ng1;
+  xd.tmp = d_ix_tmp;
+  xd.tmp_bytes = ix_tmp;
+  GG_HIP(c, launch_run_index(xd, st));
+  std::vector<uint64_t> hix(1 + 3 * ng1);
+  GG_HIP(c, hipMemcpyAsync(hix.data(), d_ix, hix.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  GG_HIP(c, hipStreamSynchronize(st));
+  if (hix[0] != ~0ull) return run_error(c, runs, hix[0], n_genomes);
+  const uint64_t* gr = hix.data() + 1;
+  const uint64_t* grs = hix.data() + 1 + ng1;
+  const uint64_t* nk = hix.data() + 1 + 2 * ng1;
+  hp.mark("index runs (device)");
   for (uint32_t g0 = 0; g0 < n_genomes; g0 += max_batch) {
     const uint32_t g1 = std::min(n_genomes, g0 + max_batch);
     const uint32_t nb = g1 - g0;
@@ -370,7 +354,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
     std::vector<uint64_t> h_tau(nb);
     std::vector<uint32_t> h_slot_genome(nb), h_slot_list(nb);
     for (uint32_t i = 0; i < nb; ++i) {
-      ts[i].tau = initial_tau(ix.nk[g0 + i], c->s, geom.over);
+      ts[i].tau = initial_tau(nk[g0 + i], c->s, geom.over);
       h_tau[i] = ts[i].tau;
       h_slot_genome[i] = g0 + i;
       h_slot_list[i] = i;
@@ -383,56 +367,57 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
     std::vector<uint32_t> active = h_slot_list;
     for (int pass = 0; !active.empty(); ++pass) {
       if (pass > 200) return fail(c, GG_ERR_INTERNAL, "bottom-s threshold search did not converge");
-      // run table for the active genomes: on the first pass the caller's
-      // runs of the batch as they are (one copy), on retries the subset
+      // run table for the active genomes: on the first pass the batch's
+      // slice of the uploaded table and its device index, on retries the
+      // subset's runs and segment starts, built here and uploaded.  K1
+      // segments never straddle runs: run r owns segments [rs[r], rs[r + 1]),
+      // ceil(k-mers / seg) of them, so every lane of a wave hashes exactly one
+      // piece per segment (a segment across a run boundary made its wave run
+      // the hashing loop twice: +30% VALU at C5, where runs are ~10 kb).
       const bool all = active.size() == nb;
-      const gg_run* run_src = runs + gr[g0];
+      const gg_run* d_run_src = d_all_runs + gr[g0];
+      const uint64_t* d_rs_src = d_rs + gr[g0];
       uint64_t nr = gr[g0 + nb] - gr[g0];
-      std::vector<gg_run> sub;
-      if (!all) {
-        sub.clear();
-        for (uint32_t slot : active)
-          for (uint64_t r = gr[g0 + slot]; r < gr[g0 + slot + 1]; ++r) sub.push_back(runs[r]);
-        run_src = sub.data();
-        nr = sub.size();
-      }
-      // K1 segments never straddle runs: run r owns segments
-      // [rs[r], rs[r + 1]), ceil(k-mers / seg) of them, so every lane of a
-      // wave hashes exactly one piece per segment (a segment across a run
-      // boundary made its wave run the hashing loop twice: +30% VALU at C5,
-      // where runs are ~10 kb).  First pass: the batch's slice of the index
-      // (segments numbered from rs[first run]); retries: the subset's own.
-      const uint64_t* rs = ix.rs.data() + gr[g0];
+      uint64_t seg0 = grs[g0], sacc = grs[g0 + nb] - grs[g0];
       uint64_t kacc = 0;
       if (!all) {
+        std::vector<gg_run> sub;
+        for (uint32_t slot : active)
+          for (uint64_t r = gr[g0 + slot]; r < gr[g0 + slot + 1]; ++r) sub.push_back(runs[r]);
+        nr = sub.size();
         std::vector<uint64_t>& sub_rs = c->sstart_host;
         sub_rs.resize(nr + 1);
-        uint64_t sacc = 0;
+        uint64_t acc = 0;
         for (uint64_t r = 0; r < nr; ++r) {
-          sub_rs[r] = sacc;
-          sacc += (run_src[r].len - (uint32_t)c->k + 1 + seg - 1) / seg;
+          sub_rs[r] = acc;
+          acc += (sub[r].len - (uint32_t)c->k + 1 + seg - 1) / seg;
         }
-        sub_rs[nr] = sacc;
-        rs = sub_rs.data();
-        for (uint32_t slot : active) kacc += ix.nk[g0 + slot];
+        sub_rs[nr] = acc;
+        seg0 = 0;
+        sacc = acc;
+        for (uint32_t slot : active) kacc += nk[g0 + slot];
+        gg_run* d_sub;
+        uint64_t* d_sub_rs;
+        GG_HIP(c, scratch_t(c, "runs_sub", std::max<size_t>(nr, 1), &d_sub));
+        GG_HIP(c, scratch_t(c, "run_sstart_sub", nr + 1, &d_sub_rs));
+        if (nr) GG_HIP(c, hipMemcpyAsync(d_sub, sub.data(), nr * sizeof(gg_run), hipMemcpyHostToDevice, st));
+        GG_HIP(c, hipMemcpyAsync(d_sub_rs, sub_rs.data(), (nr + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+        GG_HIP(c, hipStreamSynchronize(st));  // (sub goes out of scope)
+        d_run_src = d_sub;
+        d_rs_src = d_sub_rs;
       } else {
-        for (uint32_t i = 0; i < nb; ++i) kacc += ix.nk[g0 + i];
+        for (uint32_t i = 0; i < nb; ++i) kacc += nk[g0 + i];
       }
-      const uint64_t seg0 = rs[0], sacc = rs[nr] - rs[0];
       hp.mark("segment starts");
-      gg_run* d_runs;
-      uint64_t* d_rs;
-      GG_HIP(c, scratch_t(c, "runs", std::max<size_t>(nr, 1), &d_runs));
-      GG_HIP(c, scratch_t(c, "run_sstart", nr + 1, &d_rs));
-      if (nr) GG_HIP(c, hipMemcpyAsync(d_runs, run_src, nr * sizeof(gg_run), hipMemcpyHostToDevice, st));
-      GG_HIP(c, hipMemcpyAsync(d_rs, rs, (nr + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
       GG_HIP(c, hipMemcpyAsync(d_tau, h_tau.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
       GG_HIP(c, hipMemcpyAsync(d_slot_list, active.data(), active.size() * sizeof(uint32_t),
                                hipMemcpyHostToDevice, st));
       hp.mark("H2D runs/starts");
       if (pass == 0) {
-        GG_HIP(c, hipMemsetAsync(d_table, 0xFF, (size_t)nb * cap * sizeof(uint64_t), st));
-        GG_HIP(c, hipMemsetAsync(d_flags, 0, nb * sizeof(uint32_t), st));
+        if (g0 > 0) {  // (batch 0 was cleared before the run index)
+          GG_HIP(c, hipMemsetAsync(d_table, 0xFF, (size_t)nb * cap * sizeof(uint64_t), st));
+          GG_HIP(c, hipMemsetAsync(d_flags, 0, nb * sizeof(uint32_t), st));
+        }
       } else {
         for (uint32_t slot : active) {
           GG_HIP(c, hipMemsetAsync(d_table + (uint64_t)slot * cap, 0xFF, cap * sizeof(uint64_t), st));
@@ -442,8 +427,8 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       SketchLaunch a;
       a.words = d_words;
       a.n_words = n_words;
-      a.runs = d_runs;
-      a.run_sstart = d_rs;
+      a.runs = d_run_src;
+      a.run_sstart = d_rs_src;
       a.slot_genome0 = g0;
       a.n_runs = (uint32_t)nr;
       a.seg0 = seg0;
@@ -637,6 +622,7 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   GG_HIP(c, scratch_t(c, "idx_vals_in", total, &b.vals_in));
   GG_HIP(c, scratch_t(c, "idx_vals_out", total, &b.vals_out));
   GG_HIP(c, scratch_t(c, "idx_runinfo", total, &b.runinfo));
+  GG_HIP(c, scratch_t(c, "idx_mixed", (total + 31) / 32, &b.mixed));
   b.sort_tmp_bytes = index_sort_tmp_bytes(total);
   GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
   GG_HIP(c, scratch_t(c, "idx_flags", 4, &b.flags));
@@ -968,6 +954,8 @@ void gg_destroy(gg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   for (hipStream_t ps : ctx->peer_streams)
     if (ps) (void)hipStreamDestroy(ps);
+  if (ctx->copy_done) (void)hipEventDestroy(ctx->copy_done);
+  if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   delete ctx;
 }

@@ -51,6 +51,26 @@ struct SketchLaunch {
   uint64_t seed;
 };
 
+// runindex.hip: the run table's index on the device (all device pointers)
+struct RunIndexDev {
+  const gg_run* runs;  // [n_runs], uploaded
+  uint64_t n_runs;
+  uint32_t n_genomes;
+  uint64_t n_words;
+  int k;
+  uint32_t seg;        // K1 segment length
+  uint64_t* bad;       // [1] first bad run (2^64-1: none)
+  uint64_t* sc;        // [n_runs + 1] scratch: segments per run
+  uint64_t* rs;        // [n_runs + 1] first segment of each run; rs[n_runs] = total
+  uint64_t* gr;        // [n_genomes + 1] first run of each genome
+  uint64_t* grs;       // [n_genomes + 1] rs[gr[g]]
+  uint64_t* nk;        // [n_genomes] k-mers per genome
+  void* tmp;
+  size_t tmp_bytes;
+};
+size_t run_index_tmp_bytes(uint64_t n_runs);
+hipError_t launch_run_index(const RunIndexDev& x, hipStream_t st);
+
 // sketch.hip
 hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,
                                     hipStream_t st);
@@ -201,6 +221,7 @@ struct IndexBuild {
   uint64_t* vals_in;
   uint64_t* vals_out;
   uint64_t* runinfo;   // [n * stride]
+  uint32_t* mixed;     // [ceil(n * stride / 32)] bitset: runs of equal keys holding several hashes
   void* sort_tmp;
   size_t sort_tmp_bytes;
   uint32_t* flags;     // [4]: overflow

@@ -203,79 +203,128 @@ __global__ __launch_bounds__(256) void index_fill_range_kernel(
   }
 }
 
-// Runs of equal keys: the thread at a run start owns it.  Every member of a
-// hash's run of g >= 2 gets runinfo = (start | g << 32) (runinfo is zeroed
-// beforehand, so g = 1 writes nothing) and ents[q] = its entry (the pairs
-// kernel reads 4 bytes per run member instead of the 8 of vals).  A run whose members do not all
-// carry the same low hash word (two hashes with the same top bits: rare) is
-// then sorted in place by (low word, entry), split, and written again.  Runs
-// longer than max_run set *overflow (the host then uses the gate kernel).
+// Runs of equal keys, one thread per sorted entry p (every lane busy: the
+// run pass was thread-per-run before, with ~4 of 5 lanes idle at the
+// non-starts and its 8-byte runinfo stores issued by one lane per run).
+// A wave covers 64 consecutive entries; the ballot of "p starts a run" and
+// of "p + 1 starts a run" give every lane its run [start, end) from bit
+// scans; a run that begins before the wave or ends after it is extended by
+// one lane walking the sorted keys (runs are a few entries; longer than
+// max_run sets *overflow and the host uses the gate kernel).  Each entry then
+//   ents[p] = its (row << kbits | k), and
+//   runinfo[row, k] = start | g << 32 (g >= 2) or 0 (a hash no other
+//   sketch holds; every evaluated row's entries are written, so runinfo needs
+//   no clearing).
+// A run of equal keys whose members do not all carry the start's low hash
+// word (two hashes with the same top bits: rare) marks its start in the
+// `mixed` bitset; index_mixed_kernel then sorts it and writes its sub-runs.
+__device__ __forceinline__ uint32_t run_start_back(const uint32_t* __restrict__ keys, uint64_t p, uint32_t key,
+                                                   uint32_t max_run) {
+  // first position of the run holding p (bounded: a longer run overflows anyway)
+  uint64_t q = p;
+  while (q > 0 && keys[q - 1] == key && p - q <= max_run) --q;
+  return (uint32_t)q;
+}
+
 __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restrict__ keys,
-                                                         uint64_t* __restrict__ vals, uint64_t total,
+                                                         const uint64_t* __restrict__ vals, uint64_t total,
                                                          uint32_t stride, uint32_t kbits, uint32_t max_run,
                                                          uint64_t* __restrict__ runinfo, uint32_t* __restrict__ ents,
-                                                         uint32_t* __restrict__ overflow) {
-  // (no device-wide event counter: one atomic per wave on one address
-  // serialises at ~12 ns each, 1.9 ms at C3)
+                                                         uint32_t* __restrict__ mixed, uint32_t* __restrict__ overflow) {
   const uint32_t kmask = (1u << kbits) - 1u;
-  constexpr int W = 8;  // run members read in batches of W independent loads
-  for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (uint64_t)gridDim.x * 256) {
-    const uint32_t key = keys[p];
-    if (p > 0 && keys[p - 1] == key) continue;  // not a run start
-    // run end: the next W - 1 keys at once (most runs are a cluster's few
-    // genomes), then one at a time
-    uint32_t kk[W - 1];
-#pragma unroll
-    for (int j = 1; j < W; ++j) kk[j - 1] = p + j < total ? keys[p + j] : ~key;
-    uint64_t e = p + 1;
-#pragma unroll
-    for (int j = 1; j < W; ++j)
-      if (e == p + j && kk[j - 1] == key) e = p + j + 1;
-    if (e == p + W)
-      while (e < total && keys[e] == key && e - p <= max_run) ++e;
-    if (e - p > max_run) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t waves = (uint64_t)gridDim.x * 4;
+  for (uint64_t w0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; w0 < total; w0 += waves * 64) {
+    const uint64_t p = w0 + lane;
+    const bool in = p < total;
+    const uint32_t key = in ? keys[p] : 0u;
+    const uint32_t prev = (in && p > 0) ? keys[p - 1] : ~key;
+    const uint32_t next = (p + 1 < total) ? keys[p + 1] : ~key;
+    const uint64_t v = in ? vals[p] : 0ull;
+    // S: bit t = entry w0 + t starts a run; E: bit t = entry w0 + t ends one
+    const uint64_t S = __ballot(in && (p == 0 || prev != key));
+    const uint64_t E = __ballot(in && (p + 1 == total || next != key));
+    const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    const uint64_t sb = S & upto, eb = E & ~(upto >> 1);  // starts at or below / ends at or above the lane
+    // the wave's first run may begin before w0, its last may end after w0 + 63
+    uint32_t head = (uint32_t)w0, tail_end = 0;
+    if (!(S & 1ull)) {  // (uniform) walk back from w0
+      uint32_t h = 0;
+      if (lane == 0) h = run_start_back(keys, w0, key, max_run);
+      head = __builtin_amdgcn_readfirstlane(h);
+    }
+    const uint32_t last = (uint32_t)(63 - __builtin_clzll(__ballot(in)));  // last lane in range
+    if (!((E >> last) & 1ull)) {  // (uniform) walk forward from the wave's end
+      uint32_t t = 0;
+      if (lane == last) {
+        uint64_t q = p + 1;
+        while (q < total && keys[q] == key && q - p <= max_run) ++q;
+        t = (uint32_t)q;
+      }
+      tail_end = __builtin_amdgcn_readfirstlane(t);
+    }
+    if (!in) continue;
+    const uint32_t start = sb ? (uint32_t)(w0 + 63 - __builtin_clzll(sb)) : head;
+    const uint32_t end = eb ? (uint32_t)(w0 + __builtin_ctzll(eb) + 1) : tail_end;
+    const uint32_t g = end - start;
+    // the start's low hash word: from its lane, or (a run begun before the
+    // wave) from memory
+    const uint32_t lo = (uint32_t)(v >> 32);
+    const uint32_t src = start >= w0 ? (uint32_t)(start - w0) : 0u;
+    uint32_t lo0 = __shfl(lo, (int)src);
+    if (start < w0) lo0 = (uint32_t)(vals[start] >> 32);
+    const uint32_t e = (uint32_t)v;
+    ents[p] = e;
+    if (g > max_run) {
       atomicOr(overflow, 1u);
       continue;
     }
-    if (e - p == 1) continue;  // (no other row reads a singleton's entry)
-    const uint64_t info = p | ((e - p) << 32);
-    uint32_t lo0 = 0;
-    bool mixed = false;
-    for (uint64_t q0 = p; q0 < e; q0 += W) {
-      uint64_t x[W];
-#pragma unroll
-      for (int j = 0; j < W; ++j) x[j] = q0 + j < e ? vals[q0 + j] : 0ull;
-      if (q0 == p) lo0 = (uint32_t)(x[0] >> 32);
-#pragma unroll
-      for (int j = 0; j < W; ++j) {
-        if (q0 + j >= e) break;
-        mixed |= (uint32_t)(x[j] >> 32) != lo0;
-        const uint32_t v = (uint32_t)x[j];
-        ents[q0 + j] = v;
-        runinfo[(uint64_t)(v >> kbits) * stride + (v & kmask)] = info;
+    runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] = g >= 2 ? ((uint64_t)start | ((uint64_t)g << 32)) : 0ull;
+    if (lo != lo0) atomicOr(&mixed[start >> 5], 1u << (start & 31));
+  }
+}
+
+// The runs index_runs_kernel marked mixed (equal top bits, more than one
+// hash): sorted in place by (low word, entry) by one thread each, split by
+// low word, ents and runinfo rewritten for their members.  One thread per
+// bitset word.
+__global__ __launch_bounds__(256) void index_mixed_kernel(const uint32_t* __restrict__ keys,
+                                                          uint64_t* __restrict__ vals, uint64_t total,
+                                                          uint32_t stride, uint32_t kbits,
+                                                          const uint32_t* __restrict__ mixed,
+                                                          uint64_t* __restrict__ runinfo,
+                                                          uint32_t* __restrict__ ents) {
+  const uint32_t kmask = (1u << kbits) - 1u;
+  const uint64_t nw = (total + 31) / 32;
+  for (uint64_t wi = (uint64_t)blockIdx.x * 256 + threadIdx.x; wi < nw; wi += (uint64_t)gridDim.x * 256) {
+    uint32_t m = mixed[wi];
+    while (m) {
+      const uint64_t p = wi * 32 + (uint64_t)__builtin_ctz(m);
+      m &= m - 1;
+      const uint32_t key = keys[p];
+      uint64_t e = p + 1;
+      while (e < total && keys[e] == key) ++e;
+      for (uint64_t q = p + 1; q < e; ++q) {  // insertion sort by (low word, entry)
+        const uint64_t x = vals[q];
+        uint64_t w = q;
+        while (w > p && vals[w - 1] > x) {
+          vals[w] = vals[w - 1];
+          --w;
+        }
+        vals[w] = x;
       }
-    }
-    if (!mixed) continue;
-    for (uint64_t q = p + 1; q < e; ++q) {  // insertion sort by (low word, entry)
-      const uint64_t x = vals[q];
-      uint64_t w = q;
-      while (w > p && vals[w - 1] > x) {
-        vals[w] = vals[w - 1];
-        --w;
+      for (uint64_t a = p; a < e;) {
+        const uint32_t lo = (uint32_t)(vals[a] >> 32);
+        uint64_t b = a + 1;
+        while (b < e && (uint32_t)(vals[b] >> 32) == lo) ++b;
+        const uint64_t sub = b - a >= 2 ? (a | ((b - a) << 32)) : 0ull;
+        for (uint64_t q = a; q < b; ++q) {
+          const uint32_t v = (uint32_t)vals[q];
+          ents[q] = v;
+          runinfo[(uint64_t)(v >> kbits) * stride + (v & kmask)] = sub;
+        }
+        a = b;
       }
-      vals[w] = x;
-    }
-    for (uint64_t a = p; a < e;) {
-      const uint32_t lo = (uint32_t)(vals[a] >> 32);
-      uint64_t b = a + 1;
-      while (b < e && (uint32_t)(vals[b] >> 32) == lo) ++b;
-      const uint64_t sub = b - a >= 2 ? (a | ((b - a) << 32)) : 0ull;
-      for (uint64_t q = a; q < b; ++q) {
-        const uint32_t v = (uint32_t)vals[q];
-        ents[q] = v;
-        runinfo[(uint64_t)(v >> kbits) * stride + (v & kmask)] = sub;
-      }
-      a = b;
     }
   }
 }
@@ -419,18 +468,20 @@ hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_
   e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out,
                                          (int)total, 0, (int)end_bit, st);
   if (e != hipSuccess) return e;
-  // runinfo of the evaluated rows (all rows, or [r0, r1) for the row-range
-  // index: other rows' slots are written by the run pass but never read)
-  if (b.bloom)
-    e = hipMemsetAsync(b.runinfo + (size_t)b.r0 * b.stride, 0, (size_t)(b.r1 - b.r0) * b.stride * sizeof(uint64_t),
-                       st);
-  else
-    e = hipMemsetAsync(b.runinfo, 0, (size_t)b.n * b.stride * sizeof(uint64_t), st);
+  // (runinfo needs no clearing: the run pass writes the slot of every entry
+  // it sees, which includes every entry of every evaluated row)
+  e = hipMemsetAsync(b.mixed, 0, ((total + 31) / 32) * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
-  const uint64_t blocks = std::min<uint64_t>(65536, (total + 255) / 256);
+  const uint64_t waves = (total + 63) / 64;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(1u << 16, (waves + 3) / 4);
   // the entries of shared hashes land in keys_in (free after the sort)
-  hipLaunchKernelGGL(index_runs_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, b.keys_out, b.vals_out, total,
-                     b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in, b.flags);
+  hipLaunchKernelGGL(index_runs_kernel, dim3(blocks), dim3(256), 0, st, b.keys_out, b.vals_out, total, b.stride,
+                     b.kbits, b.max_run, b.runinfo, b.keys_in, b.mixed, b.flags);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint64_t words = (total + 31) / 32;
+  hipLaunchKernelGGL(index_mixed_kernel, dim3((uint32_t)std::min<uint64_t>(4096, (words + 255) / 256)), dim3(256), 0,
+                     st, b.keys_out, b.vals_out, total, b.stride, b.kbits, b.mixed, b.runinfo, b.keys_in);
   return hipGetLastError();
 }
 

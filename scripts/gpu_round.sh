@@ -42,7 +42,7 @@ for st in $STAGES; do
     bench_c5)    bench bench_c5 300 --config c5 --steps 10 --warmup 2 --no-cpu-baseline ;;
     bench_files) bench bench_files 600 --files --steps 3 --warmup 1 --no-cpu-baseline ;;
     benchalt)  # the C3 and C5 benches against an alternate build
-      GALAHGPU_LIB="${ALT_LIB:?}" bench bench_alt_c3 300 --steps 20 --warmup 5 --no-cpu-baseline
+      GALAHGPU_LIB="${ALT_LIB:?}" bench bench_alt_c3 300 --steps 20 --warmup 5 --no-cpu-baseline --no-files
       GALAHGPU_LIB="${ALT_LIB:?}" bench bench_alt_c5 300 --config c5 --steps 10 --warmup 2 --no-cpu-baseline ;;
     bench2r)  # the driver's launch shape on one GPU (two members of GPU 0)
       run bench_2rank 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
@@ -55,6 +55,8 @@ for st in $STAGES; do
         python3 -u bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
     pmc)  # PMC passes at HEAD (scripts/pmc_head.sh)
       run pmc 900 bash scripts/pmc_head.sh "$OUT/pmc" ${PMC_ARGS:-} || exit $? ;;
+    ubench3)
+      run ubench_vop3 120 ./scripts/ubench_vop3 8 && run ubench_vop3_w1 120 ./scripts/ubench_vop3 1 || exit $? ;;
     ubench)
       run ubench 300 ./scripts/ubench_dual || exit $? ;;
     *) echo "unknown stage $st"; exit 2 ;;
