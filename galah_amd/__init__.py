@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "gg_sketch", "gg_sketch_device",
     "gg_pair_tiles", "gg_pair_partition", "gg_pairs", "gg_pairs_device",
     "gg_precluster_files", "gg_ani_f64", "gg_ani_f32", "gg_parse_percentage",
-    "gg_free", "gg_synth_clustered_device", "gg_timing_enable", "gg_timing_read",
+    "gg_free", "gg_synth_clustered_device", "gg_timing_enable", "gg_timing_read", "gg_pair_paths",
     "gg_partition_preclusters", "gg_precluster_pairs", "gg_synth_mixed_lengths", "gg_synth_mixed_device",
     "gg_sketch_cache_load", "gg_sketch_cache_store", "gg_sketch_files", "gg_precluster_files_cached",
     "gg_create_multi", "gg_device_count", "gg_device_ctx", "gg_set_host_threads", "gg_phase_times",
@@ -153,6 +153,7 @@ class _KStats(ctypes.Structure):
 
 
 _sig("gg_timing_enable", _i32, [_vp, _i32])
+_sig("gg_pair_paths", _i32, [_vp, _vp])
 _sig("gg_timing_read", _i32, [_vp, _i32, ctypes.POINTER(_KStats)])
 KERNEL_SKETCH, KERNEL_FINALIZE, KERNEL_PAIRS, KERNEL_PAIRS_INDEX = 0, 1, 2, 3
 
@@ -467,6 +468,15 @@ class Context:
         st = _L.gg_timing_enable(self._c, 1 if on else 0)
         if st != GG_OK:
             raise self._err(st)
+
+    def pair_paths(self):
+        """Which pair kernel ran, counted since the context was created
+        (gg_pair_paths): {"index", "index_abandoned", "gate", "other"}."""
+        out = np.zeros(4, np.uint64)
+        st = _L.gg_pair_paths(self._c, _ptr(out))
+        if st != GG_OK:
+            raise self._err(st)
+        return dict(zip(("index", "index_abandoned", "gate", "other"), (int(x) for x in out)))
 
     def timing_read(self, kernel):
         """-> dict(ms, launches, work) summed since timing_enable."""

@@ -740,10 +740,13 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
       bool used = false;
       gg_status is = pairs_index(c, d_sk, d_lens, n, nb, tb, te, d_cmin, d_sufmin, d_out, cap, d_count, work, st,
                                  &used);
-      if (is != GG_OK || used) return is;
+      if (is != GG_OK) return is;
+      ++c->pair_paths[used ? GG_PATH_INDEX : GG_PATH_INDEX_ABANDONED];
+      if (used) return GG_OK;
     }
     kern = 0;
   }
+  ++c->pair_paths[(kern == 0 || kern == 3) ? GG_PATH_GATE : GG_PATH_OTHER];
   if (kern == 2) {
     PairsLaunch a;
     a.sketches = d_sk;
@@ -1076,6 +1079,14 @@ gg_status gg_timing_enable(gg_ctx* ctx, int on) {
   }
   ctx->timed.clear();
   ctx->timing = on != 0;
+  return GG_OK;
+}
+
+gg_status gg_pair_paths(const gg_ctx* ctx, uint64_t* paths) {
+  if (!ctx || !paths) return fail(nullptr, GG_ERR_INVALID_ARG, "gg_pair_paths: null argument");
+  for (int i = 0; i < GG_PATH_COUNT; ++i) paths[i] = ctx->pair_paths[i];
+  for (const gg_ctx* m : ctx->devs)
+    for (int i = 0; i < GG_PATH_COUNT; ++i) paths[i] += m->pair_paths[i];
   return GG_OK;
 }
 

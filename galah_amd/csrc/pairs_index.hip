@@ -42,6 +42,12 @@ constexpr uint32_t kMapLog2 = 11;
 constexpr uint32_t kMap = 1u << kMapLog2;  // LDS partner map slots per row
 constexpr uint32_t kMapFull = kMap * 3 / 4;
 constexpr int kScanThreads = 1024;
+constexpr uint32_t kXcds = 8;  // MI355X: 8 XCDs, each with its own L2
+// run pass: write every entry's runinfo slot (1; no clear needed) or only
+// those of runs of g >= 2 after clearing the evaluated rows (0)
+#ifndef GG_RUNINFO_ALL
+#define GG_RUNINFO_ALL 1
+#endif
 
 // #{ e < n : a[e] <= x }, a ascending
 __device__ __forceinline__ uint32_t count_le(const uint64_t* __restrict__ a, uint32_t n, uint64_t x) {
@@ -233,8 +239,18 @@ __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restr
                                                          uint32_t* __restrict__ mixed, uint32_t* __restrict__ overflow) {
   const uint32_t kmask = (1u << kbits) - 1u;
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t waves = (uint64_t)gridDim.x * 4;
-  for (uint64_t w0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; w0 < total; w0 += waves * 64) {
+  // XCD-aware: the sorted entries are cut into kXcds contiguous chunks and
+  // the workgroups of XCD x (blockIdx % kXcds, the dispatcher's round robin)
+  // sweep chunk x.  The runinfo stores land on every row wherever the sweep
+  // is, but at a given moment an XCD's sweep covers 1/kXcds of the hash range
+  // and so a few cache lines per row, which its own L2 can gather into whole
+  // lines (the grid-strided sweep spread every XCD over the whole range).
+  const uint64_t W = (total + 63) / 64;
+  const uint32_t x = blockIdx.x % kXcds;
+  const uint64_t wend = W * (x + 1) / kXcds;
+  const uint64_t step = (uint64_t)(gridDim.x / kXcds) * 4;
+  for (uint64_t wi = W * x / kXcds + (uint64_t)(blockIdx.x / kXcds) * 4 + (threadIdx.x >> 6); wi < wend; wi += step) {
+    const uint64_t w0 = wi * 64;
     const uint64_t p = w0 + lane;
     const bool in = p < total;
     const uint32_t key = in ? keys[p] : 0u;
@@ -251,7 +267,7 @@ __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restr
     if (!(S & 1ull)) {  // (uniform) walk back from w0
       uint32_t h = 0;
       if (lane == 0) h = run_start_back(keys, w0, key, max_run);
-      head = __builtin_amdgcn_readfirstlane(h);
+      head = __builtin_amdgcn_readlane(h, 0);
     }
     const uint32_t last = (uint32_t)(63 - __builtin_clzll(__ballot(in)));  // last lane in range
     if (!((E >> last) & 1ull)) {  // (uniform) walk forward from the wave's end
@@ -261,7 +277,7 @@ __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restr
         while (q < total && keys[q] == key && q - p <= max_run) ++q;
         t = (uint32_t)q;
       }
-      tail_end = __builtin_amdgcn_readfirstlane(t);
+      tail_end = __builtin_amdgcn_readlane(t, last);
     }
     if (!in) continue;
     const uint32_t start = sb ? (uint32_t)(w0 + 63 - __builtin_clzll(sb)) : head;
@@ -279,7 +295,11 @@ __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restr
       atomicOr(overflow, 1u);
       continue;
     }
+#if GG_RUNINFO_ALL
     runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] = g >= 2 ? ((uint64_t)start | ((uint64_t)g << 32)) : 0ull;
+#else
+    if (g >= 2) runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] = (uint64_t)start | ((uint64_t)g << 32);
+#endif
     if (lo != lo0) atomicOr(&mixed[start >> 5], 1u << (start & 31));
   }
 }
@@ -288,6 +308,7 @@ __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restr
 // hash): sorted in place by (low word, entry) by one thread each, split by
 // low word, ents and runinfo rewritten for their members.  One thread per
 // bitset word.
+constexpr uint32_t kMixedRegs = 16;
 __global__ __launch_bounds__(256) void index_mixed_kernel(const uint32_t* __restrict__ keys,
                                                           uint64_t* __restrict__ vals, uint64_t total,
                                                           uint32_t stride, uint32_t kbits,
@@ -304,14 +325,32 @@ __global__ __launch_bounds__(256) void index_mixed_kernel(const uint32_t* __rest
       const uint32_t key = keys[p];
       uint64_t e = p + 1;
       while (e < total && keys[e] == key) ++e;
-      for (uint64_t q = p + 1; q < e; ++q) {  // insertion sort by (low word, entry)
-        const uint64_t x = vals[q];
-        uint64_t w = q;
-        while (w > p && vals[w - 1] > x) {
-          vals[w] = vals[w - 1];
-          --w;
+      if (e - p <= kMixedRegs) {  // sort by (low word, entry) in registers
+        uint64_t r[kMixedRegs];
+#pragma unroll
+        for (uint32_t q = 0; q < kMixedRegs; ++q) r[q] = p + q < e ? vals[p + q] : ~0ull;
+#pragma unroll
+        for (uint32_t q = 1; q < kMixedRegs; ++q) {
+#pragma unroll
+          for (uint32_t w = q; w > 0; --w) {
+            const uint64_t a = r[w - 1], b = r[w];
+            r[w - 1] = a < b ? a : b;
+            r[w] = a < b ? b : a;
+          }
         }
-        vals[w] = x;
+#pragma unroll
+        for (uint32_t q = 0; q < kMixedRegs; ++q)
+          if (p + q < e) vals[p + q] = r[q];
+      } else {
+        for (uint64_t q = p + 1; q < e; ++q) {  // insertion sort in place
+          const uint64_t x = vals[q];
+          uint64_t w = q;
+          while (w > p && vals[w - 1] > x) {
+            vals[w] = vals[w - 1];
+            --w;
+          }
+          vals[w] = x;
+        }
       }
       for (uint64_t a = p; a < e;) {
         const uint32_t lo = (uint32_t)(vals[a] >> 32);
@@ -468,12 +507,25 @@ hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_
   e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out,
                                          (int)total, 0, (int)end_bit, st);
   if (e != hipSuccess) return e;
+#if GG_RUNINFO_ALL
   // (runinfo needs no clearing: the run pass writes the slot of every entry
   // it sees, which includes every entry of every evaluated row)
+#else
+  // runinfo of the evaluated rows (all rows, or [r0, r1) for the row-range
+  // index: other rows' slots are written by the run pass but never read)
+  if (b.bloom)
+    e = hipMemsetAsync(b.runinfo + (size_t)b.r0 * b.stride, 0, (size_t)(b.r1 - b.r0) * b.stride * sizeof(uint64_t),
+                       st);
+  else
+    e = hipMemsetAsync(b.runinfo, 0, (size_t)b.n * b.stride * sizeof(uint64_t), st);
+  if (e != hipSuccess) return e;
+#endif
   e = hipMemsetAsync(b.mixed, 0, ((total + 31) / 32) * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   const uint64_t waves = (total + 63) / 64;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>(1u << 16, (waves + 3) / 4);
+  // a multiple of kXcds workgroups, ~8 per CU-slot of the chip at most
+  const uint32_t blocks = (uint32_t)(std::min<uint64_t>(8192, std::max<uint64_t>(1, (waves + 4 * kXcds - 1) /
+                                                                                  (4 * kXcds))) * kXcds);
   // the entries of shared hashes land in keys_in (free after the sort)
   hipLaunchKernelGGL(index_runs_kernel, dim3(blocks), dim3(256), 0, st, b.keys_out, b.vals_out, total, b.stride,
                      b.kbits, b.max_run, b.runinfo, b.keys_in, b.mixed, b.flags);

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 2u
+#define GG_ABI_VERSION 3u
 
 typedef enum gg_status {
   GG_OK = 0,
@@ -323,6 +323,17 @@ typedef struct gg_kernel_stats {
 } gg_kernel_stats;
 gg_status gg_timing_enable(gg_ctx* ctx, int on);
 gg_status gg_timing_read(gg_ctx* ctx, int kernel, gg_kernel_stats* out);
+
+/* ---- which pair kernel ran ---------------------------------------------- */
+/* Counts since the context was created (all members of a multi-device
+ * context summed), one per pair-kernel call over a tile range:
+ * paths[0] the inverted index ran to completion, paths[1] the index was
+ * abandoned for the gate kernel (a hash shared by more sketches than its run
+ * limit, or a row's partners overflowing its map), paths[2] the gate kernel
+ * ran (after an abandoned index too), paths[3] another form (table / merge,
+ * GALAHGPU_PAIRS_KERNEL). */
+enum { GG_PATH_INDEX = 0, GG_PATH_INDEX_ABANDONED = 1, GG_PATH_GATE = 2, GG_PATH_OTHER = 3, GG_PATH_COUNT = 4 };
+gg_status gg_pair_paths(const gg_ctx* ctx, uint64_t* paths);
 
 /* ---- benchmark support: synthetic clustered genomes on device ---------- */
 /* Genomes [first_genome, first_genome + n_genomes) of a synthetic set of

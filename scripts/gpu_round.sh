@@ -41,9 +41,10 @@ for st in $STAGES; do
     bench_c4)    bench bench_c4 600 --config c4 --steps 3 --warmup 1 --no-cpu-baseline ;;
     bench_c5)    bench bench_c5 300 --config c5 --steps 10 --warmup 2 --no-cpu-baseline ;;
     bench_files) bench bench_files 600 --files --steps 3 --warmup 1 --no-cpu-baseline ;;
-    benchalt)  # the C3 and C5 benches against an alternate build
-      GALAHGPU_LIB="${ALT_LIB:?}" bench bench_alt_c3 300 --steps 20 --warmup 5 --no-cpu-baseline --no-files
-      GALAHGPU_LIB="${ALT_LIB:?}" bench bench_alt_c5 300 --config c5 --steps 10 --warmup 2 --no-cpu-baseline ;;
+    benchalt|benchalt2)  # the C3 and C5 benches against an alternate build (ALT_LIB / ALT_LIB2)
+      lib=$ALT_LIB; [ $st = benchalt2 ] && lib=$ALT_LIB2
+      GALAHGPU_LIB="${lib:?}" bench ${st}_c3 300 --steps 20 --warmup 5 --no-cpu-baseline --no-files
+      GALAHGPU_LIB="${lib:?}" bench ${st}_c5 300 --config c5 --steps 10 --warmup 2 --no-cpu-baseline ;;
     bench2r)  # the driver's launch shape on one GPU (two members of GPU 0)
       run bench_2rank 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29511 bench.py --gpus 2 --devices 0,0 --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
@@ -55,6 +56,11 @@ for st in $STAGES; do
         python3 -u bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
     pmc)  # PMC passes at HEAD (scripts/pmc_head.sh)
       run pmc 900 bash scripts/pmc_head.sh "$OUT/pmc" ${PMC_ARGS:-} || exit $? ;;
+    pmc_k1)  # K1 instruction counters at C3 and C5 (scripts/pmc.sh passes 1-2)
+      PMC_SETS=2 run pmc_k1_c3 400 bash scripts/pmc.sh "$OUT/pmc_k1_c3" sketch_candidates -- \
+        python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-files || exit $?
+      PMC_SETS=2 run pmc_k1_c5 400 bash scripts/pmc.sh "$OUT/pmc_k1_c5" sketch_candidates -- \
+        python3 bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline --no-files || exit $? ;;
     ubench3)
       run ubench_vop3 120 ./scripts/ubench_vop3 8 && run ubench_vop3_w1 120 ./scripts/ubench_vop3 1 || exit $? ;;
     ubench)

@@ -14,6 +14,7 @@ sets=(
 i=0
 for s in "${sets[@]}"; do
   i=$((i+1))
+  [ -n "$PMC_SETS" ] && [ $i -gt "$PMC_SETS" ] && break
   echo "== pmc pass $i: $s"
   timeout -s KILL 120 rocprofv3 --pmc $s --kernel-include-regex "$rx" --output-format csv -d "$out/p$i" -o p$i -- "$@" > "$out/p$i.log" 2>&1
   rc=$?

@@ -117,8 +117,14 @@ def check_config(ctx, d_words, runs, n, s, thr, genome_bases, spot):
     for g, exp in outs:
         assert len(exp) == ln[g] and (sk[g][:ln[g]] == exp).all(), g
 
-    # all pairs on the device
+    # all pairs on the device, through the inverted index to completion (the
+    # default at these sizes; an abandoned index would fall back to the gate
+    # kernel with the same pairs, hiding a broken index)
+    before = ctx.pair_paths()
     P = device_pairs(ctx, d_sk, d_len, n, 0, ga.pair_tiles(n), thr)
+    after = ctx.pair_paths()
+    assert after["index"] == before["index"] + 1 and after["index_abandoned"] == before["index_abandoned"]
+    assert after["gate"] == before["gate"]
     got = {(int(a), int(b)): (int(c), int(t)) for a, b, c, t in P}
     assert len(got) == len(P)
     # every within-cluster pair against the oracle
@@ -171,6 +177,8 @@ def check_config(ctx, d_words, runs, n, s, thr, genome_bases, spot):
             os.environ["GALAHGPU_PAIRS_KERNEL"] = kern
             with ga.Context(k=21, sketch_size=s) as mctx:
                 bands[kern] = device_pairs(mctx, d_sk, d_len, n, tb, te, thr)
+                if kern == "index":
+                    assert mctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0}
     finally:
         if old is None:
             os.environ.pop("GALAHGPU_PAIRS_KERNEL")

@@ -433,6 +433,8 @@ def test_index_kernel_many_partners_and_long_runs(monkeypatch):
             monkeypatch.setenv("GALAHGPU_INDEX_MAX_SPLIT", split)
             with ga.Context(k=21, sketch_size=s) as ctx:
                 assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, (thr, split)
+                if split == "0":  # 2,999 partners never fit one map: abandoned for the gate kernel
+                    assert ctx.pair_paths() == {"index": 0, "index_abandoned": 1, "gate": 1, "other": 0}
         monkeypatch.delenv("GALAHGPU_INDEX_MAX_SPLIT")
     # 5,000 sketches that all hold one hash: a run of 5,000 > the run limit
     n = 5000
@@ -450,6 +452,9 @@ def test_index_kernel_many_partners_and_long_runs(monkeypatch):
     monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
     with ga.Context(k=21, sketch_size=s) as ctx:
         assert as_tuples(ctx.pairs(sk, lens, np.float32(0.01))) == exp
+        # (one attempt per output-buffer pass: every one abandoned for the gate kernel)
+        paths = ctx.pair_paths()
+        assert paths["index"] == 0 and paths["index_abandoned"] >= 1 and paths["gate"] == paths["index_abandoned"]
 
 
 def test_many_runs_index_and_run_table_errors(gpu_ctx):
@@ -589,4 +594,6 @@ def test_index_kernel_shared_top_bits(monkeypatch, top):
         exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
         with ga.Context(k=21, sketch_size=s) as ctx:
             assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, thr
+            # the mixed runs are split by the index itself (no gate fallback)
+            assert ctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0}
         assert thr > 0.5 or len(exp) > 0

@@ -207,6 +207,8 @@ def test_row_range_index_partners_across_members(min_ani):
     for devs in ([0], [0, 0], [0, 0, 0], [0] * 5):
         with ga.Context(k=21, sketch_size=1000, devices=devs) as ctx:
             assert as_tuples(ctx.pairs(sk, lens, np.float32(min_ani))) == exp, devs
+            paths = ctx.pair_paths()  # one index call per member, none abandoned
+            assert paths["index"] == len(devs) and paths["index_abandoned"] == 0 and paths["gate"] == 0, paths
 
 
 def test_precluster_shards_mixed_lengths_s10000_1_vs_3_devices():
