@@ -43,11 +43,6 @@ constexpr uint32_t kMap = 1u << kMapLog2;  // LDS partner map slots per row
 constexpr uint32_t kMapFull = kMap * 3 / 4;
 constexpr int kScanThreads = 1024;
 constexpr uint32_t kXcds = 8;  // MI355X: 8 XCDs, each with its own L2
-// run pass: write every entry's runinfo slot (1; no clear needed) or only
-// those of runs of g >= 2 after clearing the evaluated rows (0)
-#ifndef GG_RUNINFO_ALL
-#define GG_RUNINFO_ALL 1
-#endif
 
 // #{ e < n : a[e] <= x }, a ascending
 __device__ __forceinline__ uint32_t count_le(const uint64_t* __restrict__ a, uint32_t n, uint64_t x) {
@@ -295,11 +290,7 @@ __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restr
       atomicOr(overflow, 1u);
       continue;
     }
-#if GG_RUNINFO_ALL
     runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] = g >= 2 ? ((uint64_t)start | ((uint64_t)g << 32)) : 0ull;
-#else
-    if (g >= 2) runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] = (uint64_t)start | ((uint64_t)g << 32);
-#endif
     if (lo != lo0) atomicOr(&mixed[start >> 5], 1u << (start & 31));
   }
 }
@@ -507,19 +498,10 @@ hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_
   e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out,
                                          (int)total, 0, (int)end_bit, st);
   if (e != hipSuccess) return e;
-#if GG_RUNINFO_ALL
-  // (runinfo needs no clearing: the run pass writes the slot of every entry
-  // it sees, which includes every entry of every evaluated row)
-#else
-  // runinfo of the evaluated rows (all rows, or [r0, r1) for the row-range
-  // index: other rows' slots are written by the run pass but never read)
-  if (b.bloom)
-    e = hipMemsetAsync(b.runinfo + (size_t)b.r0 * b.stride, 0, (size_t)(b.r1 - b.r0) * b.stride * sizeof(uint64_t),
-                       st);
-  else
-    e = hipMemsetAsync(b.runinfo, 0, (size_t)b.n * b.stride * sizeof(uint64_t), st);
-  if (e != hipSuccess) return e;
-#endif
+  // runinfo needs no clearing: the run pass writes the slot of every entry it
+  // sees, which includes every entry of every evaluated row (writing only the
+  // g >= 2 slots after a clear of the evaluated rows measured slower: C5 pairs
+  // phase 10.35 vs 9.98 ms, profiles/r03_d/runinfo_g2_memset_c5.json)
   e = hipMemsetAsync(b.mixed, 0, ((total + 31) / 32) * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   const uint64_t waves = (total + 63) / 64;

@@ -34,11 +34,11 @@ namespace {
 constexpr int kGroup = 4;  // k-mers per tau-check branch (1 or 2: within noise, profiles/r02_k1_group_defer_ab/)
 // K1 workgroup size.  The LDS holds the murmur tables (19 KB at k = 21) once
 // per workgroup and one candidate queue per wave; at 256 threads that is
-// 24.5 KB, six workgroups per CU, six waves per SIMD.
-#ifndef GG_K1_BLOCK
-#define GG_K1_BLOCK 256
-#endif
-constexpr int kBlock = GG_K1_BLOCK;
+// 24.5 KB, six workgroups per CU, six waves per SIMD.  512 threads (seven
+// waves per SIMD, VGPR-bound), also with 128-entry queues, measured the same
+// (C3 K1 47.02 / 46.89 vs 47.14 ms, C5 65.02 / 64.04 vs 65.19 / 64.38 ms:
+// profiles/r03_b/k1_block512*).
+constexpr int kBlock = 256;
 // min waves per SIMD forced on the register allocator: 7 (72 VGPRs, 4 dwords
 // spilled at k = 21) beats the unconstrained 76 VGPRs / 6 waves with the
 // candidate queue (C3 K1 49.3 -> 49.1 ms, C5 78.7 -> 77.9 ms)
@@ -296,10 +296,7 @@ __device__ __forceinline__ void insert_candidate(uint64_t* __restrict__ tab,
 // must stay fully unrolled, and the lanes of a wave diverge at run
 // boundaries): a push takes a position with ds_add; a push that finds the
 // ring full inserts directly; a drain hands out entries with ds_add too.
-#ifndef GG_K1_QUEUE
-#define GG_K1_QUEUE 64
-#endif
-constexpr uint32_t kQueue = GG_K1_QUEUE;
+constexpr uint32_t kQueue = 64;
 constexpr uint32_t kQueueDrain = kQueue / 2;
 struct CandQueue {
   uint64_t f1[kQueue], f2[kQueue];  // fmix64_mid of h1 / h2: the exact test runs at the drain
@@ -647,8 +644,6 @@ template <int K>
 hipError_t launch_k(const SketchLaunch& a, int grid, hipStream_t st) {
   // finch always hashes with seed 0 (src/finch.rs:41); that variant drops the
   // seed terms from the murmur3 block at compile time.
-  // (grid counts 256-thread workgroups)
-  grid = std::max(1, (int)((int64_t)grid * 256 / kBlock));
   if (a.seed == 0)
     hipLaunchKernelGGL((sketch_candidates_kernel<K, true>), dim3(grid), dim3(kBlock), 0, st, a);
   else
