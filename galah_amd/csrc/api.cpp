@@ -940,6 +940,7 @@ gg_ctx* gg_create(int kmer_length, uint32_t sketch_size, uint64_t hash_seed, int
 
 void gg_destroy(gg_ctx* ctx) {
   if (!ctx) return;
+  ctx->pool.reset();  // (member threads idle between calls: joined here)
   for (gg_ctx* m : ctx->devs) gg_destroy(m);
   if (!ctx->devs.empty()) {
     delete ctx;

@@ -52,17 +52,19 @@ std::vector<gg_ctx*> members(gg_ctx* c) { return c->devs.empty() ? std::vector<g
 template <class F>
 gg_status on_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, F&& f) {
   std::vector<gg_status> st(ms.size(), GG_OK);
-  auto run = [&](size_t i) {
+  const std::function<void(size_t)> run = [&](size_t i) {
     if (hipSetDevice(ms[i]->device) != hipSuccess) {
       st[i] = fail(ms[i], GG_ERR_HIP, "hipSetDevice failed");
       return;
     }
     st[i] = f(i, ms[i]);
   };
-  std::vector<std::thread> th;
-  for (size_t i = 1; i < ms.size(); ++i) th.emplace_back(run, i);
-  run(0);
-  for (auto& t : th) t.join();
+  if (ms.size() == 1) {
+    run(0);
+  } else {
+    if (!c->pool || c->pool->size() != ms.size()) c->pool.reset(new MemberPool(ms.size()));
+    c->pool->run(run);
+  }
   for (size_t i = 0; i < ms.size(); ++i)
     if (st[i] != GG_OK) {
       if (ms[i] != c) c->err = ms[i]->err;

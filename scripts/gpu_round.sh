@@ -61,6 +61,23 @@ for st in $STAGES; do
         python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-files || exit $?
       PMC_SETS=2 run pmc_k1_c5 400 bash scripts/pmc.sh "$OUT/pmc_k1_c5" sketch_candidates -- \
         python3 bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline --no-files || exit $? ;;
+    k1trace)  # first K1 launch of one C3 and one C5 step, per library in K1_LIBS
+      for lib in ${K1_LIBS:-galah_amd/lib/libgalahgpu.so}; do
+        tag=$(basename $(dirname $lib))
+        for cfg in c3 c5; do
+          GALAHGPU_LIB=$lib run k1trace_${tag}_$cfg 300 rocprofv3 --kernel-trace --output-format csv \
+            -d "$OUT/k1trace_${tag}_$cfg" -o t -- python3 -u bench.py --config $cfg --steps 1 --warmup 0 \
+            --no-cpu-baseline --no-files || exit $?
+        done
+      done ;;
+    overhead)  # fixed cost of a multi-member call: 1 vs 8 members of GPU 0 on a small set, HEAD lib and ALT_LIB
+      for lib in galah_amd/lib/libgalahgpu.so ${ALT_LIB:-}; do
+        tag=$(basename $(dirname $lib))
+        for devs in 0 0,0,0,0,0,0,0,0; do
+          GALAHGPU_LIB=$lib bench overhead_${tag}_$(echo $devs | tr -cd , | wc -c) 300 --devices $devs --genomes 2000 \
+            --genome-len 200000 --steps 30 --warmup 5 --no-cpu-baseline --no-files
+        done
+      done ;;
     ubench3)
       run ubench_vop3 120 ./scripts/ubench_vop3 8 && run ubench_vop3_w1 120 ./scripts/ubench_vop3 1 || exit $? ;;
     ubench)
