@@ -471,12 +471,14 @@ class Context:
 
     def pair_paths(self):
         """Which pair kernel ran, counted since the context was created
-        (gg_pair_paths): {"index", "index_abandoned", "gate", "other"}."""
-        out = np.zeros(4, np.uint64)
+        (gg_pair_paths): {"index", "index_abandoned", "gate", "other",
+        "index_full_sort"} ("index_full_sort" counts the index calls that
+        used the full sort instead of the bucketed build)."""
+        out = np.zeros(5, np.uint64)
         st = _L.gg_pair_paths(self._c, _ptr(out))
         if st != GG_OK:
             raise self._err(st)
-        return dict(zip(("index", "index_abandoned", "gate", "other"), (int(x) for x in out)))
+        return dict(zip(("index", "index_abandoned", "gate", "other", "index_full_sort"), (int(x) for x in out)))
 
     def timing_read(self, kernel):
         """-> dict(ms, launches, work) summed since timing_enable."""

@@ -623,8 +623,6 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   GG_HIP(c, scratch_t(c, "idx_vals_out", total, &b.vals_out));
   GG_HIP(c, scratch_t(c, "idx_runinfo", total, &b.runinfo));
   GG_HIP(c, scratch_t(c, "idx_mixed", (total + 31) / 32, &b.mixed));
-  b.sort_tmp_bytes = index_sort_tmp_bytes(total);
-  GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
   GG_HIP(c, scratch_t(c, "idx_flags", 4, &b.flags));
   // rows of the tile rows that intersect [tb, te)
   uint64_t I0 = UINT64_MAX, I1 = 0, t = 0;
@@ -657,6 +655,12 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
     b.r1 = r1;
     GG_HIP(c, scratch_t(c, "idx_bloom", (size_t)1 << (lg - 5), &b.bloom));
   }
+  // Bucketed build (default; GALAHGPU_INDEX_BUCKETS=0: the full 32-bit sort
+  // and the run pass).  A bucket too large for LDS falls back to the full
+  // build, from a fresh fill (its keys differ, and the bucket pass
+  // overwrote keys_in).
+  const char* be = getenv("GALAHGPU_INDEX_BUCKETS");
+  b.mix = !(be && *be == '0');
   uint64_t info[2] = {0, 0};
   uint32_t kept = 0;
   GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_fill(b, st); }));
@@ -671,11 +675,32 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   while (bits < 64 && (maxh >> bits) != 0) ++bits;
   const uint32_t sh = bits > 32 ? bits - 32 : 0;
   const uint32_t end_bit = std::max(1u, bits - sh);
-  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
-                         [&] { return index_build(b, n_entries, sh, end_bit, st); }));
-  uint32_t flags[1] = {0};
-  GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  GG_HIP(c, hipStreamSynchronize(st));
+  uint32_t flags[4] = {0, 0, 0, 0};
+  bool built = false;
+  if (b.mix) {
+    b.bucket_bits = index_bucket_bits(n_entries);
+    b.sort_tmp_bytes = index_sort_tmp_bytes(n_entries, index_bucket_sort_begin(n_entries, b.bucket_bits), 32);
+    GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
+    GG_HIP(c, scratch_t(c, "idx_bstart", ((size_t)1 << b.bucket_bits) + 1, &b.bstart));
+    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
+                           [&] { return index_build_buckets(b, n_entries, st); }));
+    GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof flags, hipMemcpyDeviceToHost, st));
+    GG_HIP(c, hipStreamSynchronize(st));
+    built = flags[3] == 0;
+    if (!built) {  // refill with the full build's keys (the row-range kept count comes out the same)
+      b.mix = false;
+      GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st, [&] { return index_fill(b, st); }));
+    }
+  }
+  if (!built) {
+    ++c->pair_paths[GG_PATH_INDEX_FULL_SORT];
+    b.sort_tmp_bytes = index_sort_tmp_bytes(n_entries, 0, end_bit);
+    GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
+    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
+                           [&] { return index_build(b, n_entries, sh, end_bit, st); }));
+    GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(c, hipStreamSynchronize(st));
+  }
   if (flags[0]) return GG_OK;  // a run longer than kMaxRun
   *used = true;
   IndexLaunch a;

@@ -114,7 +114,7 @@ struct gg_ctx {
   // a member's copy streams, one per peer it gathers rows from (created on
   // first use), so the copies from different peers run at once
   std::vector<hipStream_t> peer_streams;
-  uint64_t pair_paths[GG_PATH_COUNT] = {0, 0, 0, 0};  // gg_pair_paths
+  uint64_t pair_paths[GG_PATH_COUNT] = {};  // gg_pair_paths
   hipStream_t copy_stream = nullptr;  // run-table uploads beside work on `stream` (sketch_core)
   hipEvent_t copy_done = nullptr;
   // host threads for file ingest (<= 0: gg_pack_files' default)

@@ -233,6 +233,14 @@ struct IndexBuild {
   uint32_t* bloom = nullptr;  // [1 << (bloom_log2 - 5)] words
   uint32_t bloom_log2 = 0;
   uint32_t r0 = 0, r1 = 0;
+  // Bucketed build (index_build_buckets; mix: the fill keys entries by
+  // m = h * odd constant instead of the hash's top bits): the sort orders
+  // only the top bucket_bits of m, bstart[b] is bucket b's first sorted
+  // entry ([2^bucket_bits + 1]), and one workgroup per bucket groups equal
+  // hashes in LDS.  A bucket too large for that sets flags[3].
+  bool mix = false;
+  uint32_t* bstart = nullptr;
+  uint32_t bucket_bits = 0;
 };
 struct IndexLaunch {
   const uint64_t* sketches;
@@ -262,7 +270,11 @@ struct IndexLaunch {
 // entries, already keyed: index_build sorts them)
 hipError_t index_fill(const IndexBuild& b, hipStream_t st);
 hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_t end_bit, hipStream_t st);
-size_t index_sort_tmp_bytes(uint64_t total);
+hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, hipStream_t st);
+uint32_t index_bucket_bits(uint64_t total);
+uint32_t index_bucket_sort_begin(uint64_t total, uint32_t bucket_bits);
+// temporary storage of the sort over bits [begin_bit, end_bit)
+size_t index_sort_tmp_bytes(uint64_t total, uint32_t begin_bit, uint32_t end_bit);
 hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st);
 
 // synth.hip

@@ -427,11 +427,18 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
   __syncthreads();
 
   const uint64_t seed = SEED0 ? 0ull : a.seed;
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   uint32_t r = 0;
 
-  const uint64_t send = a.seg0 + a.n_segs;
-  for (uint64_t sg = a.seg0 + (uint64_t)blockIdx.x * kBlock + threadIdx.x; sg < send; sg += stride) {
+  // Workgroup b sweeps its own contiguous chunk of segments, kBlock at a
+  // time (a wave's 64 lanes read consecutive windows).  A lane's next
+  // segment is then kBlock segments on, in the same run or a few runs later,
+  // so find_run's forward search is one or two loads; with a grid stride
+  // it was ~50 genomes on (C3: ~14 dependent loads per segment, C5's 3.6M
+  // runs ~30).
+  const uint64_t per_wg = (a.n_segs + (uint64_t)gridDim.x * kBlock - 1) / ((uint64_t)gridDim.x * kBlock) * kBlock;
+  const uint64_t c0 = a.seg0 + (uint64_t)blockIdx.x * per_wg;
+  const uint64_t send = min(a.seg0 + a.n_segs, c0 + per_wg);
+  for (uint64_t sg = c0 + threadIdx.x; sg < send; sg += kBlock) {
     r = find_run(a.run_sstart, a.n_runs, sg, r);
     const gg_run run = a.runs[r];
     const uint32_t k0 = (uint32_t)(sg - a.run_sstart[r]) * (uint32_t)kSeg;  // first k-mer of the segment in the run

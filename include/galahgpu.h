@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 3u
+#define GG_ABI_VERSION 4u
 
 typedef enum gg_status {
   GG_OK = 0,
@@ -331,8 +331,18 @@ gg_status gg_timing_read(gg_ctx* ctx, int kernel, gg_kernel_stats* out);
  * abandoned for the gate kernel (a hash shared by more sketches than its run
  * limit, or a row's partners overflowing its map), paths[2] the gate kernel
  * ran (after an abandoned index too), paths[3] another form (table / merge,
- * GALAHGPU_PAIRS_KERNEL). */
-enum { GG_PATH_INDEX = 0, GG_PATH_INDEX_ABANDONED = 1, GG_PATH_GATE = 2, GG_PATH_OTHER = 3, GG_PATH_COUNT = 4 };
+ * GALAHGPU_PAIRS_KERNEL), paths[4] of the index calls in paths[0], those
+ * whose index was built by the full 32-bit sort and run pass instead of the
+ * bucketed build (a bucket too large for LDS, or GALAHGPU_INDEX_BUCKETS=0).
+ * paths must hold GG_PATH_COUNT values. */
+enum {
+  GG_PATH_INDEX = 0,
+  GG_PATH_INDEX_ABANDONED = 1,
+  GG_PATH_GATE = 2,
+  GG_PATH_OTHER = 3,
+  GG_PATH_INDEX_FULL_SORT = 4,
+  GG_PATH_COUNT = 5
+};
 gg_status gg_pair_paths(const gg_ctx* ctx, uint64_t* paths);
 
 /* ---- benchmark support: synthetic clustered genomes on device ---------- */

@@ -125,6 +125,7 @@ def check_config(ctx, d_words, runs, n, s, thr, genome_bases, spot):
     after = ctx.pair_paths()
     assert after["index"] == before["index"] + 1 and after["index_abandoned"] == before["index_abandoned"]
     assert after["gate"] == before["gate"]
+    assert after["index_full_sort"] == before["index_full_sort"]  # the bucketed build
     got = {(int(a), int(b)): (int(c), int(t)) for a, b, c, t in P}
     assert len(got) == len(P)
     # every within-cluster pair against the oracle
@@ -178,7 +179,8 @@ def check_config(ctx, d_words, runs, n, s, thr, genome_bases, spot):
             with ga.Context(k=21, sketch_size=s) as mctx:
                 bands[kern] = device_pairs(mctx, d_sk, d_len, n, tb, te, thr)
                 if kern == "index":
-                    assert mctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0}
+                    assert mctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0,
+                                                 "index_full_sort": 0}
     finally:
         if old is None:
             os.environ.pop("GALAHGPU_PAIRS_KERNEL")

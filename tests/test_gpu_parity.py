@@ -434,7 +434,8 @@ def test_index_kernel_many_partners_and_long_runs(monkeypatch):
             with ga.Context(k=21, sketch_size=s) as ctx:
                 assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, (thr, split)
                 if split == "0":  # 2,999 partners never fit one map: abandoned for the gate kernel
-                    assert ctx.pair_paths() == {"index": 0, "index_abandoned": 1, "gate": 1, "other": 0}
+                    assert ctx.pair_paths() == {"index": 0, "index_abandoned": 1, "gate": 1, "other": 0,
+                                                "index_full_sort": 0}
         monkeypatch.delenv("GALAHGPU_INDEX_MAX_SPLIT")
     # 5,000 sketches that all hold one hash: a run of 5,000 > the run limit
     n = 5000
@@ -569,13 +570,16 @@ def test_host_sketch_run_table_checked_before_split():
                 assert lens[g] == len(exp) and (sk[g][:lens[g]] == exp).all(), (devs, g)
 
 
+@pytest.mark.parametrize("buckets", ["1", "0"])
 @pytest.mark.parametrize("top", [2**50, 2**64 - 1, 2**31])
-def test_index_kernel_shared_top_bits(monkeypatch, top):
+def test_index_kernel_shared_top_bits(monkeypatch, top, buckets):
     """The index sorts by the top 32 significant bits of each hash and carries
     the low word: hashes that differ only below those bits share a key and
     must be split into their own runs (clusters of values within 2^12 of
     each other, rows mixing them, the largest hash setting the key shift;
-    top = 2^31 leaves whole hashes as keys).  Equal to the oracle."""
+    top = 2^31 leaves whole hashes as keys).  Equal to the oracle, with the
+    bucketed build (default: ~2,000 entries of one cluster in one bucket)
+    and with the full sort and run pass (GALAHGPU_INDEX_BUCKETS=0)."""
     rng = np.random.default_rng(31)
     n, s = 400, 300
     anchors = rng.integers(0, top // 2, 60, dtype=np.uint64)
@@ -589,11 +593,39 @@ def test_index_kernel_shared_top_bits(monkeypatch, top):
         sk[i, :len(v)] = v
         lens[i] = len(v)
     monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
+    monkeypatch.setenv("GALAHGPU_INDEX_BUCKETS", buckets)
     for thr in (0.5, 0.9):
         o = oracle.pairs(sk, lens.astype(np.int32), np.float32(thr))
         exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
         with ga.Context(k=21, sketch_size=s) as ctx:
             assert as_tuples(ctx.pairs(sk, lens, np.float32(thr))) == exp, thr
             # the mixed runs are split by the index itself (no gate fallback)
-            assert ctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0}
+            assert ctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0,
+                                        "index_full_sort": int(buckets == "0")}
         assert thr > 0.5 or len(exp) > 0
+
+
+def test_index_bucket_overflow_falls_back_to_full_sort(monkeypatch):
+    """One hash held by 3,500 sketches: its bucket of the bucketed build holds
+    more entries than one workgroup groups in LDS (3,072), while the run
+    (3,500) is within the run limit (4,096).  The host rebuilds the index
+    with the full sort and the run pass: same pairs as the oracle (the 300
+    sketches that also share a second hash pass at 0.87, the others do not),
+    the index still used (not the gate kernel)."""
+    rng = np.random.default_rng(44)
+    n, s = 3500, 20
+    sk = np.zeros((n, s), np.uint64)
+    lens = np.zeros(n, np.uint32)
+    a, b = np.uint64(2**40 + 5), np.uint64(2**50 + 11)
+    for i in range(n):
+        shared = [a, b] if i < 300 else [a]
+        v = np.unique(np.concatenate([shared, rng.integers(2**52, 2**63, s, dtype=np.uint64)]))[:s]
+        sk[i, :len(v)] = v
+        lens[i] = len(v)
+    monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
+    o = oracle.pairs(sk, lens.astype(np.int32), np.float32(0.87))
+    exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+    assert len(exp) == 300 * 299 // 2
+    with ga.Context(k=21, sketch_size=s) as ctx:
+        assert as_tuples(ctx.pairs(sk, lens, np.float32(0.87))) == exp
+        assert ctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0, "index_full_sort": 1}
