@@ -660,12 +660,17 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   // build, from a fresh fill (its keys differ, and the bucket pass
   // overwrote keys_in).
   const char* be = getenv("GALAHGPU_INDEX_BUCKETS");
-  b.mix = !(be && *be == '0');
+  b.bucket = !(be && *be == '0');
+  if (b.bucket) {
+    GG_HIP(c, scratch_t(c, "idx_hist", kIndexCoarse, &b.hist));
+    GG_HIP(c, scratch_t(c, "idx_bbase", kIndexCoarse + 1, &b.bbase));
+  }
   uint64_t info[2] = {0, 0};
-  uint32_t kept = 0;
+  uint32_t kept = 0, nbuckets = 0;
   GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_fill(b, st); }));
   GG_HIP(c, hipMemcpyAsync(info, b.info, sizeof info, hipMemcpyDeviceToHost, st));
   if (b.bloom) GG_HIP(c, hipMemcpyAsync(&kept, b.flags + 1, sizeof kept, hipMemcpyDeviceToHost, st));
+  if (b.bucket) GG_HIP(c, hipMemcpyAsync(&nbuckets, b.bbase + kIndexCoarse, sizeof nbuckets, hipMemcpyDeviceToHost, st));
   GG_HIP(c, hipStreamSynchronize(st));
   // keys = the top 32 significant bits of each hash (the low 32 bits travel
   // with the entry): shift by the bits of the largest hash beyond 32 (the
@@ -677,24 +682,23 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   const uint32_t end_bit = std::max(1u, bits - sh);
   uint32_t flags[4] = {0, 0, 0, 0};
   bool built = false;
-  if (b.mix) {
-    b.bucket_bits = index_bucket_bits(n_entries);
-    b.sort_tmp_bytes = index_sort_tmp_bytes(n_entries, index_bucket_sort_begin(n_entries, b.bucket_bits), 32);
+  if (b.bucket) {
+    b.sort_tmp_bytes = index_bucket_sort_tmp_bytes(n_entries, nbuckets);
     GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
-    GG_HIP(c, scratch_t(c, "idx_bstart", ((size_t)1 << b.bucket_bits) + 1, &b.bstart));
+    GG_HIP(c, scratch_t(c, "idx_bstart", (size_t)nbuckets + 1, &b.bstart));
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
-                           [&] { return index_build_buckets(b, n_entries, st); }));
+                           [&] { return index_build_buckets(b, n_entries, nbuckets, st); }));
     GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof flags, hipMemcpyDeviceToHost, st));
     GG_HIP(c, hipStreamSynchronize(st));
     built = flags[3] == 0;
     if (!built) {  // refill with the full build's keys (the row-range kept count comes out the same)
-      b.mix = false;
+      b.bucket = false;
       GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st, [&] { return index_fill(b, st); }));
     }
   }
   if (!built) {
     ++c->pair_paths[GG_PATH_INDEX_FULL_SORT];
-    b.sort_tmp_bytes = index_sort_tmp_bytes(n_entries, 0, end_bit);
+    b.sort_tmp_bytes = index_sort_tmp_bytes(n_entries, end_bit);
     GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
                            [&] { return index_build(b, n_entries, sh, end_bit, st); }));

@@ -233,14 +233,17 @@ struct IndexBuild {
   uint32_t* bloom = nullptr;  // [1 << (bloom_log2 - 5)] words
   uint32_t bloom_log2 = 0;
   uint32_t r0 = 0, r1 = 0;
-  // Bucketed build (index_build_buckets; mix: the fill keys entries by
-  // m = h * odd constant instead of the hash's top bits): the sort orders
-  // only the top bucket_bits of m, bstart[b] is bucket b's first sorted
-  // entry ([2^bucket_bits + 1]), and one workgroup per bucket groups equal
-  // hashes in LDS.  A bucket too large for that sets flags[3].
-  bool mix = false;
+  // Bucketed build (bucket): index_fill also histograms every entry by the
+  // top 12 bits of its top-aligned key (hist [4096]) and splits each coarse
+  // bin into sub-ranges of ~equal counts (bbase [4097], bbase[4096] = the
+  // number of buckets, at most 2^16); the fill keys entries by bucket
+  // (vals hold the 32-bit entries), the sort orders the bucket ids, bstart
+  // [buckets + 1] bounds every bucket, and one workgroup per bucket groups
+  // equal hashes in LDS.  A bucket too large for that sets flags[3].
+  bool bucket = false;
+  uint32_t* hist = nullptr;
+  uint32_t* bbase = nullptr;
   uint32_t* bstart = nullptr;
-  uint32_t bucket_bits = 0;
 };
 struct IndexLaunch {
   const uint64_t* sketches;
@@ -270,11 +273,12 @@ struct IndexLaunch {
 // entries, already keyed: index_build sorts them)
 hipError_t index_fill(const IndexBuild& b, hipStream_t st);
 hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_t end_bit, hipStream_t st);
-hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, hipStream_t st);
-uint32_t index_bucket_bits(uint64_t total);
-uint32_t index_bucket_sort_begin(uint64_t total, uint32_t bucket_bits);
-// temporary storage of the sort over bits [begin_bit, end_bit)
-size_t index_sort_tmp_bytes(uint64_t total, uint32_t begin_bit, uint32_t end_bit);
+hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nbuckets, hipStream_t st);
+// temporary storage of the full build's sort over bits [0, end_bit), and of
+// the bucketed build's
+size_t index_sort_tmp_bytes(uint64_t total, uint32_t end_bit);
+size_t index_bucket_sort_tmp_bytes(uint64_t total, uint32_t nbuckets);
+constexpr uint32_t kIndexCoarse = 4096;  // coarse bins of the bucketed build
 hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st);
 
 // synth.hip

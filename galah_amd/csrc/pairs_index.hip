@@ -43,21 +43,36 @@ constexpr uint32_t kMap = 1u << kMapLog2;  // LDS partner map slots per row
 constexpr uint32_t kMapFull = kMap * 3 / 4;
 constexpr int kScanThreads = 1024;
 constexpr uint32_t kXcds = 8;  // MI355X: 8 XCDs, each with its own L2
-constexpr uint64_t kMix = 0x9E3779B97F4A7C15ull;  // bucketed build: m = h * kMix (see index_bucket_kernel)
 
-// The sort key and carried word of hash h for entry e (row << kbits | k):
-// the top 32 significant bits of h (shift sh) and h's low word, or, for the
-// bucketed build (mix), m = h * kMix split into its high and low words.
-__device__ __forceinline__ void entry_key(uint64_t h, uint32_t sh, bool mix, uint32_t e, uint32_t& key,
-                                          uint64_t& val) {
-  if (mix) {
-    const uint64_t m = h * kMix;
-    key = (uint32_t)(m >> 32);
-    val = (m << 32) | e;
-  } else {
-    key = (uint32_t)(h >> sh);
-    val = (h << 32) | e;
-  }
+// Key shape of the index (index_scan_kernel leaves the largest hash in
+// info[1]): the sort key of the full build is the top 32 significant bits
+// of a hash (h >> sh, end_bit significant bits); the bucketed build
+// top-aligns that key (norm = 32 - end_bit) and splits it into a coarse bin
+// (top 12 bits) and the 20 bits below.
+struct KeyShape {
+  uint32_t sh, norm;
+};
+__device__ __forceinline__ KeyShape key_shape(unsigned long long maxh) {
+  const uint32_t bits = maxh ? 64u - (uint32_t)__builtin_clzll(maxh) : 0u;
+  const uint32_t sh = bits > 32 ? bits - 32 : 0u;
+  const uint32_t eb = bits - sh > 1u ? bits - sh : 1u;
+  return KeyShape{sh, 32u - eb};
+}
+
+// Bucketed build: 4096 coarse bins of the top-aligned key, each split into
+// nsub = ceil(count / per) equal sub-ranges (bbase[c] = first bucket of bin c,
+// bbase[4096] = buckets).  bucket_of is monotone in the hash and equal
+// hashes share a bucket; the buckets hold ~per entries whatever the shape of
+// the hash distribution (C5's sketches of 0.5-12 Mbp genomes put 25x more
+// entries near 0 than near the largest hash).
+constexpr uint32_t kCoarseBits = 12;
+constexpr uint32_t kCoarse = 1u << kCoarseBits;
+__device__ __forceinline__ uint32_t bucket_of(uint64_t h, KeyShape ks, const uint32_t* __restrict__ bbase) {
+  const uint32_t key = (uint32_t)(h >> ks.sh) << ks.norm;
+  const uint32_t c = key >> (32 - kCoarseBits);
+  const uint32_t rel = key & ((1u << (32 - kCoarseBits)) - 1u);
+  const uint32_t b0 = bbase[c], ns = bbase[c + 1] - b0;
+  return b0 + (uint32_t)(((uint64_t)rel * ns) >> (32 - kCoarseBits));
 }
 
 // #{ e < n : a[e] <= x }, a ascending
@@ -111,20 +126,94 @@ __global__ __launch_bounds__(kScanThreads) void index_scan_kernel(const uint64_t
   }
 }
 
-// keys[e], vals[e] = entry_key of (hash, i << kbits | k) for entry
-// e = offs[i] + k of row i, k < len_i.
+// Entry e = offs[i] + k of row i (k < len_i), value i << kbits | k:
+//   full build:     keys[e] = h >> sh (32 bits), vals[e] = lo32(h) << 32 | value
+//   bucketed build: keys[e] = bucket_of(h),     vals32[e] = value
+template <bool BUCKET>
 __global__ __launch_bounds__(256) void index_fill_kernel(const uint64_t* __restrict__ sk,
                                                          const uint32_t* __restrict__ lens,
                                                          const uint64_t* __restrict__ offs, uint32_t n,
-                                                         uint32_t stride, uint32_t kbits, uint32_t sh, uint32_t mix,
+                                                         uint32_t stride, uint32_t kbits, uint32_t sh,
+                                                         const unsigned long long* __restrict__ info,
+                                                         const uint32_t* __restrict__ bbase,
                                                          uint32_t* __restrict__ keys, uint64_t* __restrict__ vals) {
+  const KeyShape ks = BUCKET ? key_shape(info[1]) : KeyShape{sh, 0u};
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t len = lens[i];
     const uint64_t* row = sk + (uint64_t)i * stride;
     const uint64_t o = offs[i];
-    for (uint32_t k = threadIdx.x; k < len; k += 256)
-      entry_key(row[k], sh, mix != 0, (i << kbits) | k, keys[o + k], vals[o + k]);
+    for (uint32_t k = threadIdx.x; k < len; k += 256) {
+      const uint64_t h = row[k];
+      const uint32_t v = (i << kbits) | k;
+      if (BUCKET) {
+        keys[o + k] = bucket_of(h, ks, bbase);
+        ((uint32_t*)vals)[o + k] = v;
+      } else {
+        keys[o + k] = (uint32_t)(h >> sh);
+        vals[o + k] = (h << 32) | v;
+      }
+    }
   }
+}
+
+// Coarse-bin histogram of every sketch entry (one LDS histogram per
+// workgroup over a contiguous slice of rows, merged with one atomic per
+// non-empty bin).
+__global__ __launch_bounds__(256) void bucket_hist_kernel(const uint64_t* __restrict__ sk,
+                                                          const uint32_t* __restrict__ lens, uint32_t n,
+                                                          uint32_t stride,
+                                                          const unsigned long long* __restrict__ info,
+                                                          uint32_t* __restrict__ hist) {
+  __shared__ uint32_t lh[kCoarse];
+  for (uint32_t x = threadIdx.x; x < kCoarse; x += 256) lh[x] = 0u;
+  __syncthreads();
+  const KeyShape ks = key_shape(info[1]);
+  const uint32_t i0 = (uint32_t)((uint64_t)n * blockIdx.x / gridDim.x);
+  const uint32_t i1 = (uint32_t)((uint64_t)n * (blockIdx.x + 1) / gridDim.x);
+  for (uint32_t i = i0; i < i1; ++i) {
+    const uint32_t len = lens[i];
+    const uint64_t* row = sk + (uint64_t)i * stride;
+    for (uint32_t k = threadIdx.x; k < len; k += 256)
+      atomicAdd(&lh[((uint32_t)(row[k] >> ks.sh) << ks.norm) >> (32 - kCoarseBits)], 1u);
+  }
+  __syncthreads();
+  for (uint32_t x = threadIdx.x; x < kCoarse; x += 256)
+    if (lh[x]) atomicAdd(&hist[x], lh[x]);
+}
+
+// bbase from the histogram: per = max(1024, ceil(entries / 60000)) entries
+// per bucket at most on average, so that there are at most 60000 + 4096
+// buckets (16-bit bucket ids: two digit passes of the sort).
+constexpr uint32_t kBaseThreads = 1024;
+__global__ __launch_bounds__(kBaseThreads) void bucket_base_kernel(const uint32_t* __restrict__ hist,
+                                                                   const unsigned long long* __restrict__ info,
+                                                                   uint32_t* __restrict__ bbase) {
+  __shared__ uint32_t wsum[kBaseThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const unsigned long long total = info[0];
+  const uint32_t per = (uint32_t)max(1024ull, (total + 59999ull) / 60000ull);
+  constexpr uint32_t q = kCoarse / kBaseThreads;
+  uint32_t ns[q], sum = 0;
+#pragma unroll
+  for (uint32_t x = 0; x < q; ++x) {
+    ns[x] = (hist[tid * q + x] + per - 1u) / per;
+    sum += ns[x];
+  }
+  uint32_t inc = sum;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[tid >> 6] = inc;
+  __syncthreads();
+  uint32_t run = inc - sum;
+  for (uint32_t w = 0; w < (tid >> 6); ++w) run += wsum[w];
+#pragma unroll
+  for (uint32_t x = 0; x < q; ++x) {
+    bbase[tid * q + x] = run;
+    run += ns[x];
+  }
+  if (tid == kBaseThreads - 1) bbase[kCoarse] = run;
 }
 
 // Row-range index.  A blocked Bloom filter of the hashes of rows [r0, r1):
@@ -164,19 +253,19 @@ __device__ __forceinline__ bool bloom_test(const uint32_t* __restrict__ bloom, u
 // *kept, and writes them in row order (a wave-ballot prefix per 256-entry
 // chunk).  The key shift comes from the largest hash (info[1], written by
 // index_scan_kernel before this launch), as the host computes it.
+template <bool BUCKET>
 __global__ __launch_bounds__(256) void index_fill_range_kernel(
     const uint64_t* __restrict__ sk, const uint32_t* __restrict__ lens, uint32_t n, uint32_t stride, uint32_t kbits,
-    const uint32_t* __restrict__ bloom, uint32_t log2b, uint32_t r0, uint32_t r1, uint32_t mix,
-    const unsigned long long* __restrict__ info, uint32_t* __restrict__ kept, uint32_t* __restrict__ keys,
-    uint64_t* __restrict__ vals) {
+    const uint32_t* __restrict__ bloom, uint32_t log2b, uint32_t r0, uint32_t r1,
+    const unsigned long long* __restrict__ info, const uint32_t* __restrict__ bbase, uint32_t* __restrict__ kept,
+    uint32_t* __restrict__ keys, uint64_t* __restrict__ vals) {
   __shared__ uint32_t wsum[4];
   __shared__ uint32_t base_s;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t i0 = (uint32_t)((uint64_t)n * blockIdx.x / gridDim.x);
   const uint32_t i1 = (uint32_t)((uint64_t)n * (blockIdx.x + 1) / gridDim.x);
-  const unsigned long long maxh = info[1];
-  const uint32_t bits = maxh ? 64u - (uint32_t)__builtin_clzll(maxh) : 0u;
-  const uint32_t sh = bits > 32 ? bits - 32 : 0u;
+  const KeyShape ks = key_shape(info[1]);
+  const uint32_t sh = ks.sh;
   uint32_t c = 0;
   for (uint32_t i = i0; i < i1; ++i) {
     const uint32_t len = lens[i];
@@ -208,7 +297,17 @@ __global__ __launch_bounds__(256) void index_fill_range_kernel(
       __syncthreads();
       uint32_t base = 0;
       for (uint32_t w = 0; w < wave; ++w) base += wsum[w];
-      if (keep) entry_key(h, sh, mix != 0, (i << kbits) | k, keys[o + base + before], vals[o + base + before]);
+      if (keep) {
+        const uint64_t at = o + base + before;
+        const uint32_t v = (i << kbits) | k;
+        if (BUCKET) {
+          keys[at] = bucket_of(h, ks, bbase);
+          ((uint32_t*)vals)[at] = v;
+        } else {
+          keys[at] = (uint32_t)(h >> sh);
+          vals[at] = (h << 32) | v;
+        }
+      }
       o += wsum[0] + wsum[1] + wsum[2] + wsum[3];
     }
   }
@@ -369,144 +468,142 @@ __global__ __launch_bounds__(256) void index_mixed_kernel(const uint32_t* __rest
   }
 }
 
-// Bucketed build.  Equal hashes only need to end up next to each other, in
-// any order, so the entries are bucketed by a function of the hash alone:
-// m = h * kMix (odd: a bijection of the 64-bit hashes) spreads every hash
-// distribution evenly (C5's sketches of 0.5-12 Mbp genomes put 25x more
-// entries near 0 than near the largest hash: buckets of hash bits overflow),
-// and the sort orders the entries by the top bucket_bits of m only (C5's
-// 10^8 entries: 16 bits, 2 digit passes instead of 4).  Key and carried word
-// hold m (key = high word, the value's high word = low word), so a bucket
-// still sees every hash whole.  bstart[b] = first sorted entry of bucket b
-// (bstart[nb] = total), written where the bucket changes (one coalesced
-// pass over the keys).
+// Bucketed build, after the sort by bucket (16-bit keys, entry values):
+// bstart[b] = first sorted entry of bucket b (bstart[nb] = total), written
+// where the bucket changes (one coalesced pass over the keys).
 constexpr uint32_t kBucketCap = 3072;    // entries of one bucket grouped in LDS
 constexpr uint32_t kBucketSlots = 4096;  // its LDS hash table (load <= 0.75)
 constexpr int kBucketThreads = 256;
 constexpr uint32_t kBucketPer = kBucketCap / kBucketThreads;
-static_assert(kBucketCap % kBucketThreads == 0 && kBucketSlots <= 4096 && kBucketCap < kBucketSlots,
+static_assert(kBucketCap % kBucketThreads == 0 && kBucketSlots % kBucketThreads == 0 && kBucketCap < 4096,
               "bucket table: group start and size packed as 12 + 12 bits");
 
 __global__ __launch_bounds__(256) void bucket_bounds_kernel(const uint32_t* __restrict__ keys, uint64_t total,
-                                                            uint32_t begin_bit, uint32_t nbuckets,
-                                                            uint32_t* __restrict__ bstart) {
+                                                            uint32_t nbuckets, uint32_t* __restrict__ bstart) {
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p <= total; p += (uint64_t)gridDim.x * 256) {
-    const uint32_t cur = p < total ? keys[p] >> begin_bit : nbuckets;
-    const uint32_t first = p > 0 ? (keys[p - 1] >> begin_bit) + 1u : 0u;
+    const uint32_t cur = p < total ? min(keys[p], nbuckets) : nbuckets;
+    const uint32_t first = p > 0 ? min(keys[p - 1], nbuckets) + 1u : 0u;
     for (uint32_t bk = first; bk <= cur; ++bk) bstart[bk] = (uint32_t)p;
   }
 }
 
-// One workgroup per bucket: its entries' m values go into an LDS hash table
-// (one atomicCAS per entry; a second atomic gives the entry its rank among
-// equal hashes), a scan over the table gives every hash its group's start in
-// the bucket, and every entry writes its ents word at start + rank and its
-// runinfo slot (group start and size g >= 2, or 0), as index_runs_kernel
-// does.  No sort inside the bucket and no split of mixed runs: m is compared
-// whole.  A bucket over kBucketCap entries sets flags[3] and the host
-// rebuilds with the full sort.
+// One workgroup per bucket.  Each entry reads its hash from its sketch row
+// (buckets are ranges of hash values, swept in order by the workgroups of
+// one XCD, so every row is read forward and its runinfo written forward, a
+// few lines at a time, which the XCD's L2 gathers), and equal hashes meet in
+// an LDS hash table: one atomicCAS per entry (2^64 - 1 has a slot of its own,
+// the empty marker being that value), a second atomic gives the entry its
+// rank among equal hashes, a scan over the table gives every hash its
+// group's start, and every entry writes its ents word at start + rank and
+// its runinfo slot (group start and size g >= 2, or 0) as index_runs_kernel
+// does.  A bucket over kBucketCap entries sets flags[3] (the host rebuilds
+// with the full sort).
 __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
-    const uint32_t* __restrict__ keys, const uint64_t* __restrict__ vals, const uint32_t* __restrict__ bstart,
-    uint32_t nbuckets, uint64_t total, uint32_t stride, uint32_t kbits, uint32_t max_run,
-    uint64_t* __restrict__ runinfo, uint32_t* __restrict__ ents, uint32_t* __restrict__ flags) {
+    const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ bstart, uint32_t nbuckets,
+    uint32_t per_xcd, uint64_t total, const uint64_t* __restrict__ sk, uint32_t stride, uint32_t kbits,
+    uint32_t max_run, uint64_t* __restrict__ runinfo, uint32_t* __restrict__ ents, uint32_t* __restrict__ flags) {
   __shared__ uint64_t tkey[kBucketSlots];
-  __shared__ uint32_t tcnt[kBucketSlots];  // group size; after the scan start << 12 | size
+  __shared__ uint32_t tcnt[kBucketSlots + 1];  // group size; after the scan start << 12 | size
   __shared__ uint32_t wsum[kBucketThreads / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t kmask = (1u << kbits) - 1u;
+  constexpr uint64_t none = ~0ull;
   constexpr uint32_t smask = kBucketSlots - 1u;
-  for (uint32_t bk = blockIdx.x; bk < nbuckets; bk += gridDim.x) {
-    const uint32_t lo = bstart[bk], hi = bstart[bk + 1], n = hi - lo;
-    if (lo > hi || hi > total) {  // (uniform) unsorted keys: the host rebuilds with the full sort
-      if (tid == 0) atomicOr(&flags[3], 2u);
-      continue;
+  // XCD-aware: the workgroups of XCD x (blockIdx % kXcds) take the x-th
+  // contiguous range of buckets, in order
+  const uint32_t bk = (blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
+  if (bk >= nbuckets) return;
+  const uint32_t lo = bstart[bk], hi = bstart[bk + 1], n = hi - lo;
+  if (lo > hi || hi > total) {  // unsorted keys: never read through
+    if (tid == 0) atomicOr(&flags[3], 2u);
+    return;
+  }
+  if (n == 0) return;
+  if (n == 1) {  // a hash no other entry shares
+    if (tid == 0) {
+      const uint32_t e = sorted[lo];
+      ents[lo] = e;
+      runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] = 0ull;
     }
-    if (n == 0) continue;
-    if (n == 1) {  // a hash no other entry shares
-      if (tid == 0) {
-        const uint32_t e = (uint32_t)vals[lo];
-        ents[lo] = e;
-        runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] = 0ull;
-      }
-      continue;
-    }
-    if (n > kBucketCap) {  // (uniform) the host rebuilds with the full sort
-      if (tid == 0) atomicOr(&flags[3], 1u);
-      continue;
-    }
-    // every m of this bucket has bucket bits bk; a value without them marks
-    // an empty slot
-    const uint64_t none = bk ? 0ull : ~0ull;
-    for (uint32_t x = tid; x < kBucketSlots; x += kBucketThreads) {
-      tkey[x] = none;
-      tcnt[x] = 0u;
-    }
-    __syncthreads();
-    uint32_t slot[kBucketPer], rank[kBucketPer], ent[kBucketPer];
+    return;
+  }
+  if (n > kBucketCap) {
+    if (tid == 0) atomicOr(&flags[3], 1u);
+    return;
+  }
+  for (uint32_t x = tid; x <= kBucketSlots; x += kBucketThreads) {
+    if (x < kBucketSlots) tkey[x] = none;
+    tcnt[x] = 0u;
+  }
+  __syncthreads();
+  uint32_t slot[kBucketPer], rank[kBucketPer], ent[kBucketPer];
 #pragma unroll
-    for (uint32_t r = 0; r < kBucketPer; ++r) {
-      const uint32_t q = tid + r * kBucketThreads;
-      slot[r] = 0u;
-      rank[r] = 0u;
-      ent[r] = 0u;
-      if (q < n) {
-        const uint64_t v = vals[lo + q];
-        const uint64_t m = ((uint64_t)keys[lo + q] << 32) | (v >> 32);
-        uint32_t s = (uint32_t)(m >> 20) & smask;
+  for (uint32_t r = 0; r < kBucketPer; ++r) {
+    const uint32_t q = tid + r * kBucketThreads;
+    slot[r] = 0u;
+    rank[r] = 0u;
+    ent[r] = 0u;
+    if (q < n) {
+      const uint32_t e = sorted[lo + q];
+      const uint64_t h = sk[(uint64_t)(e >> kbits) * stride + (e & kmask)];
+      uint32_t s = kBucketSlots;
+      if (h != none) {
+        s = (uint32_t)(h ^ (h >> 29)) & smask;
         for (;;) {
           const unsigned long long old =
-              atomicCAS((unsigned long long*)&tkey[s], (unsigned long long)none, (unsigned long long)m);
-          if (old == none || old == m) break;
+              atomicCAS((unsigned long long*)&tkey[s], (unsigned long long)none, (unsigned long long)h);
+          if (old == none || old == h) break;
           s = (s + 1u) & smask;
         }
-        slot[r] = s;
-        rank[r] = atomicAdd(&tcnt[s], 1u);
-        ent[r] = (uint32_t)v;
       }
+      slot[r] = s;
+      rank[r] = atomicAdd(&tcnt[s], 1u);
+      ent[r] = e;
     }
+  }
+  __syncthreads();
+  // exclusive scan of the group sizes in slot order (slot kBucketSlots, the
+  // hash 2^64 - 1, last): each thread 16 consecutive slots, then the wave
+  // and workgroup totals
+  {
+    constexpr uint32_t per = kBucketSlots / kBucketThreads;
+    const uint32_t s0 = tid * per;
+    uint32_t sum = 0;
+#pragma unroll
+    for (uint32_t x = 0; x < per; ++x) sum += tcnt[s0 + x];
+    uint32_t inc = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    if (lane == 63) wsum[wave] = inc;
     __syncthreads();
-    // exclusive scan of the group sizes in slot order: each thread 16
-    // consecutive slots, the wave and then the workgroup totals
-    {
-      constexpr uint32_t per = kBucketSlots / kBucketThreads;
-      const uint32_t s0 = tid * per;
-      uint32_t sum = 0;
+    uint32_t run = inc - sum;
+    for (uint32_t w = 0; w < wave; ++w) run += wsum[w];
 #pragma unroll
-      for (uint32_t x = 0; x < per; ++x) sum += tcnt[s0 + x];
-      uint32_t inc = sum;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o);
-        if (lane >= (uint32_t)o) inc += y;
-      }
-      if (lane == 63) wsum[wave] = inc;
-      __syncthreads();
-      uint32_t run = inc - sum;
-      for (uint32_t w = 0; w < wave; ++w) run += wsum[w];
-#pragma unroll
-      for (uint32_t x = 0; x < per; ++x) {
-        const uint32_t g = tcnt[s0 + x];
-        tcnt[s0 + x] = (run << 12) | g;
-        run += g;
-      }
+    for (uint32_t x = 0; x < per; ++x) {
+      const uint32_t g = tcnt[s0 + x];
+      tcnt[s0 + x] = (run << 12) | g;
+      run += g;
     }
-    __syncthreads();
+    if (tid == kBucketThreads - 1) tcnt[kBucketSlots] |= run << 12;
+  }
+  __syncthreads();
 #pragma unroll
-    for (uint32_t r = 0; r < kBucketPer; ++r) {
-      const uint32_t q = tid + r * kBucketThreads;
-      if (q < n) {
-        const uint32_t t = tcnt[slot[r]];
-        const uint32_t start = t >> 12, g = t & 0xFFFu;
-        const uint32_t e = ent[r];
-        ents[lo + start + rank[r]] = e;
-        if (g > max_run) {
-          atomicOr(&flags[0], 1u);
-          continue;
-        }
-        runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] =
-            g >= 2 ? ((uint64_t)(lo + start) | ((uint64_t)g << 32)) : 0ull;
+  for (uint32_t r = 0; r < kBucketPer; ++r) {
+    const uint32_t q = tid + r * kBucketThreads;
+    if (q < n) {
+      const uint32_t t = tcnt[slot[r]];
+      const uint32_t start = t >> 12, g = t & 0xFFFu;
+      const uint32_t e = ent[r];
+      ents[lo + start + rank[r]] = e;
+      if (g > max_run) {
+        atomicOr(&flags[0], 1u);
+        continue;
       }
+      runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] =
+          g >= 2 ? ((uint64_t)(lo + start) | ((uint64_t)g << 32)) : 0ull;
     }
-    __syncthreads();  // (the table is cleared for the next bucket)
   }
 }
 
@@ -625,24 +722,41 @@ hipError_t index_fill(const IndexBuild& b, hipStream_t st) {
   hipLaunchKernelGGL(index_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, b.sketches, b.lens, b.n, b.stride,
                      b.offs, (unsigned long long*)b.info);
   e = hipGetLastError();
-  if (e != hipSuccess || !b.bloom) return e;
+  if (e != hipSuccess) return e;
+  const unsigned long long* info = (const unsigned long long*)b.info;
+  if (b.bucket) {  // coarse-bin histogram of every entry -> bucket bases (bbase[kCoarse] = buckets)
+    e = hipMemsetAsync(b.hist, 0, kCoarse * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(bucket_hist_kernel, dim3(std::max(1u, std::min<uint32_t>(b.n, 1024))), dim3(256), 0, st,
+                       b.sketches, b.lens, b.n, b.stride, info, b.hist);
+    hipLaunchKernelGGL(bucket_base_kernel, dim3(1), dim3(kBaseThreads), 0, st, b.hist, info, b.bbase);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (!b.bloom) return hipSuccess;
   // row-range index: filter, then the kept entries (their count -> flags[1])
   e = hipMemsetAsync(b.bloom, 0, ((size_t)1 << b.bloom_log2) / 8, st);
   if (e != hipSuccess) return e;
   if (b.r1 > b.r0)
     hipLaunchKernelGGL(bloom_build_kernel, dim3(std::min<uint32_t>(b.r1 - b.r0, 16384)), dim3(256), 0, st,
                        b.sketches, b.lens, b.r0, b.r1, b.stride, b.bloom, b.bloom_log2);
-  hipLaunchKernelGGL(index_fill_range_kernel, dim3(std::max(1u, std::min<uint32_t>(b.n, 4096))), dim3(256), 0, st,
-                     b.sketches, b.lens, b.n, b.stride, b.kbits, b.bloom, b.bloom_log2, b.r0, b.r1, b.mix ? 1u : 0u,
-                     (const unsigned long long*)b.info, b.flags + 1, b.keys_in, b.vals_in);
+  const dim3 grid(std::max(1u, std::min<uint32_t>(b.n, 4096)));
+  if (b.bucket)
+    hipLaunchKernelGGL(index_fill_range_kernel<true>, grid, dim3(256), 0, st, b.sketches, b.lens, b.n, b.stride,
+                       b.kbits, b.bloom, b.bloom_log2, b.r0, b.r1, info, b.bbase, b.flags + 1, b.keys_in, b.vals_in);
+  else
+    hipLaunchKernelGGL(index_fill_range_kernel<false>, grid, dim3(256), 0, st, b.sketches, b.lens, b.n, b.stride,
+                       b.kbits, b.bloom, b.bloom_log2, b.r0, b.r1, info, nullptr, b.flags + 1, b.keys_in,
+                       b.vals_in);
   return hipGetLastError();
 }
 
 hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_t end_bit, hipStream_t st) {
   if (total == 0) return hipSuccess;
   if (!b.bloom)  // (the row-range index filled its kept entries in index_fill)
-    hipLaunchKernelGGL(index_fill_kernel, dim3(std::min<uint32_t>(b.n, 16384)), dim3(256), 0, st, b.sketches,
-                       b.lens, b.offs, b.n, b.stride, b.kbits, sh, 0u, b.keys_in, b.vals_in);
+    hipLaunchKernelGGL(index_fill_kernel<false>, dim3(std::min<uint32_t>(b.n, 16384)), dim3(256), 0, st,
+                       b.sketches, b.lens, b.offs, b.n, b.stride, b.kbits, sh, nullptr, nullptr, b.keys_in,
+                       b.vals_in);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   size_t bytes = b.sort_tmp_bytes;
@@ -670,58 +784,58 @@ hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_
   return hipGetLastError();
 }
 
-// Bucket bits: at most ~1,600 entries per bucket on average (C5's 10^8
-// entries: 16 bits, 2 digit passes; C3's 10^7: 13), so that the largest
-// bucket stays inside kBucketCap (m is uniform; equal hashes come in groups
-// of at most a cluster's size).
-uint32_t index_bucket_bits(uint64_t total) {
-  uint32_t d = 1;
-  while (d < 28 && (total >> d) > 1600) ++d;
-  return d;
+uint32_t index_bucket_key_bits(uint32_t nbuckets) {
+  uint32_t bits = 1;
+  while (bits < 32 && (nbuckets - 1u) >> bits) ++bits;
+  return bits;
 }
 
-// First key bit the bucketed build's sort orders.  rocPRIM (ROCm 7.2) sorts
-// up to 2^20 items with its merge-sort path, and that path returns unsorted
-// keys and mismatched values when begin_bit > 0 (scripts/sortchk_probe.hip:
-// profiles/r03_g/rocprim_partial_bits_sortchk.txt); above 2^20 the onesweep
-// path handles the bit range correctly.  Small inputs sort all 32 bits
-// (fully sorted keys are sorted by their top bits too).
-uint32_t index_bucket_sort_begin(uint64_t total, uint32_t bucket_bits) {
-  return total <= (1ull << 20) ? 0u : 32u - bucket_bits;
-}
-
-hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, hipStream_t st) {
-  if (total == 0) return hipSuccess;
+hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nbuckets, hipStream_t st) {
+  if (total == 0 || nbuckets == 0) return hipSuccess;
   if (!b.bloom)
-    hipLaunchKernelGGL(index_fill_kernel, dim3(std::min<uint32_t>(b.n, 16384)), dim3(256), 0, st, b.sketches,
-                       b.lens, b.offs, b.n, b.stride, b.kbits, 0u, 1u, b.keys_in, b.vals_in);
+    hipLaunchKernelGGL(index_fill_kernel<true>, dim3(std::min<uint32_t>(b.n, 16384)), dim3(256), 0, st, b.sketches,
+                       b.lens, b.offs, b.n, b.stride, b.kbits, 0u, (const unsigned long long*)b.info, b.bbase,
+                       b.keys_in, b.vals_in);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const uint32_t begin_bit = 32u - b.bucket_bits;
-  const uint32_t nbuckets = 1u << b.bucket_bits;
+  // bucket ids as keys, entries as values, every key bit sorted (bit 0 up:
+  // rocPRIM's merge-sort path, used up to 2^20 items, mis-sorts ranges that
+  // begin above bit 0; scripts/sortchk_probe.hip,
+  // profiles/r03_g/rocprim_partial_bits_sortchk.txt)
+  uint32_t* vin = (uint32_t*)b.vals_in;
+  uint32_t* vout = (uint32_t*)b.vals_out;
   size_t bytes = b.sort_tmp_bytes;
-  e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, b.keys_in, b.keys_out, b.vals_in, b.vals_out,
-                                         (int)total, (int)index_bucket_sort_begin(total, b.bucket_bits), 32, st);
+  e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, b.keys_in, b.keys_out, vin, vout, (int)total, 0,
+                                         (int)index_bucket_key_bits(nbuckets), st);
   if (e != hipSuccess) return e;
   // (every bucket start is written when the keys are sorted; a bucket whose
   // bounds come out inconsistent is reported, never read through)
   e = hipMemsetAsync(b.bstart, 0xFF, ((size_t)nbuckets + 1) * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(bucket_bounds_kernel, dim3((uint32_t)std::min<uint64_t>(16384, total / 256 + 1)), dim3(256), 0,
-                     st, b.keys_out, total, begin_bit, nbuckets, b.bstart);
+                     st, b.keys_out, total, nbuckets, b.bstart);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   // the entries land in keys_in (free after the sort), as with the run pass
-  hipLaunchKernelGGL(index_bucket_kernel, dim3(nbuckets), dim3(kBucketThreads), 0, st, b.keys_out, b.vals_out,
-                     b.bstart, nbuckets, total, b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in, b.flags);
+  const uint32_t per_xcd = (nbuckets + kXcds - 1) / kXcds;
+  hipLaunchKernelGGL(index_bucket_kernel, dim3(per_xcd * kXcds), dim3(kBucketThreads), 0, st, vout, b.bstart,
+                     nbuckets, per_xcd, total, b.sketches, b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in,
+                     b.flags);
   return hipGetLastError();
 }
 
-size_t index_sort_tmp_bytes(uint64_t total, uint32_t begin_bit, uint32_t end_bit) {
+size_t index_sort_tmp_bytes(uint64_t total, uint32_t end_bit) {
   size_t bytes = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                           (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)total, (int)begin_bit,
-                                           (int)end_bit);
+                                           (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)total, 0, (int)end_bit);
+  return bytes;
+}
+
+size_t index_bucket_sort_tmp_bytes(uint64_t total, uint32_t nbuckets) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)total, 0,
+                                           (int)index_bucket_key_bits(nbuckets));
   return bytes;
 }
 

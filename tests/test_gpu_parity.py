@@ -609,9 +609,9 @@ def test_index_bucket_overflow_falls_back_to_full_sort(monkeypatch):
     """One hash held by 3,500 sketches: its bucket of the bucketed build holds
     more entries than one workgroup groups in LDS (3,072), while the run
     (3,500) is within the run limit (4,096).  The host rebuilds the index
-    with the full sort and the run pass: same pairs as the oracle (the 300
-    sketches that also share a second hash pass at 0.87, the others do not),
-    the index still used (not the gate kernel)."""
+    with the full sort and the run pass: same pairs as the oracle (every pair
+    of the 300 sketches that also share a second hash passes at 0.87, not
+    every pair of the others), the index still used (not the gate kernel)."""
     rng = np.random.default_rng(44)
     n, s = 3500, 20
     sk = np.zeros((n, s), np.uint64)
@@ -625,7 +625,7 @@ def test_index_bucket_overflow_falls_back_to_full_sort(monkeypatch):
     monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
     o = oracle.pairs(sk, lens.astype(np.int32), np.float32(0.87))
     exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
-    assert len(exp) == 300 * 299 // 2
+    assert 300 * 299 // 2 <= len(exp) < n * (n - 1) // 2
     with ga.Context(k=21, sketch_size=s) as ctx:
         assert as_tuples(ctx.pairs(sk, lens, np.float32(0.87))) == exp
         assert ctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0, "index_full_sort": 1}
