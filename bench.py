@@ -490,6 +490,10 @@ def run_lib(a, world, rank):
                        "devices": devs},
             "sketch_gbases_per_s": round(total_bases / (phase["sketch"] / a.steps * 1e-3) / 1e9, 3),
             "phase_ms": {p: round(v / a.steps, 3) for p, v in phase.items()},
+            # device time per step of K1, its finalize and K2 (index build + pairs kernel), device 0
+            "kernel_ms_per_step": {"k1": round(kst["sketch"]["ms"] / a.steps, 3),
+                                   "finalize": round(kst["finalize"]["ms"] / a.steps, 3),
+                                   "k2": round(kst["pairs"]["ms"] / a.steps, 3)},
             "pairs_found": found,
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -509,12 +509,13 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
 // distinct values spread uniformly over [0, tau], so they are sorted by
 // buckets of the top bits below tau (a counting sort: LDS histogram, scan,
 // scatter into the genome's own candidate table in HBM, which the next pass
-// re-initialises anyway), then every bucket (~4 values) is sorted in
-// registers by one thread: ~4 passes over the candidates instead of a
-// bitonic network's log2(n)(log2(n)+1)/2 (105 at s = 10000; 6.7 -> ~1 ms
-// per C5 step).  Any block size up to kFinalizeMaxBlock.
+// re-initialises anyway, and back into LDS in bucket order), then every
+// value's place in its bucket (~4 values) is its rank among them: one thread
+// per value, a few LDS reads and compares (a register sorting network per
+// bucket ran 120 compare-exchanges whatever the bucket held, and the lanes
+// of a wave wait for the largest bucket among them).  Any block size up to
+// kFinalizeMaxBlock.
 constexpr int kFinalizeMaxBlock = 1024;
-constexpr uint32_t kBucketRegs = 16;  // bucket sizes sorted in registers (larger: in place)
 __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
     const uint32_t* __restrict__ slot_list, const uint32_t* __restrict__ slot_genome,
     const uint64_t* __restrict__ tau, uint64_t* __restrict__ table,
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
   // streamed file list land on their global rows)
   const uint32_t g = row_of ? row_of[slot_genome[slot]] : slot_genome[slot];
   const uint32_t f = flags[slot];
-  const uint32_t T = blockDim.x, tid = threadIdx.x;
+  const uint32_t T = blockDim.x, tid = threadIdx.x, lane = tid & 63;
   if (f & kFlagOverflow) {
     if (tid == 0) {
       status[slot] = kSketchRetrySmaller;
@@ -545,11 +546,42 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
   __syncthreads();
   uint64_t* tab = table + ((uint64_t)slot << cap_log2);
   const uint32_t cap = 1u << cap_log2;
-  for (uint32_t i = tid; i < cap; i += T) {
-    const uint64_t v = tab[i];
-    if (v != kEmpty) {
-      const uint32_t at = atomicAdd(&fill, 1u);
-      if (at < sort_pow2) buf[at] = v;
+  // gather: each thread 8 consecutive slots per step, all loads in flight
+  // at once (one workgroup per CU at s = 10000: with one load per thread per
+  // step the gather waited on HBM latency step after step), a wave prefix
+  // sum of the values found and one LDS atomic per wave
+  constexpr uint32_t kGatherV = 8;
+  const uint32_t steps = (cap + T * kGatherV - 1) / (T * kGatherV);
+  for (uint32_t it = 0; it < steps; ++it) {
+    const uint32_t i0 = (it * T + tid) * kGatherV;
+    uint64_t v[kGatherV];
+#pragma unroll
+    for (uint32_t j = 0; j < kGatherV; j += 2) {
+      if (i0 + j < cap) {
+        const ulonglong2 p = *(const ulonglong2*)(tab + i0 + j);
+        v[j] = p.x;
+        v[j + 1] = p.y;
+      } else {
+        v[j] = v[j + 1] = kEmpty;
+      }
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kGatherV; ++j) c += v[j] != kEmpty ? 1u : 0u;
+    uint32_t inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (lane >= (uint32_t)o) inc += y;
+    }
+    uint32_t base = 0;
+    if (lane == 63 && inc) base = atomicAdd(&fill, inc);
+    uint32_t at = __shfl(base, 63) + inc - c;
+#pragma unroll
+    for (uint32_t j = 0; j < kGatherV; ++j) {
+      if (v[j] != kEmpty) {
+        if (at < sort_pow2) buf[at] = v[j];
+        ++at;
+      }
     }
   }
   __syncthreads();
@@ -593,48 +625,33 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
     }
   }
   __syncthreads();
-  // scatter into the table (afterwards cnt[b] = end of bucket b)
+  // scatter into the table (afterwards cnt[b] = end of bucket b), then back
+  // into LDS in bucket order
   for (uint32_t e = tid; e < n; e += T) {
     const uint64_t v = buf[e];
     tab[atomicAdd(&cnt[(uint32_t)(v >> shift)], 1u)] = v;
   }
   __syncthreads();
-  // sort every bucket that starts below s; write the first s values
+  for (uint32_t e0 = tid; e0 < n; e0 += 4 * T) {
+    uint64_t v[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) v[j] = e0 + j * T < n ? tab[e0 + j * T] : 0ull;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+      if (e0 + j * T < n) buf[e0 + j * T] = v[j];
+  }
+  __syncthreads();
+  // every value of a bucket that starts below s: its rank in the bucket
   uint64_t* o = out + (uint64_t)g * s;
   const uint32_t m = min(s, n);
-  for (uint32_t b = tid; b < NB; b += T) {
+  for (uint32_t e = tid; e < n; e += T) {
+    const uint64_t v = buf[e];
+    const uint32_t b = (uint32_t)(v >> shift);
     const uint32_t b0 = b ? cnt[b - 1] : 0u, b1 = cnt[b];
-    if (b0 >= m || b1 == b0) continue;
-    const uint32_t c = b1 - b0;
-    if (c <= kBucketRegs) {
-      uint64_t r[kBucketRegs];
-#pragma unroll
-      for (uint32_t q = 0; q < kBucketRegs; ++q) r[q] = q < c ? tab[b0 + q] : kEmpty;
-      // insertion sort, unrolled over the register array
-#pragma unroll
-      for (uint32_t q = 1; q < kBucketRegs; ++q) {
-#pragma unroll
-        for (uint32_t w = q; w > 0; --w) {
-          const uint64_t x = r[w - 1], y = r[w];
-          r[w - 1] = x < y ? x : y;
-          r[w] = x < y ? y : x;
-        }
-      }
-#pragma unroll
-      for (uint32_t q = 0; q < kBucketRegs; ++q)
-        if (q < c && b0 + q < m) o[b0 + q] = r[q];
-    } else {  // a large bucket (never expected): insertion sort in place
-      for (uint32_t q = b0 + 1; q < b1; ++q) {
-        const uint64_t x = tab[q];
-        uint32_t w = q;
-        while (w > b0 && tab[w - 1] > x) {
-          tab[w] = tab[w - 1];
-          --w;
-        }
-        tab[w] = x;
-      }
-      for (uint32_t q = b0; q < b1 && q < m; ++q) o[q] = tab[q];
-    }
+    if (b0 >= m) continue;
+    uint32_t r = b0;
+    for (uint32_t q = b0; q < b1; ++q) r += buf[q] < v ? 1u : 0u;
+    if (r < m) o[r] = v;
   }
   uint32_t mm = m;
   if ((f & kFlagSawMax) && mm < s) {
