@@ -665,48 +665,6 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
     GG_HIP(c, scratch_t(c, "idx_hist", kIndexCoarse, &b.hist));
     GG_HIP(c, scratch_t(c, "idx_bbase", kIndexCoarse + 1, &b.bbase));
   }
-  uint64_t info[2] = {0, 0};
-  uint32_t kept = 0, nbuckets = 0;
-  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_fill(b, st); }));
-  GG_HIP(c, hipMemcpyAsync(info, b.info, sizeof info, hipMemcpyDeviceToHost, st));
-  if (b.bloom) GG_HIP(c, hipMemcpyAsync(&kept, b.flags + 1, sizeof kept, hipMemcpyDeviceToHost, st));
-  if (b.bucket) GG_HIP(c, hipMemcpyAsync(&nbuckets, b.bbase + kIndexCoarse, sizeof nbuckets, hipMemcpyDeviceToHost, st));
-  GG_HIP(c, hipStreamSynchronize(st));
-  // keys = the top 32 significant bits of each hash (the low 32 bits travel
-  // with the entry): shift by the bits of the largest hash beyond 32 (the
-  // row-range fill computed the same shift on the device)
-  const uint64_t n_entries = b.bloom ? kept : info[0], maxh = info[1];
-  uint32_t bits = 0;
-  while (bits < 64 && (maxh >> bits) != 0) ++bits;
-  const uint32_t sh = bits > 32 ? bits - 32 : 0;
-  const uint32_t end_bit = std::max(1u, bits - sh);
-  uint32_t flags[4] = {0, 0, 0, 0};
-  bool built = false;
-  if (b.bucket) {
-    b.sort_tmp_bytes = index_bucket_sort_tmp_bytes(n_entries, nbuckets);
-    GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
-    GG_HIP(c, scratch_t(c, "idx_bstart", (size_t)nbuckets + 1, &b.bstart));
-    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
-                           [&] { return index_build_buckets(b, n_entries, nbuckets, st); }));
-    GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof flags, hipMemcpyDeviceToHost, st));
-    GG_HIP(c, hipStreamSynchronize(st));
-    built = flags[3] == 0;
-    if (!built) {  // refill with the full build's keys (the row-range kept count comes out the same)
-      b.bucket = false;
-      GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st, [&] { return index_fill(b, st); }));
-    }
-  }
-  if (!built) {
-    ++c->pair_paths[GG_PATH_INDEX_FULL_SORT];
-    b.sort_tmp_bytes = index_sort_tmp_bytes(n_entries, end_bit);
-    GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
-    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
-                           [&] { return index_build(b, n_entries, sh, end_bit, st); }));
-    GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    GG_HIP(c, hipStreamSynchronize(st));
-  }
-  if (flags[0]) return GG_OK;  // a run longer than kMaxRun
-  *used = true;
   IndexLaunch a;
   a.sketches = d_sk;
   a.lens = d_lens;
@@ -718,7 +676,7 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   a.tile_begin = tb;
   a.tile_end = te;
   a.runinfo = b.runinfo;
-  a.vals = b.keys_in;  // the run pass leaves the run members' entries there
+  a.vals = b.keys_in;  // the build leaves the run members' entries there
   a.cmin = d_cmin;
   a.sufmin = d_sufmin;
   a.tmax = 2 * c->s;
@@ -732,14 +690,84 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
     a.max_split_log2 = e && *e ? (uint32_t)std::min(16, std::max(0, atoi(e))) : 16u;
   }
   a.overflow = b.flags + 2;  // (zeroed by index_fill)
-  // the output count before this launch: restored if a row overflows
+  // the output count before the pairs launch: restored if a row overflows
   uint64_t* d_count0;
   GG_HIP(c, scratch_t(c, "idx_count0", 1, &d_count0));
   GG_HIP(c, hipMemcpyAsync(d_count0, d_count, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
-  GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_index_pairs(a, r1 - r0, st); }));
-  GG_HIP(c, hipMemcpyAsync(flags, b.flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  GG_HIP(c, hipStreamSynchronize(st));
-  if (flags[0]) {  // a row's partners did not fit the LDS map: drop what this launch emitted
+  auto launch_pairs = [&](bool guarded) -> gg_status {
+    a.build_flags = guarded ? b.flags : nullptr;
+    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_index_pairs(a, r1 - r0, st); }));
+    return GG_OK;
+  };
+  uint64_t info[2] = {0, 0};
+  uint32_t kept = 0;
+  uint32_t flags[4] = {0, 0, 0, 0};
+  bool built = false, paired = false;
+  if (b.bucket && !b.bloom) {
+    // one host round trip: fill, bucketed build and the pairs kernel queued
+    // back to back (every row slot is a sort item, so the sort's size is
+    // known up front; the pairs kernel emits nothing if the build failed)
+    const uint32_t nbb = index_bucket_bound(total);
+    b.sort_tmp_bytes = index_bucket_sort_tmp_bytes(total);
+    GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
+    GG_HIP(c, scratch_t(c, "idx_bstart", (size_t)nbb + 1, &b.bstart));
+    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_fill(b, st); }));
+    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st, [&] { return index_build_buckets(b, total, nbb, st); }));
+    gg_status ps = launch_pairs(true);
+    if (ps != GG_OK) return ps;
+    GG_HIP(c, hipMemcpyAsync(info, b.info, sizeof info, hipMemcpyDeviceToHost, st));
+    GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof flags, hipMemcpyDeviceToHost, st));
+    GG_HIP(c, hipStreamSynchronize(st));
+    built = paired = flags[3] == 0;
+  } else {
+    uint32_t nbuckets = 0;
+    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_fill(b, st); }));
+    GG_HIP(c, hipMemcpyAsync(info, b.info, sizeof info, hipMemcpyDeviceToHost, st));
+    if (b.bloom) GG_HIP(c, hipMemcpyAsync(&kept, b.flags + 1, sizeof kept, hipMemcpyDeviceToHost, st));
+    if (b.bucket)
+      GG_HIP(c, hipMemcpyAsync(&nbuckets, b.bbase + kIndexCoarse, sizeof nbuckets, hipMemcpyDeviceToHost, st));
+    GG_HIP(c, hipStreamSynchronize(st));
+    if (b.bucket) {  // (row-range index: its kept entries, compacted)
+      b.sort_tmp_bytes = index_bucket_sort_tmp_bytes(kept);
+      GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
+      GG_HIP(c, scratch_t(c, "idx_bstart", (size_t)nbuckets + 1, &b.bstart));
+      GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
+                             [&] { return index_build_buckets(b, kept, nbuckets, st); }));
+      GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof flags, hipMemcpyDeviceToHost, st));
+      GG_HIP(c, hipStreamSynchronize(st));
+      built = flags[3] == 0;
+    }
+  }
+  // keys of the full build = the top 32 significant bits of each hash (the
+  // low 32 bits travel with the entry): shift by the bits of the largest hash
+  // beyond 32 (the row-range fill computed the same shift on the device)
+  const uint64_t n_entries = b.bloom ? kept : info[0], maxh = info[1];
+  uint32_t bits = 0;
+  while (bits < 64 && (maxh >> bits) != 0) ++bits;
+  const uint32_t sh = bits > 32 ? bits - 32 : 0;
+  const uint32_t end_bit = std::max(1u, bits - sh);
+  if (!built) {
+    if (b.bucket) {  // refill with the full build's keys (the row-range kept count comes out the same)
+      b.bucket = false;
+      GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st, [&] { return index_fill(b, st); }));
+    }
+    ++c->pair_paths[GG_PATH_INDEX_FULL_SORT];
+    b.sort_tmp_bytes = index_sort_tmp_bytes(n_entries, end_bit);
+    GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
+    GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
+                           [&] { return index_build(b, n_entries, sh, end_bit, st); }));
+    GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(c, hipStreamSynchronize(st));
+  }
+  if (flags[0]) return GG_OK;  // a run longer than kMaxRun (the pairs kernel, if queued, emitted nothing)
+  if (!paired) {
+    gg_status ps = launch_pairs(false);
+    if (ps != GG_OK) return ps;
+    GG_HIP(c, hipMemcpyAsync(&flags[2], b.flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(c, hipStreamSynchronize(st));
+  }
+  *used = true;
+  if (flags[2]) {  // a row's partners did not fit the LDS map: drop what the pairs launch emitted
     GG_HIP(c, hipMemcpyAsync(d_count, d_count0, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
     *used = false;
   }

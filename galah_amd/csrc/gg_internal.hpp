@@ -265,6 +265,7 @@ struct IndexLaunch {
   unsigned long long* count;
   uint32_t max_split_log2;  // a row's partners split into at most 2^this classes (16)
   uint32_t* overflow;       // set when a row's partners overflow the LDS map at the last split
+  const uint32_t* build_flags = nullptr;  // the build's flags: [0] or [3] set -> emit nothing
 };
 // Row offsets, the entry count and the largest hash (info[0], info[1]);
 // then, with the key shift and the sort's bit range, the keys, the sort and
@@ -273,11 +274,15 @@ struct IndexLaunch {
 // entries, already keyed: index_build sorts them)
 hipError_t index_fill(const IndexBuild& b, hipStream_t st);
 hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_t end_bit, hipStream_t st);
-hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nbuckets, hipStream_t st);
+// (bucketed build: total = sort items, n * stride unless the row-range fill
+// compacted its kept entries; nb_bound >= the buckets the device computed,
+// index_bucket_bound(entries))
+hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_bound, hipStream_t st);
+uint32_t index_bucket_bound(uint64_t entries);
 // temporary storage of the full build's sort over bits [0, end_bit), and of
 // the bucketed build's
 size_t index_sort_tmp_bytes(uint64_t total, uint32_t end_bit);
-size_t index_bucket_sort_tmp_bytes(uint64_t total, uint32_t nbuckets);
+size_t index_bucket_sort_tmp_bytes(uint64_t total);
 constexpr uint32_t kIndexCoarse = 4096;  // coarse bins of the bucketed build
 hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st);
 

@@ -426,14 +426,23 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
   rows.assign(M, Rows{});
   spans.clear();
   if (n_cached) *n_cached = 0;
-  // cache lookups (host)
+  // cache lookups (host), in chunks of paths; the rows of the entries found
+  // are kept compact, in row order (host memory grows with the hits, not
+  // with n * s)
   std::vector<uint8_t> hit(n, 0);
-  std::vector<uint64_t> hit_rows;
-  std::vector<uint32_t> hit_lens;
+  std::vector<uint64_t> hit_rows;  // [hits * s]
+  std::vector<uint32_t> hit_lens;  // [n]
   if (cache_dir) {
-    hit_rows.assign((size_t)n * s, 0);
     hit_lens.assign(n, 0);
-    cache_load_many(cache_dir, paths, n, c->k, s, c->seed, hit_rows.data(), hit_lens.data(), hit.data());
+    constexpr uint32_t kChunk = 1024;
+    std::vector<uint64_t> chunk((size_t)std::min(n, kChunk) * s);
+    for (uint32_t i0 = 0; i0 < n; i0 += kChunk) {
+      const uint32_t cn = std::min(kChunk, n - i0);
+      cache_load_many(cache_dir, paths + i0, cn, c->k, s, c->seed, chunk.data(), hit_lens.data() + i0,
+                      hit.data() + i0);
+      for (uint32_t i = 0; i < cn; ++i)
+        if (hit[i0 + i]) hit_rows.insert(hit_rows.end(), chunk.begin() + (size_t)i * s, chunk.begin() + (size_t)(i + 1) * s);
+    }
   }
   std::vector<const char*> miss;
   std::vector<uint32_t> miss_at;
@@ -444,11 +453,17 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
     }
   if (n_cached) *n_cached = n - (uint32_t)miss.size();
   std::vector<RowSpan> hit_spans;
+  std::vector<uint64_t> hit_first;  // per span: its first row's index among the hits
   {
     std::vector<uint32_t> h;
     for (uint32_t i = 0; i < n; ++i)
       if (hit[i]) h.push_back(i);
     spans_of(h, 0, hit_spans);
+    uint64_t before = 0;
+    for (const RowSpan& sp : hit_spans) {
+      hit_first.push_back(before);
+      before += sp.rows;
+    }
   }
   const uint32_t nm = (uint32_t)miss.size();
   // in-flight packed genomes: ~2 batches per member, at least 1 GiB
@@ -470,8 +485,9 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
     if (ms_ != GG_OK) return ms_;
     GG_HIP(m, hipMemsetAsync(r.sk, 0, (size_t)n * s * sizeof(uint64_t), m->stream));
     GG_HIP(m, hipMemsetAsync(r.len, 0, (size_t)n * sizeof(uint32_t), m->stream));
-    for (const RowSpan& sp : hit_spans) {  // cached rows straight from the host
-      GG_HIP(m, hipMemcpyAsync(r.sk + (size_t)sp.row0 * s, hit_rows.data() + (size_t)sp.row0 * s,
+    for (size_t hs = 0; hs < hit_spans.size(); ++hs) {  // cached rows straight from the host
+      const RowSpan& sp = hit_spans[hs];
+      GG_HIP(m, hipMemcpyAsync(r.sk + (size_t)sp.row0 * s, hit_rows.data() + hit_first[hs] * s,
                                (size_t)sp.rows * s * sizeof(uint64_t), hipMemcpyHostToDevice, m->stream));
       GG_HIP(m, hipMemcpyAsync(r.len + sp.row0, hit_lens.data() + sp.row0, sp.rows * sizeof(uint32_t),
                                hipMemcpyHostToDevice, m->stream));

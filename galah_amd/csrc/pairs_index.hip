@@ -66,6 +66,8 @@ __device__ __forceinline__ KeyShape key_shape(unsigned long long maxh) {
 // the hash distribution (C5's sketches of 0.5-12 Mbp genomes put 25x more
 // entries near 0 than near the largest hash).
 constexpr uint32_t kCoarseBits = 12;
+constexpr uint32_t kBucketPad = 0xFFFFu;
+constexpr uint32_t kBucketKeyBits = 16;  // sort key of an unused slot (every bucket id is below: <= 64096 buckets)
 constexpr uint32_t kCoarse = 1u << kCoarseBits;
 __device__ __forceinline__ uint32_t bucket_of(uint64_t h, KeyShape ks, const uint32_t* __restrict__ bbase) {
   const uint32_t key = (uint32_t)(h >> ks.sh) << ks.norm;
@@ -126,9 +128,11 @@ __global__ __launch_bounds__(kScanThreads) void index_scan_kernel(const uint64_t
   }
 }
 
-// Entry e = offs[i] + k of row i (k < len_i), value i << kbits | k:
-//   full build:     keys[e] = h >> sh (32 bits), vals[e] = lo32(h) << 32 | value
-//   bucketed build: keys[e] = bucket_of(h),     vals32[e] = value
+// Entry of row i, k < len_i, value i << kbits | k:
+//   full build:     at offs[i] + k, keys = h >> sh (32 bits), vals = lo32(h) << 32 | value
+//   bucketed build: at i * stride + k (every slot k < stride: the sort's item
+//                   count is known before the row lengths are), keys =
+//                   bucket_of(h) or kBucketPad past len_i, vals32 = value
 template <bool BUCKET>
 __global__ __launch_bounds__(256) void index_fill_kernel(const uint64_t* __restrict__ sk,
                                                          const uint32_t* __restrict__ lens,
@@ -141,14 +145,19 @@ __global__ __launch_bounds__(256) void index_fill_kernel(const uint64_t* __restr
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t len = lens[i];
     const uint64_t* row = sk + (uint64_t)i * stride;
+    if (BUCKET) {  // row-major slots i * stride + k, unused slots keyed past every bucket
+      const uint64_t o = (uint64_t)i * stride;
+      for (uint32_t k = threadIdx.x; k < stride; k += 256) {
+        keys[o + k] = k < len ? bucket_of(row[k], ks, bbase) : kBucketPad;
+        ((uint32_t*)vals)[o + k] = (i << kbits) | k;
+      }
+      continue;
+    }
     const uint64_t o = offs[i];
     for (uint32_t k = threadIdx.x; k < len; k += 256) {
       const uint64_t h = row[k];
       const uint32_t v = (i << kbits) | k;
-      if (BUCKET) {
-        keys[o + k] = bucket_of(h, ks, bbase);
-        ((uint32_t*)vals)[o + k] = v;
-      } else {
+      {
         keys[o + k] = (uint32_t)(h >> sh);
         vals[o + k] = (h << 32) | v;
       }
@@ -479,7 +488,9 @@ static_assert(kBucketCap % kBucketThreads == 0 && kBucketSlots % kBucketThreads 
               "bucket table: group start and size packed as 12 + 12 bits");
 
 __global__ __launch_bounds__(256) void bucket_bounds_kernel(const uint32_t* __restrict__ keys, uint64_t total,
-                                                            uint32_t nbuckets, uint32_t* __restrict__ bstart) {
+                                                            const uint32_t* __restrict__ nbuckets_p,
+                                                            uint32_t* __restrict__ bstart) {
+  const uint32_t nbuckets = *nbuckets_p;
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p <= total; p += (uint64_t)gridDim.x * 256) {
     const uint32_t cur = p < total ? min(keys[p], nbuckets) : nbuckets;
     const uint32_t first = p > 0 ? min(keys[p - 1], nbuckets) + 1u : 0u;
@@ -499,8 +510,8 @@ __global__ __launch_bounds__(256) void bucket_bounds_kernel(const uint32_t* __re
 // does.  A bucket over kBucketCap entries sets flags[3] (the host rebuilds
 // with the full sort).
 __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
-    const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ bstart, uint32_t nbuckets,
-    uint32_t per_xcd, uint64_t total, const uint64_t* __restrict__ sk, uint32_t stride, uint32_t kbits,
+    const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ nbuckets_p,
+    uint64_t total, const uint64_t* __restrict__ sk, uint32_t stride, uint32_t kbits,
     uint32_t max_run, uint64_t* __restrict__ runinfo, uint32_t* __restrict__ ents, uint32_t* __restrict__ flags) {
   __shared__ uint64_t tkey[kBucketSlots];
   __shared__ uint32_t tcnt[kBucketSlots + 1];  // group size; after the scan start << 12 | size
@@ -510,7 +521,11 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
   constexpr uint64_t none = ~0ull;
   constexpr uint32_t smask = kBucketSlots - 1u;
   // XCD-aware: the workgroups of XCD x (blockIdx % kXcds) take the x-th
-  // contiguous range of buckets, in order
+  // contiguous range of buckets, in order (the grid is a bound on the
+  // buckets, whose count the device computed)
+  const uint32_t nbuckets = *nbuckets_p;
+  const uint32_t per_xcd = (nbuckets + kXcds - 1) / kXcds;
+  if (blockIdx.x / kXcds >= per_xcd) return;
   const uint32_t bk = (blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
   if (bk >= nbuckets) return;
   const uint32_t lo = bstart[bk], hi = bstart[bk + 1], n = hi - lo;
@@ -536,16 +551,29 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
     tcnt[x] = 0u;
   }
   __syncthreads();
+  // the entries, then their hashes, all loads in flight before the first
+  // atomic (one dependent pair of loads per entry at a time left the
+  // workgroup waiting on memory latency)
   uint32_t slot[kBucketPer], rank[kBucketPer], ent[kBucketPer];
+  uint64_t hv[kBucketPer];
+#pragma unroll
+  for (uint32_t r = 0; r < kBucketPer; ++r) {
+    const uint32_t q = tid + r * kBucketThreads;
+    ent[r] = q < n ? sorted[lo + q] : 0u;
+  }
+#pragma unroll
+  for (uint32_t r = 0; r < kBucketPer; ++r) {
+    const uint32_t q = tid + r * kBucketThreads;
+    const uint32_t e = ent[r];
+    hv[r] = q < n ? sk[(uint64_t)(e >> kbits) * stride + (e & kmask)] : 0ull;
+  }
 #pragma unroll
   for (uint32_t r = 0; r < kBucketPer; ++r) {
     const uint32_t q = tid + r * kBucketThreads;
     slot[r] = 0u;
     rank[r] = 0u;
-    ent[r] = 0u;
     if (q < n) {
-      const uint32_t e = sorted[lo + q];
-      const uint64_t h = sk[(uint64_t)(e >> kbits) * stride + (e & kmask)];
+      const uint64_t h = hv[r];
       uint32_t s = kBucketSlots;
       if (h != none) {
         s = (uint32_t)(h ^ (h >> 29)) & smask;
@@ -558,7 +586,6 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
       }
       slot[r] = s;
       rank[r] = atomicAdd(&tcnt[s], 1u);
-      ent[r] = e;
     }
   }
   __syncthreads();
@@ -640,6 +667,9 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
   const uint32_t tid = threadIdx.x;
   const uint32_t i = a.row0 + blockIdx.x;
   if (i >= a.n) return;
+  // (launched right after the build, before the host has seen its flags: a
+  // run over the limit or a bucket too large left runinfo incomplete)
+  if (a.build_flags && (a.build_flags[0] | a.build_flags[3])) return;
   uint32_t jlo, jhi;
   row_columns(i, a.n, a.nb, a.tile_begin, a.tile_end, jlo, jhi);
   const uint32_t la = a.lens[i];
@@ -784,17 +814,12 @@ hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_
   return hipGetLastError();
 }
 
-uint32_t index_bucket_key_bits(uint32_t nbuckets) {
-  uint32_t bits = 1;
-  while (bits < 32 && (nbuckets - 1u) >> bits) ++bits;
-  return bits;
-}
-
-hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nbuckets, hipStream_t st) {
-  if (total == 0 || nbuckets == 0) return hipSuccess;
+hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_bound, hipStream_t st) {
+  if (total == 0 || nb_bound == 0) return hipSuccess;
+  const uint32_t* nbuckets_d = b.bbase + kCoarse;
   if (!b.bloom)
     hipLaunchKernelGGL(index_fill_kernel<true>, dim3(std::min<uint32_t>(b.n, 16384)), dim3(256), 0, st, b.sketches,
-                       b.lens, b.offs, b.n, b.stride, b.kbits, 0u, (const unsigned long long*)b.info, b.bbase,
+                       b.lens, nullptr, b.n, b.stride, b.kbits, 0u, (const unsigned long long*)b.info, b.bbase,
                        b.keys_in, b.vals_in);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -806,22 +831,25 @@ hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nbu
   uint32_t* vout = (uint32_t*)b.vals_out;
   size_t bytes = b.sort_tmp_bytes;
   e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, b.keys_in, b.keys_out, vin, vout, (int)total, 0,
-                                         (int)index_bucket_key_bits(nbuckets), st);
+                                         (int)kBucketKeyBits, st);
   if (e != hipSuccess) return e;
   // (every bucket start is written when the keys are sorted; a bucket whose
   // bounds come out inconsistent is reported, never read through)
-  e = hipMemsetAsync(b.bstart, 0xFF, ((size_t)nbuckets + 1) * sizeof(uint32_t), st);
+  e = hipMemsetAsync(b.bstart, 0xFF, ((size_t)nb_bound + 1) * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(bucket_bounds_kernel, dim3((uint32_t)std::min<uint64_t>(16384, total / 256 + 1)), dim3(256), 0,
-                     st, b.keys_out, total, nbuckets, b.bstart);
+                     st, b.keys_out, total, nbuckets_d, b.bstart);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   // the entries land in keys_in (free after the sort), as with the run pass
-  const uint32_t per_xcd = (nbuckets + kXcds - 1) / kXcds;
+  const uint32_t per_xcd = (nb_bound + kXcds - 1) / kXcds;
   hipLaunchKernelGGL(index_bucket_kernel, dim3(per_xcd * kXcds), dim3(kBucketThreads), 0, st, vout, b.bstart,
-                     nbuckets, per_xcd, total, b.sketches, b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in,
-                     b.flags);
+                     nbuckets_d, total, b.sketches, b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in, b.flags);
   return hipGetLastError();
+}
+
+uint32_t index_bucket_bound(uint64_t entries) {
+  return (uint32_t)std::min<uint64_t>(kBucketPad - 1, entries / 1024 + kCoarse);
 }
 
 size_t index_sort_tmp_bytes(uint64_t total, uint32_t end_bit) {
@@ -831,11 +859,11 @@ size_t index_sort_tmp_bytes(uint64_t total, uint32_t end_bit) {
   return bytes;
 }
 
-size_t index_bucket_sort_tmp_bytes(uint64_t total, uint32_t nbuckets) {
+size_t index_bucket_sort_tmp_bytes(uint64_t total) {
   size_t bytes = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                            (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)total, 0,
-                                           (int)index_bucket_key_bits(nbuckets));
+                                           (int)kBucketKeyBits);
   return bytes;
 }
 

@@ -54,6 +54,9 @@ for st in $STAGES; do
     prof_c5)
       run prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c5 -- \
         python3 -u bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
+    trace_c5)  # kernels and memory copies of one C5 step (timeline of the sketch phase)
+      run trace_c5 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/trace_c5" -o t -- \
+        python3 -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline || exit $? ;;
     pmc)  # PMC passes at HEAD (scripts/pmc_head.sh)
       run pmc 900 bash scripts/pmc_head.sh "$OUT/pmc" ${PMC_ARGS:-} || exit $? ;;
     pmc_k1)  # K1 instruction counters at C3 and C5 (scripts/pmc.sh passes 1-2)
