@@ -409,7 +409,8 @@ def run_lib(a, world, rank):
             g0, g1 = sharding.shard_range(N, M, m)
             torch.cuda.set_device(devs[m])
             d_words, runs, bases = make_shard(ctx.member(m), a, g0, g1, devs[m])
-            shards.append((d_words, runs, g1 - g0))
+            # the run table is input too: resident on the member's device like the words
+            shards.append((d_words, ga.device_runs(runs, "cuda:%d" % devs[m]), g1 - g0))
             keep.append(d_words)
             total_bases += bases
         sync_all(devs)

@@ -25,7 +25,7 @@ __all__ = [
     "GalahGpuError", "Context", "Packed", "pack_files", "pack_records",
     "ani_f32", "ani_f64", "parse_percentage", "pair_tiles", "pair_partition",
     "SortedPairGenomeDistanceCache", "PreclusterDistanceFinder",
-    "FinchPreclusterer", "distances", "PAIR_DTYPE", "LIB_PATH", "EXPORTED_SYMBOLS",
+    "FinchPreclusterer", "distances", "PAIR_DTYPE", "LIB_PATH", "EXPORTED_SYMBOLS", "device_runs",
     "partition_preclusters", "precluster_pairs", "preclusters", "LOCAL_PAIR_DTYPE",
     "sketch_cache_load", "sketch_cache_store",
 ]
@@ -355,6 +355,25 @@ def _dev_ptr(t):
     return t if isinstance(t, int) else t.data_ptr()
 
 
+def device_runs(runs, device):
+    """A run table (RUN_DTYPE records) copied to a device tensor of 16-byte
+    records, for sketch_device / precluster_shards to read in place."""
+    runs = np.ascontiguousarray(runs, dtype=RUN_DTYPE)
+    return torch.from_numpy(runs.view(np.uint8).copy()).to(device)
+
+
+def _runs_arg(runs):
+    """(pointer, count, object to keep alive) of a run table: a RUN_DTYPE
+    array (host memory) or a device tensor of 16-byte records."""
+    if hasattr(runs, "data_ptr") and getattr(runs, "is_cuda", False):
+        nbytes = runs.numel() * runs.element_size()
+        if nbytes % RUN_DTYPE.itemsize or not runs.is_contiguous():
+            raise ValueError("device run table: contiguous 16-byte records")
+        return (runs.data_ptr() if nbytes else None), nbytes // RUN_DTYPE.itemsize, runs
+    runs = np.ascontiguousarray(runs, dtype=RUN_DTYPE)
+    return runs.ctypes.data, len(runs), runs
+
+
 PHASES = ("sketch", "replicate", "pairs", "merge")  # gg_phase_times order
 
 
@@ -433,20 +452,22 @@ class Context:
         return dict(zip(PHASES, out.tolist()))
 
     def precluster_shards(self, shards, min_ani):
-        """shards: one (d_words tensor, runs RUN_DTYPE array, n_genomes) per
-        member, device-resident on that member's device -> (pairs sorted by
-        (i, j), ani f32), genomes numbered shard after shard."""
+        """shards: one (d_words tensor, runs, n_genomes) per member,
+        device-resident on that member's device (runs: a RUN_DTYPE array, or
+        a device tensor holding the same 16-byte records, see device_runs)
+        -> (pairs sorted by (i, j), ani f32), genomes numbered shard after
+        shard."""
         if len(shards) != self.device_count:
             raise ValueError("one shard per device")
         keep = []
         arr = (_Shard * len(shards))()
         for x, (d_words, runs, ng) in enumerate(shards):
-            runs = np.ascontiguousarray(runs, dtype=RUN_DTYPE)
+            rp, nr, runs = _runs_arg(runs)
             keep.append(runs)
             arr[x].d_words = _dev_ptr(d_words)
             arr[x].n_words = d_words.numel()
-            arr[x].runs = runs.ctypes.data
-            arr[x].n_runs = len(runs)
+            arr[x].runs = rp
+            arr[x].n_runs = nr
             arr[x].n_genomes = int(ng)
         pp, ap, cnt = _vp(), _vp(), _u64()
         st = _L.gg_precluster_shards(self._c, arr, ctypes.c_float(min_ani), ctypes.byref(pp), ctypes.byref(ap),
@@ -543,8 +564,8 @@ class Context:
 
     # -- device-resident API (torch tensors on this context's device) ---------
     def sketch_device(self, d_words, runs, n_genomes, d_out, d_lens, stream=None):
-        runs = np.ascontiguousarray(runs, dtype=RUN_DTYPE)
-        st = _L.gg_sketch_device(self._c, _dev_ptr(d_words), d_words.numel(), _ptr(runs), len(runs),
+        rp, nr, runs = _runs_arg(runs)
+        st = _L.gg_sketch_device(self._c, _dev_ptr(d_words), d_words.numel(), rp, nr,
                                  n_genomes, _dev_ptr(d_out), _dev_ptr(d_lens),
                                  None if stream is None else stream)
         if st != GG_OK:

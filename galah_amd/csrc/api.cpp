@@ -214,6 +214,17 @@ void parallel_chunks(uint64_t n, int T, F&& f) {
 
 // The status and message for the first bad run of a table (check_runs, and
 // the device check in sketch_core).
+// Device whose memory p points into, or -1 for host memory (a pointer HIP
+// does not know is host memory).
+int device_of(const void* p) {
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();  // (clears the sticky error of an unknown host pointer)
+    return -1;
+  }
+  return at.type == hipMemoryTypeDevice ? at.device : -1;
+}
+
 gg_status run_error(gg_ctx* c, const gg_run* runs, uint64_t first_bad, uint32_t n_genomes) {
   const gg_run& x = runs[first_bad];
   const uint32_t prev = first_bad ? runs[first_bad - 1].genome : 0u;
@@ -319,10 +330,28 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   GG_HIP(c, scratch_t(c, "run_index", 1 + 3 * ng1, &d_ix));  // bad, gr, grs, nk
   const size_t ix_tmp = run_index_tmp_bytes(n_runs);
   GG_HIP(c, scratch(c, "run_index_tmp", std::max<size_t>(ix_tmp, 16), &d_ix_tmp));
-  if (n_runs)
-    GG_HIP(c, hipMemcpyAsync(d_all_runs, runs, n_runs * sizeof(gg_run), hipMemcpyHostToDevice, c->copy_stream));
-  GG_HIP(c, hipEventRecord(c->copy_done, c->copy_stream));
-  GG_HIP(c, hipStreamWaitEvent(st, c->copy_done, 0));
+  // A run table already in this device's memory is indexed where it lies
+  // (another device's is copied peer to peer); the host mirror of a device
+  // table is made only if a retry pass or an error message needs it.
+  const int runs_dev = n_runs ? device_of(runs) : -1;
+  std::vector<gg_run> runs_mirror;
+  auto host_runs = [&]() -> const gg_run* {
+    if (runs_dev < 0) return runs;
+    if (runs_mirror.empty()) {
+      runs_mirror.resize(n_runs);
+      if (hipMemcpy(runs_mirror.data(), runs, n_runs * sizeof(gg_run), hipMemcpyDefault) != hipSuccess)
+        return nullptr;
+    }
+    return runs_mirror.data();
+  };
+  if (runs_dev == c->device) {
+    d_all_runs = const_cast<gg_run*>(runs);
+  } else {
+    if (n_runs)
+      GG_HIP(c, hipMemcpyAsync(d_all_runs, runs, n_runs * sizeof(gg_run), hipMemcpyDefault, c->copy_stream));
+    GG_HIP(c, hipEventRecord(c->copy_done, c->copy_stream));
+    GG_HIP(c, hipStreamWaitEvent(st, c->copy_done, 0));
+  }
   RunIndexDev xd;
   xd.runs = d_all_runs;
   xd.n_runs = n_runs;
@@ -342,7 +371,11 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   std::vector<uint64_t> hix(1 + 3 * ng1);
   GG_HIP(c, hipMemcpyAsync(hix.data(), d_ix, hix.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   GG_HIP(c, hipStreamSynchronize(st));
-  if (hix[0] != ~0ull) return run_error(c, runs, hix[0], n_genomes);
+  if (hix[0] != ~0ull) {
+    const gg_run* hr = host_runs();
+    if (!hr) return fail(c, GG_ERR_HIP, "copying the run table to the host failed");
+    return run_error(c, hr, hix[0], n_genomes);
+  }
   const uint64_t* gr = hix.data() + 1;
   const uint64_t* grs = hix.data() + 1 + ng1;
   const uint64_t* nk = hix.data() + 1 + 2 * ng1;
@@ -381,9 +414,11 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       uint64_t seg0 = grs[g0], sacc = grs[g0 + nb] - grs[g0];
       uint64_t kacc = 0;
       if (!all) {
+        const gg_run* runs_h = host_runs();
+        if (!runs_h) return fail(c, GG_ERR_HIP, "copying the run table to the host failed");
         std::vector<gg_run> sub;
         for (uint32_t slot : active)
-          for (uint64_t r = gr[g0 + slot]; r < gr[g0 + slot + 1]; ++r) sub.push_back(runs[r]);
+          for (uint64_t r = gr[g0 + slot]; r < gr[g0 + slot + 1]; ++r) sub.push_back(runs_h[r]);
         nr = sub.size();
         std::vector<uint64_t>& sub_rs = c->sstart_host;
         sub_rs.resize(nr + 1);

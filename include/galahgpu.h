@@ -166,7 +166,8 @@ void gg_packed_free(gg_packed* p);
 gg_status gg_sketch(gg_ctx* ctx, const gg_packed* packed,
                     uint64_t* out_hashes, uint32_t* out_lens);
 /* Device-resident variant: d_words / d_out / d_lens are device pointers;
- * runs are host metadata (copied by the library).  Synchronises stream
+ * runs is host memory (copied by the library) or device memory (a table
+ * on the context's device is read in place, no copy).  Synchronises stream
  * internally (retry planning reads per-genome status). */
 gg_status gg_sketch_device(gg_ctx* ctx, const uint32_t* d_words,
                            uint64_t n_words, const gg_run* runs,
@@ -211,9 +212,10 @@ gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths,
                               float** ani, uint64_t* n_out);
 
 /* One member's shard of device-resident packed genomes for
- * gg_precluster_shards: d_words lives on that member's device, runs are host
- * metadata whose genome field indexes the shard's n_genomes genomes.  The
- * global genome order is shard 0's genomes, then shard 1's, ... */
+ * gg_precluster_shards: d_words lives on that member's device, runs (host
+ * memory, or device memory: read in place on that member's device) index
+ * the shard's n_genomes genomes by their genome field.  The global genome
+ * order is shard 0's genomes, then shard 1's, ... */
 typedef struct gg_shard {
   const uint32_t* d_words;
   uint64_t n_words;

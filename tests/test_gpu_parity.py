@@ -629,3 +629,48 @@ def test_index_bucket_overflow_falls_back_to_full_sort(monkeypatch):
     with ga.Context(k=21, sketch_size=s) as ctx:
         assert as_tuples(ctx.pairs(sk, lens, np.float32(0.87))) == exp
         assert ctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0, "index_full_sort": 1}
+
+
+def test_device_run_table_same_as_host(gpu_ctx):
+    """A run table in device memory (gg_sketch_device / gg_precluster_shards
+    read it in place) gives the host table's sketches, through the retry
+    pass (genome 3's 300 runs repeat one stretch: its k-mer count
+    overestimates its distinct k-mers 300 times, so the first threshold is
+    too small and the genome is sketched again from the host mirror of the
+    table) and the run-table errors (the message names the same fault)."""
+    torch = torch_dev()
+    rng = np.random.default_rng(91)
+    n_words = 1 << 16
+    words = rng.integers(0, 2**32, n_words, dtype=np.uint64).astype(np.uint32)
+    d_words = torch.from_numpy(words.view(np.int32)).cuda()
+    n_genomes = 8
+    rows = []
+    base = 0
+    for g in range(n_genomes):
+        if g == 3:
+            rows += [(g, 400, 5000)] * 300
+            continue
+        for _ in range(20):
+            ln = int(rng.integers(30, 3000))
+            rows.append((g, ln, base))
+            base += ln + 7
+    assert base < n_words * 16
+    runs = np.array(rows, dtype=ga.RUN_DTYPE)
+    outs = []
+    for table in (runs, ga.device_runs(runs, "cuda")):
+        d_out = torch.zeros((n_genomes, 1000), dtype=torch.int64, device="cuda")
+        d_lens = torch.zeros(n_genomes, dtype=torch.int32, device="cuda")
+        gpu_ctx.sketch_device(d_words, table, n_genomes, d_out, d_lens)
+        torch.cuda.synchronize()
+        outs.append((d_out.cpu().numpy().view(np.uint64).copy(), d_lens.cpu().numpy().view(np.uint32).copy()))
+    (sk_h, ln_h), (sk_d, ln_d) = outs
+    assert (ln_h == ln_d).all() and (sk_h == sk_d).all()
+    for g in (0, 3, n_genomes - 1):
+        sel = runs[runs["genome"] == g]
+        exp = oracle.sketch_records([unpack_run(words, int(r["base"]), int(r["len"])) for r in sel])
+        assert ln_d[g] == len(exp) and (sk_d[g][:ln_d[g]] == exp).all(), g
+    assert ln_d[3] < 1000  # (one 400-base stretch: fewer distinct k-mers than s)
+    r = runs.copy()
+    r["len"][5] = 20
+    with pytest.raises(ga.GalahGpuError, match="shorter than k"):
+        gpu_ctx.sketch_device(d_words, ga.device_runs(r, "cuda"), n_genomes, d_out, d_lens)
