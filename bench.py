@@ -45,12 +45,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 CLK_GHZ = 2.4          # max engine clock (MI355X_MICROARCH.md chip parameters)
 N_SIMD = 256 * 4       # 256 CUs x 4 SIMDs
 # K1's VALU-issue ceiling (the kernel is bound by VALU issue; its input is
-# 0.25 B per k-mer, ~2% of HBM): profiles/r02_k1_issue_model.json, written by
+# 0.25 B per k-mer, ~2% of HBM): profiles/r03_k1_issue_model.json, written by
 # scripts/k1_issue_model.py from a rocprofv3 PMC pass over K1 at HEAD and the
 # per-opcode issue costs measured by scripts/ubench_dual.hip.  The model
 # records a fingerprint of K1's machine code; bench.py recomputes it from the
 # library it loads and flags the peak as stale when K1 has changed since.
-ISSUE_MODEL = os.path.join(ROOT, "profiles", "r02_k1_issue_model.json")
+ISSUE_MODEL = os.path.join(ROOT, "profiles", "r03_k1_issue_model.json")
 # K2's per-kernel PMC summary (VALU issue share, LDS-array utilisation, fabric
 # GB/s against the gfx950 peaks): scripts/k2_pmc.sh + scripts/k2_pmc_model.py
 K2_PMC = os.path.join(ROOT, "profiles", "r02_k2_pmc.json")
@@ -208,7 +208,7 @@ def roofline(kst_sk, kst_pr, s, config_note, config=None):
                      "%.1f GHz x 64 k-mers / (K1's VALU instructions per wave-k-mer, PMC at HEAD, x 2 cycles: "
                      "MI355X_MICROARCH.md's wave64 VALU issue); frac_issue_model prices the same instructions at the "
                      "issue cost of their class measured on this chip (simple 32-bit ~2.3 cycles, other 32-bit ~4.2, "
-                     "64-bit ~5.0; profiles/r02_k1_issue_model.json, DESIGN §4); traffic = HBM bytes per launch "
+                     "64-bit ~5.0; profiles/r03_k1_issue_model.json, DESIGN §4); traffic = HBM bytes per launch "
                      "from the PMC pass: FETCH_SIZE x 2 (the gfx950 factor, calibrated for 4-, 8- and 16-B loads by "
                      "scripts/ubench_fetch.hip) per k-mer x k-mers; %s"
                      % (CLK_GHZ, config_note)),
