@@ -731,6 +731,7 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   GG_HIP(c, hipMemcpyAsync(d_count0, d_count, sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
   auto launch_pairs = [&](bool guarded) -> gg_status {
     a.build_flags = guarded ? b.flags : nullptr;
+    a.ents16 = b.bucket && index_ents16(n);  // (b.bucket: the bucketed build made the index)
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_index_pairs(a, r1 - r0, st); }));
     return GG_OK;
   };

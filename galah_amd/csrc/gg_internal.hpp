@@ -266,6 +266,7 @@ struct IndexLaunch {
   uint32_t max_split_log2;  // a row's partners split into at most 2^this classes (16)
   uint32_t* overflow;       // set when a row's partners overflow the LDS map at the last split
   const uint32_t* build_flags = nullptr;  // the build's flags: [0] or [3] set -> emit nothing
+  bool ents16 = false;                     // vals holds 16-bit rows (bucketed build, index_ents16)
 };
 // Row offsets, the entry count and the largest hash (info[0], info[1]);
 // then, with the key shift and the sort's bit range, the keys, the sort and
@@ -285,6 +286,7 @@ size_t index_sort_tmp_bytes(uint64_t total, uint32_t end_bit);
 size_t index_bucket_sort_tmp_bytes(uint64_t total);
 constexpr uint32_t kIndexCoarse = 4096;  // coarse bins of the bucketed build
 hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st);
+bool index_ents16(uint32_t n);
 
 // synth.hip
 hipError_t launch_synth(uint32_t first_genome, uint32_t n_genomes, uint32_t genome_len,

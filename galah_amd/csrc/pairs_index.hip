@@ -512,7 +512,8 @@ __global__ __launch_bounds__(256) void bucket_bounds_kernel(const uint32_t* __re
 __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
     const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ nbuckets_p,
     uint64_t total, const uint64_t* __restrict__ sk, uint32_t stride, uint32_t kbits,
-    uint32_t max_run, uint64_t* __restrict__ runinfo, uint32_t* __restrict__ ents, uint32_t* __restrict__ flags) {
+    uint32_t max_run, uint64_t* __restrict__ runinfo, uint32_t* __restrict__ ents, uint32_t ents16,
+    uint32_t* __restrict__ flags) {
   __shared__ uint64_t tkey[kBucketSlots];
   __shared__ uint32_t tcnt[kBucketSlots + 1];  // group size; after the scan start << 12 | size
   __shared__ uint32_t wsum[kBucketThreads / 64];
@@ -537,7 +538,8 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
   if (n == 1) {  // a hash no other entry shares
     if (tid == 0) {
       const uint32_t e = sorted[lo];
-      ents[lo] = e;
+      if (ents16) ((uint16_t*)ents)[lo] = (uint16_t)(e >> kbits);
+      else ents[lo] = e;
       runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] = 0ull;
     }
     return;
@@ -623,7 +625,8 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
       const uint32_t t = tcnt[slot[r]];
       const uint32_t start = t >> 12, g = t & 0xFFFu;
       const uint32_t e = ent[r];
-      ents[lo + start + rank[r]] = e;
+      if (ents16) ((uint16_t*)ents)[lo + start + rank[r]] = (uint16_t)(e >> kbits);
+      else ents[lo + start + rank[r]] = e;
       if (g > max_run) {
         atomicOr(&flags[0], 1u);
         continue;
@@ -659,6 +662,7 @@ __device__ __forceinline__ uint32_t part_of(uint32_t j, uint32_t plog2) {
 // row's column interval, from the runs of its hashes, then the finch test.
 // Rows whose partners overflow the LDS map are redone in 2, 4, ... passes,
 // each counting one hash class of partners.
+template <bool E16>
 __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a) {
   __shared__ uint32_t mkey[kMap];  // partner + 1 (0 = empty)
   __shared__ uint32_t mcnt[kMap];
@@ -689,8 +693,7 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
       if (g < 2) continue;
       const uint32_t st = (uint32_t)info;
       for (uint32_t q = st; q < st + g; ++q) {
-        const uint32_t v = a.vals[q];
-        const uint32_t j = v >> a.kbits;
+        const uint32_t j = E16 ? (uint32_t)((const uint16_t*)a.vals)[q] : a.vals[q] >> a.kbits;
         if (j < jlo || j >= jhi) continue;
         if (plog2 && part_of(j, plog2) != p) continue;
         uint32_t h = (j * 0x85EBCA6Bu) >> (32 - kMapLog2);
@@ -844,7 +847,8 @@ hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_
   // the entries land in keys_in (free after the sort), as with the run pass
   const uint32_t per_xcd = (nb_bound + kXcds - 1) / kXcds;
   hipLaunchKernelGGL(index_bucket_kernel, dim3(per_xcd * kXcds), dim3(kBucketThreads), 0, st, vout, b.bstart,
-                     nbuckets_d, total, b.sketches, b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in, b.flags);
+                     nbuckets_d, total, b.sketches, b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in,
+                     index_ents16(b.n) ? 1u : 0u, b.flags);
   return hipGetLastError();
 }
 
@@ -869,8 +873,16 @@ size_t index_bucket_sort_tmp_bytes(uint64_t total) {
 
 hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st) {
   if (n_rows == 0) return hipSuccess;
-  hipLaunchKernelGGL(index_pairs_kernel, dim3(n_rows), dim3(kRowThreads), 0, st, a);
+  if (a.ents16)
+    hipLaunchKernelGGL(index_pairs_kernel<true>, dim3(n_rows), dim3(kRowThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(index_pairs_kernel<false>, dim3(n_rows), dim3(kRowThreads), 0, st, a);
   return hipGetLastError();
 }
+
+// The bucketed build stores each run member as its 16-bit row when rows fit
+// (C3/C5's 10k rows: C5's 10^8 members in 200 MB instead of 400 MB, inside
+// the 256 MB MALL that the pairs kernel's member reads then hit).
+bool index_ents16(uint32_t n) { return n <= 65536u; }
 
 }  // namespace gg
