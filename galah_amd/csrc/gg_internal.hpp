@@ -251,7 +251,8 @@ struct IndexLaunch {
   uint32_t n;
   uint32_t stride;
   uint32_t kbits;
-  uint32_t row0;         // first row processed (blockIdx.x = row - row0)
+  uint32_t row0;         // first row processed
+  uint32_t n_rows;       // rows processed (set by launch_index_pairs)
   uint64_t nb;           // tile rows
   uint64_t tile_begin;
   uint64_t tile_end;

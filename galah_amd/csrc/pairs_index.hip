@@ -669,7 +669,14 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
   __shared__ uint32_t fill;
   __shared__ volatile uint32_t over;
   const uint32_t tid = threadIdx.x;
-  const uint32_t i = a.row0 + blockIdx.x;
+  // XCD-aware rows: the workgroups of XCD x (blockIdx % kXcds) take the x-th
+  // contiguous range of rows, in order, so rows near each other share that
+  // XCD's L2 (the run members one row reads, a row next to it in the input
+  // order often reads too: related genomes sit together in many inputs)
+  const uint32_t per_xcd = (a.n_rows + kXcds - 1) / kXcds;
+  const uint32_t ri_ = (blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
+  if (ri_ >= a.n_rows) return;
+  const uint32_t i = a.row0 + ri_;
   if (i >= a.n) return;
   // (launched right after the build, before the host has seen its flags: a
   // run over the limit or a bucket too large left runinfo incomplete)
@@ -873,10 +880,13 @@ size_t index_bucket_sort_tmp_bytes(uint64_t total) {
 
 hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st) {
   if (n_rows == 0) return hipSuccess;
+  IndexLaunch b = a;
+  b.n_rows = n_rows;
+  const dim3 grid((n_rows + kXcds - 1) / kXcds * kXcds);
   if (a.ents16)
-    hipLaunchKernelGGL(index_pairs_kernel<true>, dim3(n_rows), dim3(kRowThreads), 0, st, a);
+    hipLaunchKernelGGL(index_pairs_kernel<true>, grid, dim3(kRowThreads), 0, st, b);
   else
-    hipLaunchKernelGGL(index_pairs_kernel<false>, dim3(n_rows), dim3(kRowThreads), 0, st, a);
+    hipLaunchKernelGGL(index_pairs_kernel<false>, grid, dim3(kRowThreads), 0, st, b);
   return hipGetLastError();
 }
 
