@@ -311,8 +311,14 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   // batch 0's candidate sets are cleared on `stream` while the run table
   // uploads on the copy stream (C5: 2.6 GB of sets, 58 MB of runs)
   const uint32_t nb0 = std::min(n_genomes, max_batch);
-  GG_HIP(c, hipMemsetAsync(d_table, 0xFF, (size_t)nb0 * cap * sizeof(uint64_t), st));
-  GG_HIP(c, hipMemsetAsync(d_flags, 0, nb0 * sizeof(uint32_t), st));
+  const size_t batch_bytes = (size_t)nb0 * cap * sizeof(uint64_t);
+  if (c->clean_table != d_table || c->clean_table_bytes < batch_bytes) {
+    GG_HIP(c, hipMemsetAsync(d_table, 0xFF, batch_bytes, st));
+    GG_HIP(c, hipMemsetAsync(d_flags, 0, nb0 * sizeof(uint32_t), st));
+  }
+  // (dirty until every batch's finalize has run; an error return leaves it so)
+  c->clean_table = nullptr;
+  c->clean_table_bytes = 0;
   if (!c->copy_stream) {
     GG_HIP(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     GG_HIP(c, hipEventCreateWithFlags(&c->copy_done, hipEventDisableTiming));
@@ -448,17 +454,9 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       GG_HIP(c, hipMemcpyAsync(d_slot_list, active.data(), active.size() * sizeof(uint32_t),
                                hipMemcpyHostToDevice, st));
       hp.mark("H2D runs/starts");
-      if (pass == 0) {
-        if (g0 > 0) {  // (batch 0 was cleared before the run index)
-          GG_HIP(c, hipMemsetAsync(d_table, 0xFF, (size_t)nb * cap * sizeof(uint64_t), st));
-          GG_HIP(c, hipMemsetAsync(d_flags, 0, nb * sizeof(uint32_t), st));
-        }
-      } else {
-        for (uint32_t slot : active) {
-          GG_HIP(c, hipMemsetAsync(d_table + (uint64_t)slot * cap, 0xFF, cap * sizeof(uint64_t), st));
-          GG_HIP(c, hipMemsetAsync(d_flags + slot, 0, sizeof(uint32_t), st));
-        }
-      }
+      // (the sets of batch 0 were cleared above if they needed it; every
+      // later pass and batch finds the sets its slots use emptied by the
+      // previous finalize)
       SketchLaunch a;
       a.words = d_words;
       a.n_words = n_words;
@@ -497,6 +495,8 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       active.swap(next);
     }
   }
+  c->clean_table = d_table;
+  c->clean_table_bytes = batch_bytes;
   return GG_OK;
 }
 

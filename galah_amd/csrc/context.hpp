@@ -89,6 +89,11 @@ struct gg_ctx {
   std::string err;
   // grow-only device scratch, keyed by purpose
   std::map<std::string, std::pair<void*, size_t>> scratch;
+  // K1's candidate sets ("table" scratch) known empty, with their flags
+  // clear, over [0, clean_table_bytes) of clean_table: the finalize kernel
+  // leaves every set it reads empty, so only a new or grown buffer is cleared
+  const void* clean_table = nullptr;
+  size_t clean_table_bytes = 0;
   // grow-only pinned host staging buffer (streamed ingest)
   void* pinned = nullptr;
   size_t pinned_bytes = 0;

@@ -78,7 +78,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   const uint32_t* slot_genome,
                                   const uint64_t* tau, uint64_t* table,
                                   uint32_t cap_log2,
-                                  const uint32_t* flags, uint32_t s,
+                                  uint32_t* flags, uint32_t s,
                                   uint32_t sort_pow2, const uint32_t* row_of, uint64_t* out,
                                   uint32_t* lens, uint32_t* status,
                                   hipStream_t st);

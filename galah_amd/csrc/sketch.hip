@@ -520,7 +520,7 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
     const uint32_t* __restrict__ slot_list, const uint32_t* __restrict__ slot_genome,
     const uint64_t* __restrict__ tau, uint64_t* __restrict__ table,
     uint32_t cap_log2,
-    const uint32_t* __restrict__ flags, uint32_t s, uint32_t sort_pow2, uint32_t nb_log2,
+    uint32_t* __restrict__ flags, uint32_t s, uint32_t sort_pow2, uint32_t nb_log2,
     const uint32_t* __restrict__ row_of, uint64_t* __restrict__ out, uint32_t* __restrict__ lens,
     uint32_t* __restrict__ status) {
   extern __shared__ uint64_t buf[];  // [sort_pow2] values, then [1 << nb_log2] u32 bucket counters
@@ -533,19 +533,27 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
   const uint32_t g = row_of ? row_of[slot_genome[slot]] : slot_genome[slot];
   const uint32_t f = flags[slot];
   const uint32_t T = blockDim.x, tid = threadIdx.x, lane = tid & 63;
+  uint64_t* tab = table + ((uint64_t)slot << cap_log2);
+  const uint32_t cap = 1u << cap_log2;
+  // every path leaves the slot's set empty and its flags clear for the next
+  // K1 launch (the host clears the sets only before their first use)
+  auto clear_slot = [&]() {
+    for (uint32_t i = tid; i < cap; i += T) tab[i] = kEmpty;
+    if (tid == 0) flags[slot] = 0u;
+  };
   if (f & kFlagOverflow) {
     if (tid == 0) {
       status[slot] = kSketchRetrySmaller;
       lens[g] = 0;
     }
+    __syncthreads();  // (every thread has read flags[slot])
+    clear_slot();
     return;
   }
   const uint32_t NB = 1u << nb_log2;
   if (tid == 0) fill = 0;
   for (uint32_t i = tid; i < NB; i += T) cnt[i] = 0;
   __syncthreads();
-  uint64_t* tab = table + ((uint64_t)slot << cap_log2);
-  const uint32_t cap = 1u << cap_log2;
   // gather: each thread 8 consecutive slots per step, all loads in flight
   // at once (one workgroup per CU at s = 10000: with one load per thread per
   // step the gather waited on HBM latency step after step), a wave prefix
@@ -595,6 +603,7 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
       status[slot] = st;
       lens[g] = 0;
     }
+    clear_slot();  // (the gather's reads are done: barrier above)
     return;
   }
   // bucket = the nb_log2 bits below tau's top bit (monotone in the value)
@@ -641,6 +650,7 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
       if (e0 + j * T < n) buf[e0 + j * T] = v[j];
   }
   __syncthreads();
+  clear_slot();  // (the table's values are all in LDS now)
   // every value of a bucket that starts below s: its rank in the bucket
   uint64_t* o = out + (uint64_t)g * s;
   const uint32_t m = min(s, n);
@@ -697,7 +707,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   const uint32_t* slot_genome,
                                   const uint64_t* tau, uint64_t* table,
                                   uint32_t cap_log2,
-                                  const uint32_t* flags, uint32_t s,
+                                  uint32_t* flags, uint32_t s,
                                   uint32_t sort_pow2, const uint32_t* row_of, uint64_t* out,
                                   uint32_t* lens, uint32_t* status,
                                   hipStream_t st) {
