@@ -5,15 +5,15 @@
 // iff common >= cmin[total]).  common(i, j) is the number of hash values
 // that occur in both sketches, and a hash occurs at most once per sketch, so
 //
-//   1. every sketch entry (row i, position k < len_i) is radix-sorted
-//      (hipCUB / rocPRIM onesweep) by the top 32 significant bits of its
-//      hash, carrying the hash's low 32 bits with (i, k): 32-bit keys need at
-//      most 4 digit passes where the 64-bit hashes needed 7-8, and key and
-//      low word together still hold the whole hash;
-//   2. a run pass finds the runs of equal keys, splits the rare ones that
-//      hold more than one hash (equal top bits, different low words: sorted
-//      in place by the thread that owns the run), and writes (run start, g)
-//      to every member's row-major slot (runinfo; g = 1 writes 0);
+//   1. every sketch entry (row i, position k < len_i) is grouped with the
+//      entries of equal hash: the bucketed build (default) sorts the entries
+//      by a monotone, population-balanced bucket of their hash (16-bit ids,
+//      two radix passes) and groups equal hashes per bucket in an LDS hash
+//      table; the full build (fallback) radix-sorts the top 32 significant
+//      bits of each hash, carrying its low 32 bits, in four passes;
+//   2. each group of g >= 2 equal hashes ("run") lies contiguous in ents,
+//      and (run start, g) goes to every member's row-major slot (runinfo;
+//      g = 1 writes 0);
 //   3. one workgroup per row i walks its own runinfo (coalesced), reads the
 //      members of its runs and counts every partner j > i in an LDS hash map
 //      -> common(i, j) exactly, for every pair that shares a hash;

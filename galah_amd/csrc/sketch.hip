@@ -9,22 +9,27 @@
 //   sketch = the min(s, #distinct) smallest distinct h, ascending.
 //
 // MI355X design
-//   * Input is 2-bit packed (0.25 B/base).  Each lane owns SEG consecutive
-//     k-mer positions and rolls the forward code in both bit orders:
-//       fm = MSB-first code (lexicographic order of the forward k-mer)
-//       fl = LSB-first code (byte p of the hash input = base p)
-//     The reverse complement needs no separate state:
-//       rc MSB-first = ~fl, rc LSB-first = ~fm   (within 2k bits).
-//   * The first multiply of each murmur3 input word and the ASCII byte
-//     assembly are folded into LDS tables (see hash_parts).
+//   * Input is 2-bit packed (0.25 B/base).  Each lane owns a segment of 44
+//     consecutive k-mer positions of one run (k = 21), loads the 64-base
+//     window at its start and that window's reverse complement once, and
+//     takes every k-mer's forward and reverse-complement codes as static
+//     64-bit slices of the two (the canonical code is a 64-bit min).  Each
+//     workgroup sweeps a contiguous chunk of segments.
+//   * The first multiply of each murmur3 input word, the rotates and the
+//     second multiply of the k1 and k2 words, and the whole tail word are
+//     folded into LDS tables indexed by 8-bit groups of 4 bases (see
+//     hash_parts).
 //   * Bottom-s selection is a threshold prefilter: a k-mer survives iff
 //     h <= tau[g] where tau[g] ~ C*s/nk_g * 2^64, so only ~C*s of the
 //     ~nk_g hashes per genome reach a per-genome open-addressing set in HBM
-//     (atomicCAS, duplicates collapse).  The finalize kernel sorts the set in
-//     LDS and keeps the first s.  When the set holds fewer than s distinct
-//     values below tau (tau < 2^64-1) or overflows, the host moves tau and
-//     re-runs the affected genomes only; the result is exact in both cases
-//     because every distinct hash <= tau is in the set.
+//     (atomicCAS, duplicates collapse).  The test runs on the high words of
+//     the two finalisers first; the k-mers that pass go to a per-wave LDS
+//     queue whose drain finishes the exact hash and inserts.  The finalize
+//     kernel sorts the set in LDS, keeps the first s and leaves the set
+//     empty.  When the set holds fewer than s distinct values below tau
+//     (tau < 2^64-1) or overflows, the host moves tau and re-runs the
+//     affected genomes only; the result is exact in both cases because every
+//     distinct hash <= tau is in the set.
 #include "device_util.hpp"
 #include "gg_internal.hpp"
 
