@@ -884,6 +884,8 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
   return GG_OK;
 }
 
+// Passing pairs of tiles [tb, te) appended to res; at least
+// kDeviceSortPairs of them come sorted by (i, j) (sorted on the device).
 gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
                               uint64_t tb, uint64_t te, float min_ani, std::vector<gg_pair>& res,
                               hipStream_t st) {
@@ -905,9 +907,27 @@ gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d
     if (cnt <= cap) {
       const size_t at = res.size();
       res.resize(at + cnt);
-      if (cnt) {
-        GG_HIP(c, hipMemcpyAsync(res.data() + at, d_out, cnt * sizeof(gg_pair), hipMemcpyDeviceToHost, st));
-        GG_HIP(c, hipStreamSynchronize(st));
+      if (cnt < kDeviceSortPairs) {  // (few: the host sorts them)
+        if (cnt) {
+          GG_HIP(c, hipMemcpyAsync(res.data() + at, d_out, cnt * sizeof(gg_pair), hipMemcpyDeviceToHost, st));
+          GG_HIP(c, hipStreamSynchronize(st));
+        }
+        return GG_OK;
+      }
+      // many: sorted by (i, j) on the device, taken in order
+      uint64_t* d_kv;
+      void* d_tmp;
+      const size_t tmp_bytes = pair_sort_tmp_bytes(cnt, n);
+      GG_HIP(c, scratch_t(c, "pair_sort_kv", 4 * cnt, &d_kv));
+      GG_HIP(c, scratch(c, "pair_sort_tmp", std::max<size_t>(tmp_bytes, 16), &d_tmp));
+      GG_HIP(c, sort_pairs_device(d_out, cnt, n, d_kv, d_kv + cnt, d_kv + 2 * cnt, d_kv + 3 * cnt, d_tmp, tmp_bytes,
+                                  st));
+      std::vector<uint64_t> kv(2 * cnt);
+      GG_HIP(c, hipMemcpyAsync(kv.data(), d_kv + 2 * cnt, 2 * cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+      GG_HIP(c, hipStreamSynchronize(st));
+      for (uint64_t x = 0; x < cnt; ++x) {
+        const uint64_t key = kv[x], val = kv[cnt + x];
+        res[at + x] = gg_pair{(uint32_t)(key / n), (uint32_t)(key % n), (uint32_t)(val >> 32), (uint32_t)val};
       }
       return GG_OK;
     }

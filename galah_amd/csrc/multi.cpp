@@ -132,42 +132,7 @@ gg_status replicate(gg_ctx* m, size_t mi, const std::vector<gg_ctx*>& ms, const 
   return GG_OK;
 }
 
-// Sort by (i, j) (SortedPairGenomeDistanceCache order): LSD radix sort on
-// the key i * n + j, 11-bit digits over its significant bits (C4's 153k
-// pairs: 3 passes instead of a comparison sort's ~17 compares per pair).
-void sort_pairs_ij(std::vector<gg_pair>& v, uint32_t n) {
-  if (v.size() < 4096) {
-    std::sort(v.begin(), v.end(), [](const gg_pair& x, const gg_pair& y) { return x.i != y.i ? x.i < y.i : x.j < y.j; });
-    return;
-  }
-  constexpr int D = 11;
-  constexpr uint32_t B = 1u << D;
-  const uint64_t maxkey = (uint64_t)n * n;
-  int bits = 1;
-  while (bits < 64 && (maxkey >> bits) != 0) ++bits;
-  const size_t m = v.size();
-  std::vector<uint64_t> key(m), key2(m);
-  std::vector<gg_pair> v2(m);
-  for (size_t x = 0; x < m; ++x) key[x] = (uint64_t)v[x].i * n + v[x].j;
-  std::vector<size_t> cnt(B);
-  for (int sh = 0; sh < bits; sh += D) {
-    std::fill(cnt.begin(), cnt.end(), 0);
-    for (size_t x = 0; x < m; ++x) ++cnt[(key[x] >> sh) & (B - 1)];
-    size_t acc = 0;
-    for (uint32_t d = 0; d < B; ++d) {
-      const size_t c = cnt[d];
-      cnt[d] = acc;
-      acc += c;
-    }
-    for (size_t x = 0; x < m; ++x) {
-      const size_t at = cnt[(key[x] >> sh) & (B - 1)]++;
-      key2[at] = key[x];
-      v2[at] = v[x];
-    }
-    key.swap(key2);
-    v.swap(v2);
-  }
-}
+bool pair_ij_less(const gg_pair& x, const gg_pair& y) { return x.i != y.i ? x.i < y.i : x.j < y.j; }
 
 // Steps 2-4 over rows resident on every member: gather, pairs, merge.
 gg_status gather_pairs_merge(gg_ctx* c, const std::vector<gg_ctx*>& ms, const std::vector<Rows>& rows,
@@ -203,12 +168,21 @@ gg_status gather_pairs_merge(gg_ctx* c, const std::vector<gg_ctx*>& ms, const st
   if (st != GG_OK) return st;
   c->phase_ms[GG_PHASE_PAIRS] = ms_since(t0);
   t0 = Clock::now();
-  size_t total = 0;
-  for (auto& p : part) total += p.size();
+  // every member's part in (i, j) order (large parts come sorted from the
+  // device, pairs_range_to_host), then merged: SortedPairGenomeDistanceCache
+  // order
+  for (auto& p : part)
+    if (p.size() < kDeviceSortPairs) std::sort(p.begin(), p.end(), pair_ij_less);
   res.clear();
-  res.reserve(total);
-  for (auto& p : part) res.insert(res.end(), p.begin(), p.end());
-  sort_pairs_ij(res, n);
+  for (auto& p : part) {
+    if (res.empty()) {
+      res.swap(p);
+      continue;
+    }
+    std::vector<gg_pair> merged(res.size() + p.size());
+    std::merge(res.begin(), res.end(), p.begin(), p.end(), merged.begin(), pair_ij_less);
+    res.swap(merged);
+  }
   c->phase_ms[GG_PHASE_MERGE] = ms_since(t0);
   return GG_OK;
 }

@@ -890,6 +890,48 @@ hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t
   return hipGetLastError();
 }
 
+// Passing pairs in (i, j) order on the device (the output of every K2 form
+// is an atomic append): key i * n + j, value common << 32 | total, radix
+// sorted over the key's significant bits, so the host takes them in order
+// (C4's 153k pairs: the host radix sort took ~1 ms of a 2.3 ms merge).
+namespace {
+__global__ __launch_bounds__(256) void pair_keys_kernel(const gg_pair* __restrict__ p, uint64_t cnt, uint32_t n,
+                                                        uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
+  for (uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x; x < cnt; x += (uint64_t)gridDim.x * 256) {
+    const gg_pair q = p[x];
+    keys[x] = (uint64_t)q.i * n + q.j;
+    vals[x] = ((uint64_t)q.common << 32) | q.total;
+  }
+}
+}  // namespace
+
+uint32_t pair_key_bits(uint32_t n) {
+  const uint64_t mx = (uint64_t)n * n;
+  uint32_t bits = 1;
+  while (bits < 64 && (mx >> bits) != 0) ++bits;
+  return bits;
+}
+
+size_t pair_sort_tmp_bytes(uint64_t cnt, uint32_t n) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                           (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)cnt, 0,
+                                           (int)pair_key_bits(n));
+  return bytes;
+}
+
+hipError_t sort_pairs_device(const gg_pair* d_pairs, uint64_t cnt, uint32_t n, uint64_t* keys, uint64_t* vals,
+                             uint64_t* keys_out, uint64_t* vals_out, void* tmp, size_t tmp_bytes, hipStream_t st) {
+  if (cnt == 0) return hipSuccess;
+  hipLaunchKernelGGL(pair_keys_kernel, dim3((uint32_t)std::min<uint64_t>(4096, (cnt + 255) / 256)), dim3(256), 0, st,
+                     d_pairs, cnt, n, keys, vals);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // (bit 0 up: see index_build_buckets on rocPRIM's merge-sort path)
+  return hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_out, vals, vals_out, (int)cnt, 0,
+                                            (int)pair_key_bits(n), st);
+}
+
 // The bucketed build stores each run member as its 16-bit row when rows fit
 // (C3/C5's 10k rows: C5's 10^8 members in 200 MB instead of 400 MB, inside
 // the 256 MB MALL that the pairs kernel's member reads then hit).
