@@ -54,6 +54,24 @@ hipError_t scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
   return hipSuccess;
 }
 
+hipError_t host_scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
+  auto& e = c->host_scratch[key];
+  if (e.second < bytes) {
+    if (e.first) {
+      hipError_t err = hipHostFree(e.first);
+      if (err != hipSuccess) return err;
+      e.first = nullptr;
+      e.second = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 4096);
+    hipError_t err = hipHostMalloc(&e.first, want, hipHostMallocDefault);
+    if (err != hipSuccess) return err;
+    e.second = want;
+  }
+  *out = e.first;
+  return hipSuccess;
+}
+
 hipError_t pinned(gg_ctx* c, size_t bytes, void** out) {
   if (c->pinned_bytes < bytes) {
     if (c->pinned) {
@@ -303,10 +321,19 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   uint64_t* d_tau;
   GG_HIP(c, scratch_t(c, "table", (size_t)max_batch * cap, &d_table));
   GG_HIP(c, scratch_t(c, "flags", max_batch, &d_flags));
-  GG_HIP(c, scratch_t(c, "status", max_batch, &d_status));
   GG_HIP(c, scratch_t(c, "slot_list", max_batch, &d_slot_list));
   GG_HIP(c, scratch_t(c, "slot_genome", max_batch, &d_slot_genome));
-  GG_HIP(c, scratch_t(c, "tau", max_batch, &d_tau));
+  // what the host reads back, contiguous on the device and in pinned host
+  // memory (one DMA per pass): the run index (bad run, per genome first run,
+  // first segment and k-mers), then tau and status per batch slot
+  const size_t ng1 = (size_t)n_genomes + 1;
+  const size_t rb_ix = 1 + 3 * ng1, rb_u64 = rb_ix + max_batch + (max_batch + 1) / 2;
+  uint64_t *d_rb, *h_rb;
+  GG_HIP(c, scratch_t(c, "readback", rb_u64, &d_rb));
+  GG_HIP(c, host_scratch_t(c, "readback", rb_u64, &h_rb));
+  d_tau = d_rb + rb_ix;
+  d_status = reinterpret_cast<uint32_t*>(d_rb + rb_ix + max_batch);
+  const uint32_t* h_status = reinterpret_cast<const uint32_t*>(h_rb + rb_ix + max_batch);
 
   // batch 0's candidate sets are cleared on `stream` while the run table
   // uploads on the copy stream (C5: 2.6 GB of sets, 58 MB of runs)
@@ -327,13 +354,12 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   // (runindex.hip); the host keeps per genome its first run, k-mer count and
   // first segment
   gg_run* d_all_runs;
-  uint64_t *d_ix, *d_rs, *d_sc;
+  uint64_t *d_rs, *d_sc;
+  uint64_t* d_ix = d_rb;  // bad, gr, grs, nk
   void* d_ix_tmp;
-  const size_t ng1 = (size_t)n_genomes + 1;
   GG_HIP(c, scratch_t(c, "runs_all", std::max<uint64_t>(n_runs, 1), &d_all_runs));
   GG_HIP(c, scratch_t(c, "run_sstart", n_runs + 1, &d_rs));
   GG_HIP(c, scratch_t(c, "run_segs", n_runs + 1, &d_sc));
-  GG_HIP(c, scratch_t(c, "run_index", 1 + 3 * ng1, &d_ix));  // bad, gr, grs, nk
   const size_t ix_tmp = run_index_tmp_bytes(n_runs);
   GG_HIP(c, scratch(c, "run_index_tmp", std::max<size_t>(ix_tmp, 16), &d_ix_tmp));
   // A run table already in this device's memory is indexed where it lies
@@ -374,9 +400,48 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   xd.tmp = d_ix_tmp;
   xd.tmp_bytes = ix_tmp;
   GG_HIP(c, launch_run_index(xd, st));
-  std::vector<uint64_t> hix(1 + 3 * ng1);
-  GG_HIP(c, hipMemcpyAsync(hix.data(), d_ix, hix.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  // One batch (every BASELINE config): its first pass is queued behind the
+  // run index with no host round trip (tau and the slot maps computed on the
+  // device, K1 reading its segment count there and skipping a bad table);
+  // the host reads the index, the pass's status and the taus afterwards.
+  const bool one_batch = n_genomes <= max_batch;
+  size_t k1_timed = SIZE_MAX;
+  if (one_batch) {
+    GG_HIP(c, launch_first_pass(xd.nk, n_genomes, geom.over * (double)c->s, d_tau, d_slot_genome, d_slot_list, st));
+    SketchLaunch a;
+    a.words = d_words;
+    a.n_words = n_words;
+    a.runs = d_all_runs;
+    a.run_sstart = d_rs;
+    a.slot_genome0 = 0;
+    a.n_runs = (uint32_t)n_runs;
+    a.seg0 = 0;
+    a.n_segs = 0;
+    a.n_segs_dev = d_rs + n_runs;
+    a.bad_dev = d_ix;
+    a.tau = d_tau;
+    a.table = d_table;
+    a.cap_log2 = geom.cap_log2;
+    a.flags = d_flags;
+    a.seed = c->seed;
+    if (c->timing) k1_timed = c->timed.size();
+    GG_HIP(c, timed_launch(c, GG_KERNEL_SKETCH, 0, st, [&] { return launch_sketch_candidates(c->k, a, grid, st); }));
+    GG_HIP(c, timed_launch(c, GG_KERNEL_FINALIZE, n_genomes, st, [&] {
+      return launch_sketch_finalize(d_slot_list, n_genomes, d_slot_genome, d_tau, d_table, geom.cap_log2, d_flags,
+                                    c->s, geom.sort_pow2, d_row_of, d_out, d_lens, d_status, st);
+    }));
+  }
+  // the index, and in one batch the first pass's taus and status (one batch:
+  // max_batch = n_genomes, so the three are one contiguous read)
+  GG_HIP(c, hipMemcpyAsync(h_rb, d_rb, (one_batch ? rb_u64 : rb_ix) * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   GG_HIP(c, hipStreamSynchronize(st));
+  std::vector<uint64_t> hix(h_rb, h_rb + rb_ix);
+  std::vector<uint32_t> status0;
+  std::vector<uint64_t> tau0;
+  if (one_batch) {
+    tau0.assign(h_rb + rb_ix, h_rb + rb_ix + n_genomes);
+    status0.assign(h_status, h_status + n_genomes);
+  }
   if (hix[0] != ~0ull) {
     const gg_run* hr = host_runs();
     if (!hr) return fail(c, GG_ERR_HIP, "copying the run table to the host failed");
@@ -385,6 +450,11 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   const uint64_t* gr = hix.data() + 1;
   const uint64_t* grs = hix.data() + 1 + ng1;
   const uint64_t* nk = hix.data() + 1 + 2 * ng1;
+  if (k1_timed < c->timed.size()) {  // (the k-mers of the first pass, known now)
+    uint64_t kall = 0;
+    for (uint32_t g = 0; g < n_genomes; ++g) kall += nk[g];
+    c->timed[k1_timed].work = kall;
+  }
   hp.mark("index runs (device)");
   for (uint32_t g0 = 0; g0 < n_genomes; g0 += max_batch) {
     const uint32_t g1 = std::min(n_genomes, g0 + max_batch);
@@ -393,19 +463,32 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
     std::vector<uint64_t> h_tau(nb);
     std::vector<uint32_t> h_slot_genome(nb), h_slot_list(nb);
     for (uint32_t i = 0; i < nb; ++i) {
-      ts[i].tau = initial_tau(nk[g0 + i], c->s, geom.over);
+      ts[i].tau = one_batch ? tau0[i] : initial_tau(nk[g0 + i], c->s, geom.over);
       h_tau[i] = ts[i].tau;
       h_slot_genome[i] = g0 + i;
       h_slot_list[i] = i;
     }
-    GG_HIP(c, hipMemcpyAsync(d_slot_genome, h_slot_genome.data(), nb * sizeof(uint32_t),
-                             hipMemcpyHostToDevice, st));
+    if (!one_batch)
+      GG_HIP(c, hipMemcpyAsync(d_slot_genome, h_slot_genome.data(), nb * sizeof(uint32_t),
+                               hipMemcpyHostToDevice, st));
     hp.mark("initial tau");
 
     // active genome slots for this pass
     std::vector<uint32_t> active = h_slot_list;
     for (int pass = 0; !active.empty(); ++pass) {
       if (pass > 200) return fail(c, GG_ERR_INTERNAL, "bottom-s threshold search did not converge");
+      if (pass == 0 && one_batch) {  // (queued above)
+        std::vector<uint32_t> next;
+        for (uint32_t slot : active) {
+          if (status0[slot] == kSketchOk) continue;
+          if (!advance_tau(ts[slot], status0[slot]))
+            return fail(c, GG_ERR_INTERNAL, "bottom-s threshold search failed");
+          h_tau[slot] = ts[slot].tau;
+          next.push_back(slot);
+        }
+        active.swap(next);
+        continue;
+      }
       // run table for the active genomes: on the first pass the batch's
       // slice of the uploaded table and its device index, on retries the
       // subset's runs and segment starts, built here and uploaded.  K1
@@ -480,9 +563,10 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
                                       geom.sort_pow2, d_row_of, d_out, d_lens, d_status, st);
       }));
       hp.mark("enqueue K1 + finalize");
-      std::vector<uint32_t> status(nb);
-      GG_HIP(c, hipMemcpyAsync(status.data(), d_status, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+      GG_HIP(c, hipMemcpyAsync(const_cast<uint32_t*>(h_status), d_status, nb * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, st));
       GG_HIP(c, hipStreamSynchronize(st));
+      const std::vector<uint32_t> status(h_status, h_status + nb);
       hp.mark("wait (GPU)");
       std::vector<uint32_t> next;
       for (uint32_t slot : active) {
@@ -651,14 +735,15 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   b.kbits = kbits;
   b.max_run = kMaxRun;
   GG_HIP(c, scratch_t(c, "idx_offs", std::max(n, 1u), &b.offs));
-  GG_HIP(c, scratch_t(c, "idx_info", 2, &b.info));
+  // info (2 u64) and flags (4 u32) adjacent: one read-back
+  GG_HIP(c, scratch_t(c, "idx_info", 4, &b.info));
+  b.flags = reinterpret_cast<uint32_t*>(b.info + 2);
   GG_HIP(c, scratch_t(c, "idx_keys_in", total, &b.keys_in));
   GG_HIP(c, scratch_t(c, "idx_keys_out", total, &b.keys_out));
   GG_HIP(c, scratch_t(c, "idx_vals_in", total, &b.vals_in));
   GG_HIP(c, scratch_t(c, "idx_vals_out", total, &b.vals_out));
   GG_HIP(c, scratch_t(c, "idx_runinfo", total, &b.runinfo));
   GG_HIP(c, scratch_t(c, "idx_mixed", (total + 31) / 32, &b.mixed));
-  GG_HIP(c, scratch_t(c, "idx_flags", 4, &b.flags));
   // rows of the tile rows that intersect [tb, te)
   uint64_t I0 = UINT64_MAX, I1 = 0, t = 0;
   for (uint64_t I = 0; I < nb && t < te; ++I) {
@@ -751,9 +836,12 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st, [&] { return index_build_buckets(b, total, nbb, st); }));
     gg_status ps = launch_pairs(true);
     if (ps != GG_OK) return ps;
-    GG_HIP(c, hipMemcpyAsync(info, b.info, sizeof info, hipMemcpyDeviceToHost, st));
-    GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof flags, hipMemcpyDeviceToHost, st));
+    uint64_t* h_if;
+    GG_HIP(c, host_scratch_t(c, "idx_info", 4, &h_if));
+    GG_HIP(c, hipMemcpyAsync(h_if, b.info, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(c, hipStreamSynchronize(st));
+    memcpy(info, h_if, sizeof info);
+    memcpy(flags, h_if + 2, sizeof flags);
     built = paired = flags[3] == 0;
   } else {
     uint32_t nbuckets = 0;
@@ -890,8 +978,9 @@ gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d
                               uint64_t tb, uint64_t te, float min_ani, std::vector<gg_pair>& res,
                               hipStream_t st) {
   if (n < 2 || tb >= te) return GG_OK;
-  uint64_t* d_count;
+  uint64_t *d_count, *h_count;
   GG_HIP(c, scratch_t(c, "pair_count", 1, &d_count));
+  GG_HIP(c, host_scratch_t(c, "pair_count", 1, &h_count));
   uint64_t cap = std::max<uint64_t>(1 << 20, (uint64_t)n * 16);
   const uint64_t all = (uint64_t)n * (n > 0 ? n - 1 : 0) / 2;
   cap = std::min<uint64_t>(cap, std::max<uint64_t>(all, 1));
@@ -901,9 +990,9 @@ gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d
     GG_HIP(c, hipMemsetAsync(d_count, 0, sizeof(uint64_t), st));
     gg_status ps = pairs_core(c, d_sk, d_lens, n, tb, te, min_ani, d_out, cap, d_count, st);
     if (ps != GG_OK) return ps;
-    uint64_t cnt = 0;
-    GG_HIP(c, hipMemcpyAsync(&cnt, d_count, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(c, hipMemcpyAsync(h_count, d_count, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(c, hipStreamSynchronize(st));
+    const uint64_t cnt = *h_count;
     if (cnt <= cap) {
       const size_t at = res.size();
       res.resize(at + cnt);
@@ -922,8 +1011,9 @@ gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d
       GG_HIP(c, scratch(c, "pair_sort_tmp", std::max<size_t>(tmp_bytes, 16), &d_tmp));
       GG_HIP(c, sort_pairs_device(d_out, cnt, n, d_kv, d_kv + cnt, d_kv + 2 * cnt, d_kv + 3 * cnt, d_tmp, tmp_bytes,
                                   st));
-      std::vector<uint64_t> kv(2 * cnt);
-      GG_HIP(c, hipMemcpyAsync(kv.data(), d_kv + 2 * cnt, 2 * cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+      uint64_t* kv;
+      GG_HIP(c, host_scratch_t(c, "pair_sort_kv", 2 * cnt, &kv));
+      GG_HIP(c, hipMemcpyAsync(kv, d_kv + 2 * cnt, 2 * cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
       GG_HIP(c, hipStreamSynchronize(st));
       for (uint64_t x = 0; x < cnt; ++x) {
         const uint64_t key = kv[x], val = kv[cnt + x];
@@ -1055,6 +1145,9 @@ void gg_destroy(gg_ctx* ctx) {
   if (!ctx) return;
   ctx->pool.reset();  // (member threads idle between calls: joined here)
   for (gg_ctx* m : ctx->devs) gg_destroy(m);
+  for (auto& kv : ctx->host_scratch)
+    if (kv.second.first) (void)hipHostFree(kv.second.first);
+  ctx->host_scratch.clear();
   if (!ctx->devs.empty()) {
     delete ctx;
     return;

@@ -97,6 +97,9 @@ struct gg_ctx {
   // grow-only pinned host staging buffer (streamed ingest)
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
+  // grow-only pinned host buffers keyed by purpose (small read-backs: one
+  // DMA instead of a staged copy of pageable memory, ~35 us each)
+  std::map<std::string, std::pair<void*, size_t>> host_scratch;
   // cached cmin table
   float cmin_key = -1.0f;
   std::vector<uint32_t> cmin_host;
@@ -153,6 +156,15 @@ hipError_t scratch_t(gg_ctx* c, const char* key, size_t count, T** out) {
 }
 // Grow-only pinned host buffer of the context (contents not preserved).
 hipError_t pinned(gg_ctx* c, size_t bytes, void** out);
+// Grow-only pinned host buffer keyed by purpose (contents not preserved).
+hipError_t host_scratch(gg_ctx* c, const char* key, size_t bytes, void** out);
+template <typename T>
+hipError_t host_scratch_t(gg_ctx* c, const char* key, size_t count, T** out) {
+  void* p = nullptr;
+  hipError_t e = host_scratch(c, key, count * sizeof(T), &p);
+  *out = static_cast<T*>(p);
+  return e;
+}
 
 // The run-table checks sketch_core applies (genome < n_genomes and
 // non-decreasing, len >= k, base + len <= 16 n_words), for callers that

@@ -49,6 +49,10 @@ struct SketchLaunch {
   uint32_t cap_log2;
   uint32_t* flags;             // [slots]
   uint64_t seed;
+  // (first pass queued before the host has seen the run index) the segment
+  // count on the device, and the run-table check: K1 does nothing if set
+  const uint64_t* n_segs_dev = nullptr;
+  const uint64_t* bad_dev = nullptr;
 };
 
 // runindex.hip: the run table's index on the device (all device pointers)
@@ -70,6 +74,10 @@ struct RunIndexDev {
 };
 size_t run_index_tmp_bytes(uint64_t n_runs);
 hipError_t launch_run_index(const RunIndexDev& x, hipStream_t st);
+// tau[g] from nk[g] (want = oversampling * s) and identity slot maps for
+// genomes [0, n_genomes)
+hipError_t launch_first_pass(const uint64_t* nk, uint32_t n_genomes, double want, uint64_t* tau,
+                             uint32_t* slot_genome, uint32_t* slot_list, hipStream_t st);
 
 // sketch.hip
 hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,

@@ -78,7 +78,35 @@ __global__ __launch_bounds__(256) void run_genome_kmers_kernel(const gg_run* __r
   }
 }
 
+// First K1 pass of a single-batch call, set up on the device: each genome's
+// initial threshold tau = over * s / nk * 2^64 (2^64 - 1 when the genome has
+// at most over * s k-mers: every distinct hash is a candidate) and the
+// identity slot maps.  The host reads tau back for its threshold search.
+__global__ __launch_bounds__(256) void first_pass_kernel(const uint64_t* __restrict__ nk, uint32_t n_genomes,
+                                                         double want, uint64_t* __restrict__ tau,
+                                                         uint32_t* __restrict__ slot_genome,
+                                                         uint32_t* __restrict__ slot_list) {
+  for (uint32_t g = blockIdx.x * 256 + threadIdx.x; g < n_genomes; g += gridDim.x * 256) {
+    const uint64_t k = nk[g];
+    uint64_t t = ~0ull;
+    if (k != 0 && want < (double)k) {
+      const double x = want / (double)k * 18446744073709551616.0;
+      if (x < 18446744073709549568.0) t = (uint64_t)x;  // (the largest double below 2^64)
+    }
+    tau[g] = t;
+    slot_genome[g] = g;
+    slot_list[g] = g;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_first_pass(const uint64_t* nk, uint32_t n_genomes, double want, uint64_t* tau,
+                             uint32_t* slot_genome, uint32_t* slot_list, hipStream_t st) {
+  hipLaunchKernelGGL(first_pass_kernel, dim3(std::min<uint32_t>(4096, (n_genomes + 255) / 256)), dim3(256), 0, st, nk,
+                     n_genomes, want, tau, slot_genome, slot_list);
+  return hipGetLastError();
+}
 
 size_t run_index_tmp_bytes(uint64_t n_runs) {
   size_t bytes = 0;

@@ -424,9 +424,21 @@ template <int K, bool SEED0>
 __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_kernel(SketchLaunch a) {
   constexpr int kSeg = k1_seg_len(K, kGroup);
   static_assert(K >= 1 && K <= 32 && kSeg + K - 1 <= 64 && kSeg % kGroup == 0, "window");
+  if (a.bad_dev && *a.bad_dev != ~0ull) return;  // (uniform) a bad run table: the host reports it
   __shared__ __attribute__((aligned(16))) uint64_t mtab[HashShape<K>::TAB_U64];  // murmur word tables (hash_parts)
   __shared__ CandQueue queues[kBlock / 64];
   CandQueue& q = queues[threadIdx.x >> 6];
+  // Workgroup b sweeps its own contiguous chunk of segments, kBlock at a
+  // time (a wave's 64 lanes read consecutive windows).  A lane's next
+  // segment is then kBlock segments on, in the same run or a few runs later,
+  // so find_run's forward search is one or two loads; with a grid stride
+  // it was ~50 genomes on (C3: ~14 dependent loads per segment, C5's 3.6M
+  // runs ~30).
+  const uint64_t n_segs = a.n_segs_dev ? *a.n_segs_dev : a.n_segs;
+  const uint64_t per_wg = (n_segs + (uint64_t)gridDim.x * kBlock - 1) / ((uint64_t)gridDim.x * kBlock) * kBlock;
+  const uint64_t c0 = a.seg0 + (uint64_t)blockIdx.x * per_wg;
+  const uint64_t send = min(a.seg0 + n_segs, c0 + per_wg);
+  if (c0 >= send) return;  // (uniform) no segment for this workgroup
   if ((threadIdx.x & 63) == 0) q.head = q.tail = q.claim = 0;
   build_tables<K>(mtab);
   __syncthreads();
@@ -434,15 +446,6 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
   const uint64_t seed = SEED0 ? 0ull : a.seed;
   uint32_t r = 0;
 
-  // Workgroup b sweeps its own contiguous chunk of segments, kBlock at a
-  // time (a wave's 64 lanes read consecutive windows).  A lane's next
-  // segment is then kBlock segments on, in the same run or a few runs later,
-  // so find_run's forward search is one or two loads; with a grid stride
-  // it was ~50 genomes on (C3: ~14 dependent loads per segment, C5's 3.6M
-  // runs ~30).
-  const uint64_t per_wg = (a.n_segs + (uint64_t)gridDim.x * kBlock - 1) / ((uint64_t)gridDim.x * kBlock) * kBlock;
-  const uint64_t c0 = a.seg0 + (uint64_t)blockIdx.x * per_wg;
-  const uint64_t send = min(a.seg0 + a.n_segs, c0 + per_wg);
   for (uint64_t sg = c0 + threadIdx.x; sg < send; sg += kBlock) {
     r = find_run(a.run_sstart, a.n_runs, sg, r);
     const gg_run run = a.runs[r];
@@ -696,7 +699,7 @@ int sketch_segment_len(int k) { return k1_seg_len(k, kGroup); }
 
 hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,
                                     hipStream_t st) {
-  if (a.n_segs == 0) return hipSuccess;
+  if (a.n_segs == 0 && !a.n_segs_dev) return hipSuccess;
   switch (k) {
 #define GG_K(N) case N: return launch_k<N>(a, grid, st);
     GG_K(1) GG_K(2) GG_K(3) GG_K(4) GG_K(5) GG_K(6) GG_K(7) GG_K(8)

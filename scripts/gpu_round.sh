@@ -54,6 +54,9 @@ for st in $STAGES; do
     prof_c5)
       run prof_c5 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c5 -- \
         python3 -u bench.py --config c5 --steps 10 --warmup 2 --no-cpu-baseline || exit $? ;;
+    trace_c3)  # kernels and memory copies of C3 steps (timeline, host gaps)
+      run trace_c3 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/trace_c3" -o t -- \
+        python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-files || exit $? ;;
     trace_c5)  # kernels and memory copies of one C5 step (timeline of the sketch phase)
       run trace_c5 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OUT/trace_c5" -o t -- \
         python3 -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline || exit $? ;;
