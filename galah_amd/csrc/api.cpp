@@ -298,9 +298,12 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   if (n_runs && !runs) return fail(c, GG_ERR_INVALID_ARG, "null run table");
   const SketchGeom geom = sketch_geom(c->s);
   const uint64_t cap = 1ull << geom.cap_log2;
-  // genomes per batch: tables limited to ~4 GiB
-  const uint32_t max_batch = (uint32_t)std::max<uint64_t>(
-      1, std::min<uint64_t>(n_genomes, (4ull << 30) / (cap * sizeof(uint64_t))));
+  // genomes per batch: tables limited to ~4 GiB (GALAHGPU_K1_MAX_BATCH,
+  // tests only: smaller batches, so the multi-batch path runs on small inputs)
+  uint64_t batch_cap = (4ull << 30) / (cap * sizeof(uint64_t));
+  if (const char* e = getenv("GALAHGPU_K1_MAX_BATCH"))
+    if (*e && atoi(e) > 0) batch_cap = std::min<uint64_t>(batch_cap, (uint64_t)atoi(e));
+  const uint32_t max_batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(n_genomes, batch_cap));
 
   int n_cu = 256;
   (void)hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, c->device);

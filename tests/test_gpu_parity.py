@@ -674,3 +674,46 @@ def test_device_run_table_same_as_host(gpu_ctx):
     r["len"][5] = 20
     with pytest.raises(ga.GalahGpuError, match="shorter than k"):
         gpu_ctx.sketch_device(d_words, ga.device_runs(r, "cuda"), n_genomes, d_out, d_lens)
+
+
+@pytest.mark.parametrize("max_batch", ["7", "1"])
+def test_sketch_in_several_batches(monkeypatch, max_batch):
+    """More genomes than one K1 batch (GALAHGPU_K1_MAX_BATCH forces batches
+    of 7 or 1 genome: the host-planned passes, candidate sets reused from
+    batch to batch): the same sketches as one batch, through the retry
+    passes (genome 3 repeats one stretch) and on the device run table."""
+    torch = torch_dev()
+    rng = np.random.default_rng(92)
+    n_words = 1 << 16
+    words = rng.integers(0, 2**32, n_words, dtype=np.uint64).astype(np.uint32)
+    d_words = torch.from_numpy(words.view(np.int32)).cuda()
+    n_genomes = 23
+    rows, base = [], 0
+    for g in range(n_genomes):
+        if g == 3:
+            rows += [(g, 400, 5000)] * 300
+            continue
+        for _ in range(8):
+            ln = int(rng.integers(30, 4000))
+            rows.append((g, ln, base))
+            base += ln + 5
+    assert base < n_words * 16
+    runs = np.array(rows, dtype=ga.RUN_DTYPE)
+    outs = []
+    for mb in ("0", max_batch):
+        monkeypatch.setenv("GALAHGPU_K1_MAX_BATCH", mb)
+        for table in (runs, ga.device_runs(runs, "cuda")):
+            with ga.Context(k=21, sketch_size=1000) as ctx:
+                d_out = torch.zeros((n_genomes, 1000), dtype=torch.int64, device="cuda")
+                d_lens = torch.zeros(n_genomes, dtype=torch.int32, device="cuda")
+                for _ in range(2):  # (the second call reuses the emptied candidate sets)
+                    ctx.sketch_device(d_words, table, n_genomes, d_out, d_lens)
+                torch.cuda.synchronize()
+                outs.append((d_out.cpu().numpy().view(np.uint64).copy(), d_lens.cpu().numpy().view(np.uint32).copy()))
+    sk0, ln0 = outs[0]
+    for sk, ln in outs[1:]:
+        assert (ln == ln0).all() and (sk == sk0).all()
+    for g in (0, 3, 7, n_genomes - 1):
+        sel = runs[runs["genome"] == g]
+        exp = oracle.sketch_records([unpack_run(words, int(r["base"]), int(r["len"])) for r in sel])
+        assert ln0[g] == len(exp) and (sk0[g][:ln0[g]] == exp).all(), g
