@@ -975,8 +975,9 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
   return GG_OK;
 }
 
-// Passing pairs of tiles [tb, te) appended to res; at least
-// kDeviceSortPairs of them come sorted by (i, j) (sorted on the device).
+// Passing pairs of tiles [tb, te) appended to res; from kDeviceSortPairs
+// up to 2^31 of them they come sorted by (i, j) (sorted on the device:
+// pairs_sorted_on_device).
 gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
                               uint64_t tb, uint64_t te, float min_ani, std::vector<gg_pair>& res,
                               hipStream_t st) {
@@ -999,7 +1000,7 @@ gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d
     if (cnt <= cap) {
       const size_t at = res.size();
       res.resize(at + cnt);
-      if (cnt < kDeviceSortPairs) {  // (few: the host sorts them)
+      if (cnt < kDeviceSortPairs || cnt >= (1ull << 31)) {  // (few, or beyond the sort's int count: the host sorts)
         if (cnt) {
           GG_HIP(c, hipMemcpyAsync(res.data() + at, d_out, cnt * sizeof(gg_pair), hipMemcpyDeviceToHost, st));
           GG_HIP(c, hipStreamSynchronize(st));

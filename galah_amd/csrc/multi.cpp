@@ -172,7 +172,7 @@ gg_status gather_pairs_merge(gg_ctx* c, const std::vector<gg_ctx*>& ms, const st
   // device, pairs_range_to_host), then merged: SortedPairGenomeDistanceCache
   // order
   for (auto& p : part)
-    if (p.size() < kDeviceSortPairs) std::sort(p.begin(), p.end(), pair_ij_less);
+    if (!pairs_sorted_on_device(p.size())) std::sort(p.begin(), p.end(), pair_ij_less);
   res.clear();
   for (auto& p : part) {
     if (res.empty()) {
