@@ -57,7 +57,24 @@ constexpr int kRep = 64;
   X(22, "v_xor_b32_e64 v,v (VOP3 encoding)", "v_xor_b32_e64 v10, v11, v12\n")                   \
   X(23, "v_bitop3_b32 banks 3/0/1", "v_bitop3_b32 v10, v11, v12, v13 bitop3:0x96\n")           \
   X(24, "v_pk_add_f32 banks distinct", "v_pk_add_f32 v[10:11], v[12:13], v[14:15]\n")           \
-  X(25, "v_pk_mul_f32 banks distinct", "v_pk_mul_f32 v[10:11], v[12:13], v[14:15]\n")
+  X(25, "v_pk_mul_f32 banks distinct", "v_pk_mul_f32 v[10:11], v[12:13], v[14:15]\n")           \
+  X(26, "v_lshlrev_b32_sdwa byte3 (K1 table address)",                                          \
+    "v_lshlrev_b32_sdwa v10, v11, v12 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3\n") \
+  X(27, "v_bfe_u32 v,v,inl,inl", "v_bfe_u32 v10, v11, 8, 8\n")                                  \
+  X(28, "v_perm_b32 banks 3/0/1", "v_perm_b32 v10, v11, v12, v13\n")                            \
+  X(29, "v_and_b32 literal,v", "v_and_b32 v10, 0xff0, v11\n")                                   \
+  X(30, "v_lshrrev_b32 20,v", "v_lshrrev_b32 v10, 20, v11\n")                                   \
+  X(31, "v_mul_u32_u24 v,v", "v_mul_u32_u24 v10, v11, v12\n")                                   \
+  X(32, "v_lshl_or_b32 v,inl,v", "v_lshl_or_b32 v10, v11, 4, v12\n")                            \
+  X(33, "v_and_or_b32 banks 3/0/1", "v_and_or_b32 v10, v11, v12, v13\n")                        \
+  X(34, "v_cndmask_b32_e32 vcc", "v_cndmask_b32_e32 v10, v11, v12, vcc\n")                       \
+  X(35, "v_cmp_lt_u64_e64 -> sgpr", "v_cmp_lt_u64_e64 s[20:21], v[12:13], v[14:15]\n")          \
+  X(36, "v_mad_u32_u24 banks 3/0/1", "v_mad_u32_u24 v10, v11, v12, v13\n")                      \
+  X(37, "v_lshlrev_b64 inl", "v_lshlrev_b64 v[10:11], 4, v[12:13]\n")                           \
+  X(38, "v_lshl_add_u32 v,inl,v", "v_lshl_add_u32 v10, v11, 4, v12\n")                          \
+  X(39, "v_add_co_u32 vcc", "v_add_co_u32 v10, vcc, v11, v12\n")                                \
+  X(40, "v_lshrrev_b32_sdwa byte1", "v_lshrrev_b32_sdwa v10, v11, v12 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1\n") \
+  X(41, "v_and_b32_sdwa byte2 (src0 sel)", "v_and_b32_sdwa v10, v11, v12 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD\n")
 
 #define KERNEL(id, name, text)                                        \
   __global__ __launch_bounds__(256) void k##id(int* sink) {           \
