@@ -48,6 +48,13 @@ for st in $STAGES; do
     bench2r)  # the driver's launch shape on one GPU (two members of GPU 0)
       run bench_2rank 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29511 bench.py --gpus 2 --devices 0,0 --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
+    bench_dist)  # one process per GPU layout (--mode dist) at world 1: the per-rank sketch + row-tile pairs path
+      bench bench_dist 300 --mode dist --steps 20 --warmup 5 --no-cpu-baseline --no-files ;;
+    bench_dist2)  # --mode dist at world 2 on one GPU: gloo all-gather through host memory (RCCL refuses two ranks on one GPU)
+      run bench_dist2 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29512 bench.py --gpus 2 --mode dist --dist-backend gloo --steps 10 --warmup 2 --no-cpu-baseline \
+        --no-files || exit $?
+      tail -n 1 "$OUT/bench_dist2.log" > "$OUT/bench_dist2.json" ;;
     prof)  # kernel trace + stats of the C3 bench (per-kernel averages for profiles/)
       run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c3 -- \
         python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-files || exit $? ;;
