@@ -55,6 +55,8 @@ for st in $STAGES; do
         --master-port 29512 bench.py --gpus 2 --mode dist --dist-backend gloo --steps 10 --warmup 2 --no-cpu-baseline \
         --no-files || exit $?
       tail -n 1 "$OUT/bench_dist2.log" > "$OUT/bench_dist2.json" ;;
+    bench_shards)  # one member's share of C3 at 8/4/2 GPUs (1250/2500/5000 genomes) on one device: per-launch fixed costs
+      for g in 1250 2500 5000; do bench bench_g$g 200 --genomes $g --steps 30 --warmup 5 --no-cpu-baseline --no-files; done ;;
     prof)  # kernel trace + stats of the C3 bench (per-kernel averages for profiles/)
       run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o c3 -- \
         python3 -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-files || exit $? ;;

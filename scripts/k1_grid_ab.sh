@@ -1,9 +1,20 @@
 #!/bin/bash
-# K1 grid A/B: C3 bench per GALAHGPU_K1_WG_PER_CU value (args), K1 avg ms each.
+# K1 grid A/B: the bench per GALAHGPU_K1_WG_PER_CU value, K1/finalize/K2 ms each.
+#   CONFIGS="c3 c5" PASSES=2 STEPS=10 OUT=r3ai bash scripts/k1_grid_ab.sh 96 108 112 120 132
+# (round 3 ran 56/112/224/28 at C3 and C5 -> profiles/r03_*; 96-132 at C3 -> profiles/r03_t/)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-for w in "$@"; do
-  GALAHGPU_K1_WG_PER_CU=$w timeout -k 10 240 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-files > gpurun_out/k1grid_$w.log 2>&1 || exit $?
-  python -c "import json; d=json.loads(open('gpurun_out/k1grid_$w.log').read().strip().splitlines()[-1]); print('wg/cu', $w, d['ms_per_step'], d['phase_ms'], d['roofline']['kernels'][0]['avg_ms'])"
+out="gpurun_out/${OUT:-k1grid}"
+mkdir -p "$out"
+for pass in $(seq 1 "${PASSES:-1}"); do
+  for w in "$@"; do
+    for cfg in ${CONFIGS:-c3}; do
+      log="$out/wg${w}_${cfg}_p$pass.log"
+      GALAHGPU_K1_WG_PER_CU=$w timeout -k 10 300 python3 -u bench.py --config $cfg --steps "${STEPS:-10}" --warmup 2 \
+        --no-cpu-baseline --no-files > "$log" 2>&1 || exit 1
+      tail -n 1 "$log" > "${log%.log}.json"
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], sys.argv[3], sys.argv[4], d['ms_per_step'], d['kernel_ms_per_step'])" \
+        "${log%.log}.json" "$pass" "$w" "$cfg"
+    done
+  done
 done
