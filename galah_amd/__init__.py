@@ -344,8 +344,10 @@ def _take_pairs(ptr, n):
     if n == 0:
         _L.gg_free(ptr)
         return np.zeros(0, dtype=PAIR_DTYPE)
-    buf = (ctypes.c_char * (n * PAIR_DTYPE.itemsize)).from_address(ptr.value)
-    out = np.frombuffer(buf, dtype=PAIR_DTYPE).copy()
+    # one memmove into a fresh array (a ctypes array type per call, or
+    # np.ctypeslib.as_array, cost ~0.1-0.25 ms at C3's 15k pairs)
+    out = np.empty(n, dtype=PAIR_DTYPE)
+    ctypes.memmove(out.ctypes.data, ptr.value, n * PAIR_DTYPE.itemsize)
     _L.gg_free(ptr)
     return out
 
@@ -479,7 +481,8 @@ class Context:
     @staticmethod
     def _pairs_ani(pp, ap, n):
         if n:
-            ani = np.ctypeslib.as_array(ctypes.cast(ap, ctypes.POINTER(ctypes.c_float)), shape=(n,)).copy()
+            ani = np.empty(n, np.float32)
+            ctypes.memmove(ani.ctypes.data, ap.value, n * 4)
         else:
             ani = np.zeros(0, np.float32)
         _L.gg_free(ap)
