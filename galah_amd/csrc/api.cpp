@@ -975,9 +975,9 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
   return GG_OK;
 }
 
-// Passing pairs of tiles [tb, te) appended to res; from kDeviceSortPairs
-// up to 2^31 of them they come sorted by (i, j) (sorted on the device:
-// pairs_sorted_on_device).
+// Passing pairs of tiles [tb, te) appended to res in (i, j) order: from
+// kDeviceSortPairs up to 2^31 of them sorted on the device, otherwise on
+// the calling thread.
 gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
                               uint64_t tb, uint64_t te, float min_ani, std::vector<gg_pair>& res,
                               hipStream_t st) {
@@ -1004,25 +1004,31 @@ gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d
         if (cnt) {
           GG_HIP(c, hipMemcpyAsync(res.data() + at, d_out, cnt * sizeof(gg_pair), hipMemcpyDeviceToHost, st));
           GG_HIP(c, hipStreamSynchronize(st));
+          // in (i, j) order here, on the calling (member) thread: the members
+          // of a multi-device call sort their parts at the same time
+          std::sort(res.begin() + at, res.end(), [](const gg_pair& x, const gg_pair& y) {
+            return x.i != y.i ? x.i < y.i : x.j < y.j;
+          });
         }
         return GG_OK;
       }
-      // many: sorted by (i, j) on the device, taken in order
+      // many: sorted by (i, j) on the device and copied out in that order
+      // (scratch: keys and sorted keys [cnt] u64, positions and sorted
+      // positions [cnt] u32, the sorted pairs [cnt] x 16 B)
       uint64_t* d_kv;
       void* d_tmp;
       const size_t tmp_bytes = pair_sort_tmp_bytes(cnt, n);
-      GG_HIP(c, scratch_t(c, "pair_sort_kv", 4 * cnt, &d_kv));
+      GG_HIP(c, scratch_t(c, "pair_sort_kv", 5 * cnt, &d_kv));
       GG_HIP(c, scratch(c, "pair_sort_tmp", std::max<size_t>(tmp_bytes, 16), &d_tmp));
-      GG_HIP(c, sort_pairs_device(d_out, cnt, n, d_kv, d_kv + cnt, d_kv + 2 * cnt, d_kv + 3 * cnt, d_tmp, tmp_bytes,
+      uint32_t* d_idx = (uint32_t*)(d_kv + 2 * cnt);
+      gg_pair* d_sorted = (gg_pair*)(d_kv + 3 * cnt);
+      GG_HIP(c, sort_pairs_device(d_out, cnt, n, d_kv, d_kv + cnt, d_idx, d_idx + cnt, d_sorted, d_tmp, tmp_bytes,
                                   st));
-      uint64_t* kv;
-      GG_HIP(c, host_scratch_t(c, "pair_sort_kv", 2 * cnt, &kv));
-      GG_HIP(c, hipMemcpyAsync(kv, d_kv + 2 * cnt, 2 * cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+      gg_pair* h_sorted;
+      GG_HIP(c, host_scratch_t(c, "pair_sorted", cnt, &h_sorted));
+      GG_HIP(c, hipMemcpyAsync(h_sorted, d_sorted, cnt * sizeof(gg_pair), hipMemcpyDeviceToHost, st));
       GG_HIP(c, hipStreamSynchronize(st));
-      for (uint64_t x = 0; x < cnt; ++x) {
-        const uint64_t key = kv[x], val = kv[cnt + x];
-        res[at + x] = gg_pair{(uint32_t)(key / n), (uint32_t)(key % n), (uint32_t)(val >> 32), (uint32_t)val};
-      }
+      memcpy(res.data() + at, h_sorted, cnt * sizeof(gg_pair));
       return GG_OK;
     }
     cap = cnt;

@@ -181,9 +181,9 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
 gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
                      uint64_t tb, uint64_t te, float min_ani, gg_pair* d_out, uint64_t cap,
                      uint64_t* d_count, hipStream_t st);
-// K2 over tiles [tb, te), passing pairs appended to res (unsorted).
+// K2 over tiles [tb, te), passing pairs appended to res, the appended part
+// in (i, j) order.
 constexpr uint64_t kDeviceSortPairs = 4096;  // pairs_range_to_host sorts this many or more on the device
-inline bool pairs_sorted_on_device(uint64_t cnt) { return cnt >= kDeviceSortPairs && cnt < (1ull << 31); }
 gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n,
                               uint64_t tb, uint64_t te, float min_ani, std::vector<gg_pair>& res,
                               hipStream_t st);

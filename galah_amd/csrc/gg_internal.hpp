@@ -296,12 +296,13 @@ size_t index_bucket_sort_tmp_bytes(uint64_t total);
 constexpr uint32_t kIndexCoarse = 4096;  // coarse bins of the bucketed build
 hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st);
 bool index_ents16(uint32_t n);
-// Passing pairs sorted by (i, j) on the device: keys_out = i * n + j,
-// vals_out = common << 32 | total (every buffer [cnt])
+// Passing pairs sorted by (i, j) on the device into sorted[cnt] (keys,
+// keys_out: [cnt] u64; idx, idx_out: [cnt] u32; cnt < 2^31)
 uint32_t pair_key_bits(uint32_t n);
 size_t pair_sort_tmp_bytes(uint64_t cnt, uint32_t n);
-hipError_t sort_pairs_device(const gg_pair* d_pairs, uint64_t cnt, uint32_t n, uint64_t* keys, uint64_t* vals,
-                             uint64_t* keys_out, uint64_t* vals_out, void* tmp, size_t tmp_bytes, hipStream_t st);
+hipError_t sort_pairs_device(const gg_pair* d_pairs, uint64_t cnt, uint32_t n, uint64_t* keys, uint64_t* keys_out,
+                             uint32_t* idx, uint32_t* idx_out, gg_pair* sorted, void* tmp, size_t tmp_bytes,
+                             hipStream_t st);
 
 // synth.hip
 hipError_t launch_synth(uint32_t first_genome, uint32_t n_genomes, uint32_t genome_len,

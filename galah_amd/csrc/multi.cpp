@@ -168,20 +168,43 @@ gg_status gather_pairs_merge(gg_ctx* c, const std::vector<gg_ctx*>& ms, const st
   if (st != GG_OK) return st;
   c->phase_ms[GG_PHASE_PAIRS] = ms_since(t0);
   t0 = Clock::now();
-  // every member's part in (i, j) order (large parts come sorted from the
-  // device, pairs_range_to_host), then merged: SortedPairGenomeDistanceCache
-  // order
-  for (auto& p : part)
-    if (!pairs_sorted_on_device(p.size())) std::sort(p.begin(), p.end(), pair_ij_less);
+  // every member's part comes in (i, j) order (pairs_range_to_host: sorted
+  // on the device, or few and sorted by the member's thread), then merged:
+  // SortedPairGenomeDistanceCache order
   res.clear();
-  for (auto& p : part) {
-    if (res.empty()) {
-      res.swap(p);
-      continue;
+  // members given whole tile rows (the inverted index) hold disjoint,
+  // increasing row ranges: their parts are already in order one after the
+  // other and are concatenated; otherwise (a tile row split between members
+  // by the gate kernel's partition) merged
+  size_t total = 0;
+  bool ordered = true;
+  const gg_pair* last = nullptr;
+  for (const auto& p : part) {
+    if (p.empty()) continue;
+    total += p.size();
+    if (last && !pair_ij_less(*last, p.front())) ordered = false;
+    last = &p.back();
+  }
+  if (ordered) {
+    for (auto& p : part) {
+      if (p.empty()) continue;
+      if (res.empty() && p.size() == total) {
+        res.swap(p);
+        break;
+      }
+      if (res.empty()) res.reserve(total);
+      res.insert(res.end(), p.begin(), p.end());
     }
-    std::vector<gg_pair> merged(res.size() + p.size());
-    std::merge(res.begin(), res.end(), p.begin(), p.end(), merged.begin(), pair_ij_less);
-    res.swap(merged);
+  } else {
+    for (auto& p : part) {
+      if (res.empty()) {
+        res.swap(p);
+        continue;
+      }
+      std::vector<gg_pair> merged(res.size() + p.size());
+      std::merge(res.begin(), res.end(), p.begin(), p.end(), merged.begin(), pair_ij_less);
+      res.swap(merged);
+    }
   }
   c->phase_ms[GG_PHASE_MERGE] = ms_since(t0);
   return GG_OK;
@@ -190,9 +213,19 @@ gg_status gather_pairs_merge(gg_ctx* c, const std::vector<gg_ctx*>& ms, const st
 gg_status pairs_with_ani(gg_ctx* c, const std::vector<gg_pair>& res, gg_pair** pairs, float** ani,
                          uint64_t* n_out) {
   auto t0 = Clock::now();
-  std::vector<float> a(res.size());
-  // f64 log per pair (src/finch.rs:56): on several threads for large outputs
   const size_t m = res.size();
+  // the caller's arrays are filled in place (no staging vector for the ANI)
+  *pairs = copy_out(res);
+  *ani = (float*)malloc(std::max<size_t>(m, 1) * sizeof(float));
+  if (!*pairs || !*ani) {
+    free(*pairs);
+    free(*ani);
+    *pairs = nullptr;
+    *ani = nullptr;
+    return fail(c, GG_ERR_OUT_OF_MEMORY, "out of host memory");
+  }
+  float* a = *ani;
+  // f64 log per pair (src/finch.rs:56): on several threads for large outputs
   const int T = m >= (1u << 16) ? (int)std::min<size_t>(16, std::max(1, ingest_threads(c->host_threads))) : 1;
   std::vector<std::thread> th;
   auto work = [&](int t) {
@@ -201,16 +234,7 @@ gg_status pairs_with_ani(gg_ctx* c, const std::vector<gg_pair>& res, gg_pair** p
   for (int t = 1; t < T; ++t) th.emplace_back(work, t);
   work(0);
   for (auto& x : th) x.join();
-  *pairs = copy_out(res);
-  *ani = copy_out(a);
-  if (!*pairs || !*ani) {
-    free(*pairs);
-    free(*ani);
-    *pairs = nullptr;
-    *ani = nullptr;
-    return fail(c, GG_ERR_OUT_OF_MEMORY, "out of host memory");
-  }
-  *n_out = res.size();
+  *n_out = m;
   c->phase_ms[GG_PHASE_MERGE] += ms_since(t0);
   return GG_OK;
 }

@@ -891,17 +891,25 @@ hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t
 }
 
 // Passing pairs in (i, j) order on the device (the output of every K2 form
-// is an atomic append): key i * n + j, value common << 32 | total, radix
-// sorted over the key's significant bits, so the host takes them in order
-// (C4's 153k pairs: the host radix sort took ~1 ms of a 2.3 ms merge).
+// is an atomic append): key i * n + j, value the pair's position, radix
+// sorted over the key's significant bits, then the pairs gathered in that
+// order, so the host copies them out as they are (C4's 153k pairs: the host
+// radix sort took ~1 ms of a 2.3 ms merge; unpacking sorted keys and values
+// on the host, one 64-bit division per pair, ~0.1 ms of C3's 15k).
 namespace {
-__global__ __launch_bounds__(256) void pair_keys_kernel(const gg_pair* __restrict__ p, uint64_t cnt, uint32_t n,
-                                                        uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
-  for (uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x; x < cnt; x += (uint64_t)gridDim.x * 256) {
+__global__ __launch_bounds__(256) void pair_keys_kernel(const gg_pair* __restrict__ p, uint32_t cnt, uint32_t n,
+                                                        uint64_t* __restrict__ keys, uint32_t* __restrict__ idx) {
+  for (uint32_t x = blockIdx.x * 256 + threadIdx.x; x < cnt; x += gridDim.x * 256) {
     const gg_pair q = p[x];
     keys[x] = (uint64_t)q.i * n + q.j;
-    vals[x] = ((uint64_t)q.common << 32) | q.total;
+    idx[x] = x;
   }
+}
+
+__global__ __launch_bounds__(256) void pair_gather_kernel(const gg_pair* __restrict__ p, uint32_t cnt,
+                                                          const uint32_t* __restrict__ idx,
+                                                          gg_pair* __restrict__ sorted) {
+  for (uint32_t y = blockIdx.x * 256 + threadIdx.x; y < cnt; y += gridDim.x * 256) sorted[y] = p[idx[y]];
 }
 }  // namespace
 
@@ -915,21 +923,26 @@ uint32_t pair_key_bits(uint32_t n) {
 size_t pair_sort_tmp_bytes(uint64_t cnt, uint32_t n) {
   size_t bytes = 0;
   (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                           (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)cnt, 0,
+                                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)cnt, 0,
                                            (int)pair_key_bits(n));
   return bytes;
 }
 
-hipError_t sort_pairs_device(const gg_pair* d_pairs, uint64_t cnt, uint32_t n, uint64_t* keys, uint64_t* vals,
-                             uint64_t* keys_out, uint64_t* vals_out, void* tmp, size_t tmp_bytes, hipStream_t st) {
+hipError_t sort_pairs_device(const gg_pair* d_pairs, uint64_t cnt, uint32_t n, uint64_t* keys, uint64_t* keys_out,
+                             uint32_t* idx, uint32_t* idx_out, gg_pair* sorted, void* tmp, size_t tmp_bytes,
+                             hipStream_t st) {
   if (cnt == 0) return hipSuccess;
-  hipLaunchKernelGGL(pair_keys_kernel, dim3((uint32_t)std::min<uint64_t>(4096, (cnt + 255) / 256)), dim3(256), 0, st,
-                     d_pairs, cnt, n, keys, vals);
+  if (cnt >= (1ull << 31)) return hipErrorInvalidValue;  // (the sort's count is an int)
+  const dim3 grid((uint32_t)std::min<uint64_t>(4096, (cnt + 255) / 256));
+  hipLaunchKernelGGL(pair_keys_kernel, grid, dim3(256), 0, st, d_pairs, (uint32_t)cnt, n, keys, idx);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // (bit 0 up: see index_build_buckets on rocPRIM's merge-sort path)
-  return hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_out, vals, vals_out, (int)cnt, 0,
-                                            (int)pair_key_bits(n), st);
+  e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, keys, keys_out, idx, idx_out, (int)cnt, 0,
+                                         (int)pair_key_bits(n), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pair_gather_kernel, grid, dim3(256), 0, st, d_pairs, (uint32_t)cnt, idx_out, sorted);
+  return hipGetLastError();
 }
 
 // The bucketed build stores each run member as its 16-bit row when rows fit
