@@ -131,7 +131,7 @@ __global__ __launch_bounds__(kScanThreads) void index_scan_kernel(const uint64_t
 // Entry of row i, k < len_i, value i << kbits | k:
 //   full build:     at offs[i] + k, keys = h >> sh (32 bits), vals = lo32(h) << 32 | value
 //   bucketed build: at i * stride + k (every slot k < stride: the sort's item
-//                   count is known before the row lengths are), keys =
+//                   count is known before the row lengths are), 16-bit keys =
 //                   bucket_of(h) or kBucketPad past len_i, vals32 = value
 template <bool BUCKET>
 __global__ __launch_bounds__(256) void index_fill_kernel(const uint64_t* __restrict__ sk,
@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void index_fill_kernel(const uint64_t* __restr
     if (BUCKET) {  // row-major slots i * stride + k, unused slots keyed past every bucket
       const uint64_t o = (uint64_t)i * stride;
       for (uint32_t k = threadIdx.x; k < stride; k += 256) {
-        keys[o + k] = k < len ? bucket_of(row[k], ks, bbase) : kBucketPad;
+        ((uint16_t*)keys)[o + k] = (uint16_t)(k < len ? bucket_of(row[k], ks, bbase) : kBucketPad);
         ((uint32_t*)vals)[o + k] = (i << kbits) | k;
       }
       continue;
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(256) void index_fill_range_kernel(
         const uint64_t at = o + base + before;
         const uint32_t v = (i << kbits) | k;
         if (BUCKET) {
-          keys[at] = bucket_of(h, ks, bbase);
+          ((uint16_t*)keys)[at] = (uint16_t)bucket_of(h, ks, bbase);
           ((uint32_t*)vals)[at] = v;
         } else {
           keys[at] = (uint32_t)(h >> sh);
@@ -487,13 +487,13 @@ constexpr uint32_t kBucketPer = kBucketCap / kBucketThreads;
 static_assert(kBucketCap % kBucketThreads == 0 && kBucketSlots % kBucketThreads == 0 && kBucketCap < 4096,
               "bucket table: group start and size packed as 12 + 12 bits");
 
-__global__ __launch_bounds__(256) void bucket_bounds_kernel(const uint32_t* __restrict__ keys, uint64_t total,
+__global__ __launch_bounds__(256) void bucket_bounds_kernel(const uint16_t* __restrict__ keys, uint64_t total,
                                                             const uint32_t* __restrict__ nbuckets_p,
                                                             uint32_t* __restrict__ bstart) {
   const uint32_t nbuckets = *nbuckets_p;
   for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p <= total; p += (uint64_t)gridDim.x * 256) {
-    const uint32_t cur = p < total ? min(keys[p], nbuckets) : nbuckets;
-    const uint32_t first = p > 0 ? min(keys[p - 1], nbuckets) + 1u : 0u;
+    const uint32_t cur = p < total ? min((uint32_t)keys[p], nbuckets) : nbuckets;
+    const uint32_t first = p > 0 ? min((uint32_t)keys[p - 1], nbuckets) + 1u : 0u;
     for (uint32_t bk = first; bk <= cur; ++bk) bstart[bk] = (uint32_t)p;
   }
 }
@@ -840,15 +840,15 @@ hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_
   uint32_t* vin = (uint32_t*)b.vals_in;
   uint32_t* vout = (uint32_t*)b.vals_out;
   size_t bytes = b.sort_tmp_bytes;
-  e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, b.keys_in, b.keys_out, vin, vout, (int)total, 0,
-                                         (int)kBucketKeyBits, st);
+  e = hipcub::DeviceRadixSort::SortPairs(b.sort_tmp, bytes, (const uint16_t*)b.keys_in, (uint16_t*)b.keys_out, vin,
+                                         vout, (int)total, 0, (int)kBucketKeyBits, st);
   if (e != hipSuccess) return e;
   // (every bucket start is written when the keys are sorted; a bucket whose
   // bounds come out inconsistent is reported, never read through)
   e = hipMemsetAsync(b.bstart, 0xFF, ((size_t)nb_bound + 1) * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(bucket_bounds_kernel, dim3((uint32_t)std::min<uint64_t>(16384, total / 256 + 1)), dim3(256), 0,
-                     st, b.keys_out, total, nbuckets_d, b.bstart);
+                     st, (const uint16_t*)b.keys_out, total, nbuckets_d, b.bstart);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   // the entries land in keys_in (free after the sort), as with the run pass
@@ -872,7 +872,7 @@ size_t index_sort_tmp_bytes(uint64_t total, uint32_t end_bit) {
 
 size_t index_bucket_sort_tmp_bytes(uint64_t total) {
   size_t bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint16_t*)nullptr, (uint16_t*)nullptr,
                                            (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)total, 0,
                                            (int)kBucketKeyBits);
   return bytes;
