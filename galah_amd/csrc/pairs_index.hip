@@ -491,10 +491,31 @@ __global__ __launch_bounds__(256) void bucket_bounds_kernel(const uint16_t* __re
                                                             const uint32_t* __restrict__ nbuckets_p,
                                                             uint32_t* __restrict__ bstart) {
   const uint32_t nbuckets = *nbuckets_p;
-  for (uint64_t p = (uint64_t)blockIdx.x * 256 + threadIdx.x; p <= total; p += (uint64_t)gridDim.x * 256) {
-    const uint32_t cur = p < total ? min((uint32_t)keys[p], nbuckets) : nbuckets;
-    const uint32_t first = p > 0 ? min((uint32_t)keys[p - 1], nbuckets) + 1u : 0u;
-    for (uint32_t bk = first; bk <= cur; ++bk) bstart[bk] = (uint32_t)p;
+  // 8 consecutive positions per thread (one 16-byte load of keys)
+  for (uint64_t p0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 8; p0 <= total; p0 += (uint64_t)gridDim.x * 256 * 8) {
+    uint16_t k[8];
+    if (p0 + 8 <= total) {
+      const uint4 v = *(const uint4*)(keys + p0);
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        k[2 * j] = (uint16_t)w[j];
+        k[2 * j + 1] = (uint16_t)(w[j] >> 16);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) k[j] = p0 + j < total ? keys[p0 + j] : 0;
+    }
+    uint32_t prev = p0 > 0 ? min((uint32_t)keys[p0 - 1], nbuckets) : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint64_t p = p0 + j;
+      if (p > total) break;
+      const uint32_t cur = p < total ? min((uint32_t)k[j], nbuckets) : nbuckets;
+      const uint32_t first = p > 0 ? prev + 1u : 0u;
+      for (uint32_t bk = first; bk <= cur; ++bk) bstart[bk] = (uint32_t)p;
+      prev = cur;
+    }
   }
 }
 
@@ -847,7 +868,7 @@ hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_
   // bounds come out inconsistent is reported, never read through)
   e = hipMemsetAsync(b.bstart, 0xFF, ((size_t)nb_bound + 1) * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(bucket_bounds_kernel, dim3((uint32_t)std::min<uint64_t>(16384, total / 256 + 1)), dim3(256), 0,
+  hipLaunchKernelGGL(bucket_bounds_kernel, dim3((uint32_t)std::min<uint64_t>(16384, total / 2048 + 1)), dim3(256), 0,
                      st, (const uint16_t*)b.keys_out, total, nbuckets_d, b.bstart);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
