@@ -700,6 +700,7 @@ __device__ __forceinline__ uint32_t part_of(uint32_t j, uint32_t plog2) {
 // row's column interval, from the runs of its hashes, then the finch test.
 // Rows whose partners overflow the LDS map are redone in 2, 4, ... passes,
 // each counting one hash class of partners.
+constexpr uint32_t kMemberLoads = 8;  // run members loaded together per step
 template <bool E16>
 __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a) {
   __shared__ uint32_t mkey[kMap];  // partner + 1 (0 = empty)
@@ -731,34 +732,50 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
     for (uint32_t x = tid; x < kMap; x += kRowThreads) mkey[x] = 0u, mcnt[x] = 0u;
     if (tid == 0) fill = 0u, over = 0u;
     __syncthreads();
+    // the next entry's runinfo and up to kMemberLoads members of a run are
+    // loaded before the map's atomics (one member load at a time left each
+    // thread waiting on L2 latency per member)
+    uint64_t info_next = tid < la ? ri[tid] : 0ull;
     for (uint32_t k = tid; k < la; k += kRowThreads) {
       if (over) break;
-      const uint64_t info = ri[k];
+      const uint64_t info = info_next;
+      info_next = k + kRowThreads < la ? ri[k + kRowThreads] : 0ull;
       const uint32_t g = (uint32_t)(info >> 32);
       if (g < 2) continue;
       const uint32_t st = (uint32_t)info;
-      for (uint32_t q = st; q < st + g; ++q) {
-        const uint32_t j = E16 ? (uint32_t)((const uint16_t*)a.vals)[q] : a.vals[q] >> a.kbits;
-        if (j < jlo || j >= jhi) continue;
-        if (plog2 && part_of(j, plog2) != p) continue;
-        uint32_t h = (j * 0x85EBCA6Bu) >> (32 - kMapLog2);
-        for (uint32_t probe = 0;; ++probe) {
-          const uint32_t old = atomicCAS(&mkey[h], 0u, j + 1u);
-          if (old == 0u) {
-            if (atomicAdd(&fill, 1u) >= kMapFull) over = 1u;
-          }
-          if (old == 0u || old == j + 1u) {
-            atomicAdd(&mcnt[h], 1u);
-            break;
-          }
-          if (probe >= kMap) {
-            over = 1u;
-            break;
-          }
-          h = (h + 1) & (kMap - 1);
+      bool stop = false;
+      for (uint32_t q0 = st; q0 < st + g && !stop; q0 += kMemberLoads) {
+        uint32_t jv[kMemberLoads];
+#pragma unroll
+        for (uint32_t u = 0; u < kMemberLoads; ++u) {
+          const uint32_t q = q0 + u;
+          jv[u] = q < st + g ? (E16 ? (uint32_t)((const uint16_t*)a.vals)[q] : a.vals[q] >> a.kbits) : jhi;
         }
-        if (over) break;
+#pragma unroll
+        for (uint32_t u = 0; u < kMemberLoads; ++u) {
+          const uint32_t j = jv[u];
+          if (stop || j < jlo || j >= jhi) continue;
+          if (plog2 && part_of(j, plog2) != p) continue;
+          uint32_t h = (j * 0x85EBCA6Bu) >> (32 - kMapLog2);
+          for (uint32_t probe = 0;; ++probe) {
+            const uint32_t old = atomicCAS(&mkey[h], 0u, j + 1u);
+            if (old == 0u) {
+              if (atomicAdd(&fill, 1u) >= kMapFull) over = 1u;
+            }
+            if (old == 0u || old == j + 1u) {
+              atomicAdd(&mcnt[h], 1u);
+              break;
+            }
+            if (probe >= kMap) {
+              over = 1u;
+              break;
+            }
+            h = (h + 1) & (kMap - 1);
+          }
+          if (over) stop = true;
+        }
       }
+      if (stop) break;
     }
     __syncthreads();
     if (over) {
