@@ -372,7 +372,15 @@ def _runs_arg(runs):
         if nbytes % RUN_DTYPE.itemsize or not runs.is_contiguous():
             raise ValueError("device run table: contiguous 16-byte records")
         return (runs.data_ptr() if nbytes else None), nbytes // RUN_DTYPE.itemsize, runs
-    runs = np.ascontiguousarray(runs, dtype=RUN_DTYPE)
+    if hasattr(runs, "data_ptr"):  # a host torch tensor of 16-byte records (device_runs(..., "cpu"))
+        nbytes = runs.numel() * runs.element_size()
+        if nbytes % RUN_DTYPE.itemsize:
+            raise ValueError("host run table tensor: 16-byte records")
+        runs = runs.contiguous().numpy().view(np.uint8).reshape(-1).view(RUN_DTYPE)
+        return runs.ctypes.data, len(runs), runs
+    if not (isinstance(runs, np.ndarray) and runs.dtype == RUN_DTYPE):
+        raise TypeError("run table: a RUN_DTYPE array or a device tensor of 16-byte records")
+    runs = np.ascontiguousarray(runs)
     return runs.ctypes.data, len(runs), runs
 
 

@@ -178,13 +178,8 @@ SketchGeom sketch_geom(uint32_t s) {
   return g;
 }
 
-uint64_t initial_tau(uint64_t nk, uint32_t s, double over) {
-  const long double want = (long double)over * (long double)s;
-  if (nk == 0 || want >= (long double)nk) return kEmpty;
-  const long double t = want / (long double)nk * 18446744073709551616.0L;
-  if (t >= 18446744073709551615.0L) return kEmpty;
-  return (uint64_t)t;
-}
+// (the same expression as the one-batch path's first_pass_kernel)
+uint64_t initial_tau(uint64_t nk, uint32_t s, double over) { return first_tau(nk, over * (double)s); }
 
 struct TauSearch {
   uint64_t tau;
@@ -431,7 +426,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
     GG_HIP(c, timed_launch(c, GG_KERNEL_SKETCH, 0, st, [&] { return launch_sketch_candidates(c->k, a, grid, st); }));
     GG_HIP(c, timed_launch(c, GG_KERNEL_FINALIZE, n_genomes, st, [&] {
       return launch_sketch_finalize(d_slot_list, n_genomes, d_slot_genome, d_tau, d_table, geom.cap_log2, d_flags,
-                                    c->s, geom.sort_pow2, d_row_of, d_out, d_lens, d_status, st);
+                                    c->s, geom.sort_pow2, d_row_of, d_out, d_lens, d_status, st, d_ix);
     }));
   }
   // the index, and in one batch the first pass's taus and status (one batch:
@@ -1024,11 +1019,18 @@ gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d
       gg_pair* d_sorted = (gg_pair*)(d_kv + 3 * cnt);
       GG_HIP(c, sort_pairs_device(d_out, cnt, n, d_kv, d_kv + cnt, d_idx, d_idx + cnt, d_sorted, d_tmp, tmp_bytes,
                                   st));
+      // staged through a pinned chunk of at most kPairStage pairs (16 MiB), so
+      // a long-lived context holds no page-locked memory sized by its largest
+      // result
+      constexpr uint64_t kPairStage = 1ull << 20;
       gg_pair* h_sorted;
-      GG_HIP(c, host_scratch_t(c, "pair_sorted", cnt, &h_sorted));
-      GG_HIP(c, hipMemcpyAsync(h_sorted, d_sorted, cnt * sizeof(gg_pair), hipMemcpyDeviceToHost, st));
-      GG_HIP(c, hipStreamSynchronize(st));
-      memcpy(res.data() + at, h_sorted, cnt * sizeof(gg_pair));
+      GG_HIP(c, host_scratch_t(c, "pair_sorted", std::min(cnt, kPairStage), &h_sorted));
+      for (uint64_t x = 0; x < cnt; x += kPairStage) {
+        const uint64_t m = std::min(kPairStage, cnt - x);
+        GG_HIP(c, hipMemcpyAsync(h_sorted, d_sorted + x, m * sizeof(gg_pair), hipMemcpyDeviceToHost, st));
+        GG_HIP(c, hipStreamSynchronize(st));
+        memcpy(res.data() + at + x, h_sorted, m * sizeof(gg_pair));
+      }
       return GG_OK;
     }
     cap = cnt;

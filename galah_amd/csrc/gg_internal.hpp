@@ -79,6 +79,19 @@ hipError_t launch_run_index(const RunIndexDev& x, hipStream_t st);
 hipError_t launch_first_pass(const uint64_t* nk, uint32_t n_genomes, double want, uint64_t* tau,
                              uint32_t* slot_genome, uint32_t* slot_list, hipStream_t st);
 
+// First bottom-s threshold of a genome with nk k-mers: tau = want / nk * 2^64
+// (want = over * s expected candidates), or 2^64 - 1 when the genome has at
+// most `want` k-mers (every distinct hash is a candidate).  One formula for
+// the device's first pass (runindex.hip) and the host's multi-batch path.
+__host__ __device__ inline uint64_t first_tau(uint64_t nk, double want) {
+  uint64_t t = ~0ull;
+  if (nk != 0 && want < (double)nk) {
+    const double x = want / (double)nk * 18446744073709551616.0;
+    if (x < 18446744073709549568.0) t = (uint64_t)x;  // (the largest double below 2^64)
+  }
+  return t;
+}
+
 // sketch.hip
 hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,
                                     hipStream_t st);
@@ -89,7 +102,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   uint32_t* flags, uint32_t s,
                                   uint32_t sort_pow2, const uint32_t* row_of, uint64_t* out,
                                   uint32_t* lens, uint32_t* status,
-                                  hipStream_t st);
+                                  hipStream_t st, const uint64_t* bad = nullptr);
 
 // pairs.hip
 struct PairsLaunch {

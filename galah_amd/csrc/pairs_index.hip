@@ -780,8 +780,11 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
     __syncthreads();
     if (over) {
       if (plog2 < a.max_split_log2) {  // too many partners for one map: split them in twice as many classes
+        // part_of takes the top plog2 bits of one hash, so class p at plog2 is
+        // classes 2p and 2p + 1 at plog2 + 1: the classes below p were already
+        // emitted as classes below 2p, which must not be counted again
         ++plog2;
-        p = 0;
+        p *= 2;
         __syncthreads();
         continue;
       }

@@ -87,13 +87,7 @@ __global__ __launch_bounds__(256) void first_pass_kernel(const uint64_t* __restr
                                                          uint32_t* __restrict__ slot_genome,
                                                          uint32_t* __restrict__ slot_list) {
   for (uint32_t g = blockIdx.x * 256 + threadIdx.x; g < n_genomes; g += gridDim.x * 256) {
-    const uint64_t k = nk[g];
-    uint64_t t = ~0ull;
-    if (k != 0 && want < (double)k) {
-      const double x = want / (double)k * 18446744073709551616.0;
-      if (x < 18446744073709549568.0) t = (uint64_t)x;  // (the largest double below 2^64)
-    }
-    tau[g] = t;
+    tau[g] = first_tau(nk[g], want);
     slot_genome[g] = g;
     slot_list[g] = g;
   }

@@ -530,7 +530,7 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
     uint32_t cap_log2,
     uint32_t* __restrict__ flags, uint32_t s, uint32_t sort_pow2, uint32_t nb_log2,
     const uint32_t* __restrict__ row_of, uint64_t* __restrict__ out, uint32_t* __restrict__ lens,
-    uint32_t* __restrict__ status) {
+    uint32_t* __restrict__ status, const uint64_t* __restrict__ bad) {
   extern __shared__ uint64_t buf[];  // [sort_pow2] values, then [1 << nb_log2] u32 bucket counters
   uint32_t* cnt = reinterpret_cast<uint32_t*>(buf + sort_pow2);
   __shared__ uint32_t fill;
@@ -549,6 +549,11 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
     for (uint32_t i = tid; i < cap; i += T) tab[i] = kEmpty;
     if (tid == 0) flags[slot] = 0u;
   };
+  if (bad && *bad != ~0ull) {  // (uniform) a bad run table: K1 did nothing, the caller's rows stay untouched
+    __syncthreads();
+    clear_slot();
+    return;
+  }
   if (f & kFlagOverflow) {
     if (tid == 0) {
       status[slot] = kSketchRetrySmaller;
@@ -718,7 +723,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   uint32_t* flags, uint32_t s,
                                   uint32_t sort_pow2, const uint32_t* row_of, uint64_t* out,
                                   uint32_t* lens, uint32_t* status,
-                                  hipStream_t st) {
+                                  hipStream_t st, const uint64_t* bad) {
   if (n_slots == 0) return hipSuccess;
   // ~4 candidates per bucket
   uint32_t nb_log2 = 6;
@@ -734,7 +739,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
   const int threads = sort_pow2 >= 4096 ? kFinalizeMaxBlock : 256;
   hipLaunchKernelGGL(sketch_finalize_kernel, dim3(n_slots), dim3(threads), lds, st,
                      slot_list, slot_genome, tau, table, cap_log2, flags, s,
-                     sort_pow2, nb_log2, row_of, out, lens, status);
+                     sort_pow2, nb_log2, row_of, out, lens, status, bad);
   return hipGetLastError();
 }
 

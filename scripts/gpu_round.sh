@@ -33,6 +33,8 @@ for st in $STAGES; do
     tests)
       run gpu_tests 900 python3 -u -m pytest ${TESTS:-tests -m gpu} -v --timeout 300 --timeout-method thread
       rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
+    hostinfo)  # the host's CPUs as this process sees them (nproc, affinity, cgroup quota)
+      run hostinfo 60 python3 -u scripts/host_cpus.py || exit $? ;;
     smoke)
       run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)       bench bench_c3 600 --steps 20 --warmup 5 ;;
@@ -71,6 +73,9 @@ for st in $STAGES; do
         python3 -u bench.py --config c5 --steps 2 --warmup 1 --no-cpu-baseline || exit $? ;;
     pmc)  # PMC passes at HEAD (scripts/pmc_head.sh)
       run pmc 900 bash scripts/pmc_head.sh "$OUT/pmc" ${PMC_ARGS:-} || exit $? ;;
+    pmc_k2)  # K2 counters at C3 and C5 (scripts/k2_pmc.sh; summarised by scripts/k2_pmc_model.py)
+      run pmc_k2_c3 1000 bash scripts/k2_pmc.sh "$OUT/pmc_k2_c3" || exit $?
+      run pmc_k2_c5 1000 bash scripts/k2_pmc.sh "$OUT/pmc_k2_c5" --config c5 || exit $? ;;
     pmc_k1)  # K1 instruction counters at C3 and C5 (scripts/pmc.sh passes 1-2)
       PMC_SETS=2 run pmc_k1_c3 400 bash scripts/pmc.sh "$OUT/pmc_k1_c3" sketch_candidates -- \
         python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-files || exit $?

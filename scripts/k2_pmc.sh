@@ -1,17 +1,21 @@
 #!/bin/bash
-# PMC passes over one bench step (K1 and every K2 kernel: index scan/fill,
-# the radix sort, runs, pairs), one rocprofv3 run per counter set.
+# PMC passes over one bench step for every K2 kernel of the default
+# (bucketed) inverted index: index_scan, bucket_hist, bucket_base, index_fill,
+# the 16-bit onesweep sort, bucket_bounds, index_bucket, index_pairs and the
+# passing pairs' device sort (pair_keys, rocPRIM, pair_gather).  One
+# rocprofv3 run per counter set (MI355X_MICROARCH.md: FETCH_SIZE and
+# WRITE_SIZE each in a pass of their own).
 # usage: scripts/k2_pmc.sh <outdir> [bench args...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 out=$1; shift
 mkdir -p "$out"
-rx='sketch_candidates|index_|onesweep'
+rx='index_|bucket_|onesweep|pair_keys|pair_gather|sort|merge'
 sets=(
   "GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_LDS_LOAD_BANDWIDTH SQ_INSTS_VMEM_RD"
-  "GRBM_GUI_ACTIVE TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum"
-  "GRBM_GUI_ACTIVE TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"
   "GRBM_GUI_ACTIVE FETCH_SIZE"
+  "GRBM_GUI_ACTIVE WRITE_SIZE"
+  "GRBM_GUI_ACTIVE TCC_HIT_sum TCC_MISS_sum"
 )
 i=0
 for s in "${sets[@]}"; do

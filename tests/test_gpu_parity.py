@@ -458,6 +458,45 @@ def test_index_kernel_many_partners_and_long_runs(monkeypatch):
         assert paths["index"] == 0 and paths["index_abandoned"] >= 1 and paths["gate"] == paths["index_abandoned"]
 
 
+def _part_of(j, plog2):
+    # pairs_index.hip part_of: the top plog2 bits of j * 0x9E3779B1 (mod 2^32)
+    return ((j * 0x9E3779B1) & 0xFFFFFFFF) >> (32 - plog2) if plog2 else 0
+
+
+def test_index_kernel_later_partner_class_overflows(monkeypatch):
+    """Row 0's partners split into 2 classes where class 0 fits the LDS map
+    and class 1 (2,000 partners > the map's 1,536) does not: the row goes on
+    at classes 2 and 3 of 4 without counting class 0 again (it
+    restarted at class 0 and emitted those pairs twice)."""
+    rng = np.random.default_rng(41)
+    s = 1000
+    n = 4400
+    c1 = [j for j in range(1, n) if _part_of(j, 1) == 1][:2000]
+    c0 = [j for j in range(1, n) if _part_of(j, 1) == 0][:200]
+    assert len(c1) == 2000 and len(c0) == 200
+    partners = set(c0) | set(c1)
+    base = np.unique(rng.integers(1, 2**62, 4 * s, dtype=np.uint64))[:s]
+    sk = np.zeros((n, s), np.uint64)
+    lens = np.zeros(n, np.uint32)
+    sk[0] = base
+    lens[0] = s
+    for i in range(1, n):
+        own = rng.integers(2**62, 2**63, 40, dtype=np.uint64)
+        v = np.unique(np.concatenate([[base[i % s]], own]) if i in partners else own)
+        sk[i, :len(v)] = v
+        lens[i] = len(v)
+    monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
+    for thr in (0.001, 0.5):
+        o = oracle.pairs(sk, lens.astype(np.int32), np.float32(thr))
+        exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
+        assert sum(1 for p in exp if p[0] == 0) == len(partners)
+        with ga.Context(k=21, sketch_size=s) as ctx:
+            got = as_tuples(ctx.pairs(sk, lens, np.float32(thr)))
+            assert len({(p[0], p[1]) for p in got}) == len(got), "duplicate (i, j)"
+            assert got == exp, thr
+            assert ctx.pair_paths()["index"] == 1 and ctx.pair_paths()["index_abandoned"] == 0
+
+
 def test_many_runs_index_and_run_table_errors(gpu_ctx):
     """> 2^18 runs (the host run index runs in parallel chunks), ragged run
     lengths around one K1 segment (44 k-mers), genomes without runs between
@@ -502,9 +541,21 @@ def test_many_runs_index_and_run_table_errors(gpu_ctx):
     r4 = runs.copy()
     r4["genome"][-1] = n_genomes
     bad.append((r4, "non-decreasing genome"))
+    # a rejected table leaves the caller's rows and lengths as they were
+    # (the one-batch path's finalize used to write them first)
+    d_out.fill_(7)
+    d_lens.fill_(9)
     for r, msg in bad:
         with pytest.raises(ga.GalahGpuError, match=msg):
             gpu_ctx.sketch_device(d_words, r, n_genomes, d_out, d_lens)
+        torch.cuda.synchronize()
+        assert bool((d_out == 7).all()) and bool((d_lens == 9).all()), msg
+    # and the context still sketches correctly afterwards
+    gpu_ctx.sketch_device(d_words, runs, n_genomes, d_out, d_lens)
+    torch.cuda.synchronize()
+    sk2 = d_out.cpu().numpy().view(np.uint64)
+    assert (d_lens.cpu().numpy().view(np.uint32) == gl).all()
+    assert all((sk2[g][:gl[g]] == sk[g][:gl[g]]).all() for g in range(n_genomes))
 
 
 class HostPacked:
