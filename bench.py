@@ -51,9 +51,12 @@ N_SIMD = 256 * 4       # 256 CUs x 4 SIMDs
 # records a fingerprint of K1's machine code; bench.py recomputes it from the
 # library it loads and flags the peak as stale when K1 has changed since.
 ISSUE_MODEL = os.path.join(ROOT, "profiles", "r03_k1_issue_model.json")
-# K2's per-kernel PMC summary (VALU issue share, LDS-array utilisation, fabric
-# GB/s against the gfx950 peaks): scripts/k2_pmc.sh + scripts/k2_pmc_model.py
-K2_PMC = os.path.join(ROOT, "profiles", "r02_k2_pmc.json")
+# K2's per-kernel PMC summary (HBM bytes from FETCH_SIZE x 2 and WRITE_SIZE,
+# VALU issue share, LDS-array utilisation) of the bucketed inverted index:
+# scripts/k2_pmc.sh + scripts/k2_pmc_model.py
+K2_PMC = os.path.join(ROOT, "profiles", "r04_k2_pmc.json")
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+from host_cpus import host_cpu_info  # noqa: E402
 
 
 def parse():
@@ -140,12 +143,74 @@ def k2_pmc(config):
     c = m.get(config)
     if not c:
         return None
-    keep = ("ms", "bound", "bound_frac", "valu_frac_full", "lds_util", "lds_GBps", "hbm_read_GBps", "hbm_write_GBps",
-            "hbm_frac")
-    out = {k: {x: e[x] for x in keep if x in e} for k, e in c.items() if isinstance(e, dict) and k != "sketch_candidates"}
-    return {"source": "profiles/r02_k2_pmc.json (%s, one step)" % config, "kernels": out,
-            "peaks": "VALU: issue slots at 4.21 cycles per wave64 instruction per SIMD; LDS: array busy cycles per CU; "
-                     "HBM: 8 TB/s"}
+    keep = ("dispatches", "ms", "hbm_bytes", "hbm_GBps", "hbm_frac", "valu_frac_guide", "lds_util", "l2_hit",
+            "bound", "bound_frac")
+    ks = {k: {x: e[x] for x in keep if x in e} for k, e in c["kernels"].items()}
+    return {"source": "profiles/r04_k2_pmc.json (%s, one step; raw: %s)" % (config, c.get("source")), "kernels": ks,
+            "peaks": "VALU: 2 cycles per wave64 instruction per SIMD (MI355X_MICROARCH.md); LDS: array busy cycles "
+                     "per CU; HBM: 8 TB/s, bytes = FETCH_SIZE x 2 + WRITE_SIZE"}
+
+
+# K2 kernels timed under GG_KERNEL_PAIRS / GG_KERNEL_PAIRS_INDEX (the passing
+# pairs' device sort is not: it is output handling, ~0.1 ms at C3)
+K2_TIMED = ("index_scan", "bucket_hist", "bucket_base", "index_fill", "sort_histogram", "sort_pass",
+            "bucket_bounds", "index_bucket", "index_pairs")
+
+
+def k2_algorithmic_bytes(d_sk, d_len, n, s):
+    """Algorithmic HBM bytes of one K2 launch set (the bucketed inverted index
+    over n sketches of stride s) from the sketches themselves:
+    E = entries (sum of lengths), S = row slots (n x s: the fill keys every
+    slot, unused ones sort last), runs of g >= 2 equal hashes give the pairs
+    kernel g member reads per member (sum of g^2).  Member ids are 2 B when
+    n <= 65,536 (index_ents16), else 4 B."""
+    lens = d_len.to(torch.int64)
+    E = int(lens.sum())
+    S = n * s
+    mask = torch.arange(s, device=d_sk.device)[None, :] < lens[:, None]
+    _, cnt = torch.unique(d_sk[mask], return_counts=True)
+    cnt = cnt[cnt >= 2].to(torch.float64)
+    g2 = float((cnt * cnt).sum())
+    runs = int(cnt.numel())
+    del mask
+    m = 2 if n <= 65536 else 4
+    per = {
+        "index_scan": 4.0 * n,                        # row lengths
+        "bucket_hist": 8.0 * E,                       # each hash once
+        "index_fill": 8.0 * E + 6.0 * S,              # hash read; 16-bit bucket key + 32-bit entry written per slot
+        "sort_16bit_2pass": 2.0 * S + 2 * 12.0 * S,   # key histogram; 2 passes reading and writing 6 B per slot
+        "bucket_bounds": 2.0 * S,                     # sorted keys
+        "index_bucket": (4.0 + 8.0 + m + 8.0) * E,    # entry, its hash, member id and runinfo written
+        "index_pairs": 8.0 * E + m * g2,              # runinfo of every entry; g members of each of its runs
+    }
+    return {"bytes": sum(per.values()), "per_kernel": per, "entries": E, "slots": S, "shared_runs": runs,
+            "sum_g2": g2}
+
+
+def roofline_k2(model, kst_pr, config):
+    """K2's own roofline: algorithmic bytes of the index build + pairs kernel
+    per launch set over its HIP-event time, against 8 TB/s."""
+    sets = max(1, kst_pr["launches_sets"])
+    ms = kst_pr["ms"] / sets
+    ach = model["bytes"] / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+    out = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_launch_ms": round(ms, 4),
+           "algorithmic_bytes": round(model["bytes"]),
+           "algorithmic_bytes_per_kernel": {k: round(v) for k, v in model["per_kernel"].items()},
+           "entries": model["entries"], "slots": model["slots"], "shared_runs": model["shared_runs"],
+           "sum_g2": round(model["sum_g2"]),
+           "kernel": "K2: bucketed inverted index (index_scan, bucket_hist, bucket_base, index_fill, 16-bit onesweep "
+                     "sort, bucket_bounds, index_bucket) + index_pairs_kernel",
+           "note": "achieved = algorithmic bytes (per kernel above, DESIGN §4) / K2's HIP-event time per step (index "
+                   "build + pairs kernel, on the stream they run on); traffic = HBM bytes of the same kernels from "
+                   "the PMC pass (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md), per step"}
+    pmc = k2_pmc(config) if config else None
+    if pmc:
+        out["pmc"] = pmc
+        tr = sum(e.get("hbm_bytes", 0.0) for k, e in pmc["kernels"].items() if k in K2_TIMED)
+        out["traffic"] = round(tr) if tr else None
+        out["pmc_ms"] = round(sum(e.get("ms", 0.0) for k, e in pmc["kernels"].items() if k in K2_TIMED), 4)
+    return out
 
 
 def roofline(kst_sk, kst_pr, s, config_note, config=None):
@@ -185,15 +250,9 @@ def roofline(kst_sk, kst_pr, s, config_note, config=None):
         k1["frac_issue_model"] = k1_gkmer / model["peak_gkmer_per_s"]
         k1["peak"] = guide
         k1["frac"] = k1["frac_vs_guide_valu"]
-    k2 = {"kernel": "K2: index_pairs_kernel (+ fill, radix sort, runs) or pairs_gate_kernel", "unit": "Gpair/s",
+    k2 = {"kernel": "K2: index_pairs_kernel (+ the bucketed index build) or pairs_gate_kernel", "unit": "Gpair/s",
           "achieved": pairs / (pr_ms * 1e-3) / 1e9 if pr_ms > 0 else 0.0, "avg_ms": pr_ms, "work_per_launch": pairs,
-          "merge_priced_GBps": pairs * 16.0 * s / (pr_ms * 1e-3) / 1e9 if pr_ms > 0 else 0.0,
-          "note": "merge_priced_GBps = SURVEY 8(d)'s pricing (8 B x (|A|+|B|) per pair); neither K2 form merges: "
-                  "the inverted index counts shared hashes from one sort of all sketch entries, the gate kernel "
-                  "tests each column hash once against a row block's Bloom gate"}
-    pmc = k2_pmc(config) if config else None
-    if pmc:
-        k2["pmc"] = pmc
+          "note": "pairs evaluated per second; K2's HBM roofline is the line's roofline_k2"}
     dom = k1 if sk_ms * kst_sk["launches"] >= pr_ms * kst_pr["launches"] else k2
     roof = {"bound": dom.get("bound", "valu"), "achieved": round(dom["achieved"], 3),
             "peak": round(dom.get("peak", 0.0), 3), "unit": dom["unit"],
@@ -231,10 +290,10 @@ def cpu_model():
 
 
 def cpu_threads():
-    try:
-        return max(1, min(16, len(os.sched_getaffinity(0))))
-    except AttributeError:
-        return max(1, min(16, os.cpu_count() or 1))
+    """Every CPU this process can use (the CPU path on all host
+    cores): the affinity mask, capped by the cgroup CPU quota (on the GPU
+    box: 16 of the host's 256; scripts/host_cpus.py)."""
+    return host_cpu_info()["usable"]
 
 
 def cpu_baseline(sample_words, glen, sk_all, lens_all, k, s, min_ani, n_total, budget_s):
@@ -281,9 +340,17 @@ def cpu_baseline(sample_words, glen, sk_all, lens_all, k, s, min_ani, n_total, b
     npairs = n_total * (n_total - 1) / 2
     t_total = n_total * glen / sketch_bases_per_s + npairs / pair_rate
     t_total_all = n_total * glen / sketch_bases_per_s + npairs / pair_rate_all
+    hi = host_cpu_info()
+    # the same CPU path on every logical CPU of the host at the measured
+    # per-thread rates (sketching is parallel over genomes, the all-core pair
+    # loop over pairs): an upper bound for the CPU, as SMT threads are counted
+    # as full cores; used when the quota keeps this process below nproc
+    scale = (hi["nproc"] or T) / T
+    t_total_host = n_total * glen / (sketch_bases_per_s * scale) + npairs / (pair_rate_all * scale)
     return {
         "value": npairs / t_total, "unit": "genome-pairs/s", "cores": T, "kind": "port",
-        "cpu_model": cpu_model(),
+        "cpu_model": cpu_model(), "nproc": hi["nproc"], "affinity_cpus": hi["affinity"],
+        "cgroup_cpu_quota": hi["cgroup_cpu_quota"],
         "sample": ("oracle/ C restatement of finch on %d host threads (%s): sketched %d x %d bp synthetic genomes "
                    "of the workload (%.1f Mbases/s), serial pair loop (1 core, src/finch.rs:53) over %d genomes' "
                    "sketches (%.0f pairs/s), all-core pair loop over %d genomes (%.0f pairs/s); extrapolated to %d "
@@ -294,6 +361,11 @@ def cpu_baseline(sample_words, glen, sk_all, lens_all, k, s, min_ani, n_total, b
         "pair_rate_1core": pair_rate,
         "pair_rate_all_cores": pair_rate_all,
         "value_all_core_pairs": npairs / t_total_all,
+        "value_all_host_cpus_extrapolated": npairs / t_total_host,
+        "host_cpus_note": ("this process may use %d CPUs (affinity %s, cgroup quota %s of nproc %s); "
+                           "value_all_host_cpus_extrapolated scales the measured per-thread sketch and all-core "
+                           "pair rates linearly to all %s logical CPUs (an upper bound for the CPU path)"
+                           % (T, hi["affinity"], hi["cgroup_cpu_quota"], hi["nproc"], hi["nproc"])),
     }
 
 
@@ -448,7 +520,8 @@ def run_lib(a, world, rank):
         ms_step = elapsed_max / a.steps * 1e3
         npairs = N * (N - 1) // 2
         note = ("per-launch figures are device 0's (%d of %d genomes)" % (shards[0][2], N)) if M > 1 else ""
-        roof = roofline(kst["sketch"], kst["pairs"], s, note, a.config if M == 1 and N == {"c3": 10000, "c5": 10000}.get(a.config) else None)
+        roof = roofline(kst["sketch"], kst["pairs"], s, note)
+        pmc_config = a.config if M == 1 and N == {"c3": 10000, "c5": 10000}.get(a.config) else None
         downstream = None
         if M == 1 and found:
             t1 = time.perf_counter()
@@ -461,17 +534,23 @@ def run_lib(a, world, rank):
                           round(t_tr * 1e3, 3), "preclusters": int(len(offsets) - 1),
                           "largest": int(np.diff(offsets).max()) if N else 0}
         cpu = None
-        if world == 1 and M == 1 and not a.no_cpu_baseline and a.config in ("c2", "c3", "c4"):
+        roof_k2 = None
+        d_sk = d_len = None
+        if M == 1:  # the step's sketches, for K2's byte model and the CPU baseline's parity spot check
             d_words, runs, _ = shards[0]
             d_sk = torch.zeros((N, s), dtype=torch.int64, device="cuda:%d" % devs[0])
             d_len = torch.zeros(N, dtype=torch.int32, device="cuda:%d" % devs[0])
             ctx.sketch_device(d_words, runs, N, d_sk, d_len)
             torch.cuda.synchronize()
+            kp = dict(kst["pairs"])
+            kp["launches_sets"] = kst["pairs"]["launches"]
+            roof_k2 = roofline_k2(k2_algorithmic_bytes(d_sk, d_len, N, s), kp, pmc_config)
+        if world == 1 and M == 1 and not a.no_cpu_baseline and a.config in ("c2", "c3", "c4"):
             n_sample = cpu_threads()
             sample = d_words[: n_sample * a.genome_len // 16].cpu().numpy().view(np.uint32)
             cpu = cpu_baseline(sample, a.genome_len, d_sk.cpu().numpy().view(np.uint64),
                                d_len.cpu().numpy().view(np.uint32), a.k, s, min_ani, N, a.cpu_budget_s)
-            del d_sk, d_len
+        del d_sk, d_len
         files = None
         want_files = a.files if a.files is not None else (a.config == "c3")
         if world == 1 and M == 1 and want_files:
@@ -497,6 +576,7 @@ def run_lib(a, world, rank):
                                    "k2": round(kst["pairs"]["ms"] / a.steps, 3)},
             "pairs_found": found,
             "roofline": roof,
+            "roofline_k2": roof_k2,
             "cpu_baseline": cpu,
             "downstream": downstream,
             "files": files,

@@ -17,6 +17,7 @@ GalahGpuError otherwise.  The library must have been built in-tree
 an ImportError, never a silent substitute.
 """
 import ctypes
+import logging
 import os
 
 import numpy as np
@@ -49,7 +50,7 @@ EXPORTED_SYMBOLS = (
     "gg_partition_preclusters", "gg_precluster_pairs", "gg_synth_mixed_lengths", "gg_synth_mixed_device",
     "gg_sketch_cache_load", "gg_sketch_cache_store", "gg_sketch_files", "gg_precluster_files_cached",
     "gg_create_multi", "gg_device_count", "gg_device_ctx", "gg_set_host_threads", "gg_phase_times",
-    "gg_precluster_shards",
+    "gg_precluster_shards", "gg_fallbacks", "gg_peer_links", "gg_info_line",
 )
 
 GG_OK = 0
@@ -154,6 +155,10 @@ class _KStats(ctypes.Structure):
 
 _sig("gg_timing_enable", _i32, [_vp, _i32])
 _sig("gg_pair_paths", _i32, [_vp, _vp])
+_sig("gg_fallbacks", _i32, [_vp, _vp])
+_sig("gg_peer_links", _i32, [_vp, _vp])
+_sig("gg_info_line", _i32, [_vp, ctypes.c_char_p, ctypes.c_size_t])
+FALLBACKS = ("index_to_gate", "index_full_sort", "peer_staged", "sketch_retry")  # gg_fallbacks order
 _sig("gg_timing_read", _i32, [_vp, _i32, ctypes.POINTER(_KStats)])
 KERNEL_SKETCH, KERNEL_FINALIZE, KERNEL_PAIRS, KERNEL_PAIRS_INDEX = 0, 1, 2, 3
 
@@ -512,6 +517,33 @@ class Context:
             raise self._err(st)
         return dict(zip(("index", "index_abandoned", "gate", "other", "index_full_sort"), (int(x) for x in out)))
 
+    def fallbacks(self):
+        """Slow paths taken since the context was created (gg_fallbacks):
+        {"index_to_gate", "index_full_sort", "peer_staged", "sketch_retry"}."""
+        out = np.zeros(len(FALLBACKS), np.uint64)
+        st = _L.gg_fallbacks(self._c, _ptr(out))
+        if st != GG_OK:
+            raise self._err(st)
+        return dict(zip(FALLBACKS, (int(x) for x in out)))
+
+    def peer_links(self):
+        """[M, M] int array (gg_peer_links): 1 = member a copies from member b
+        device to device, 0 = staged through host memory."""
+        M = self.device_count
+        out = np.zeros(M * M, np.int32)
+        st = _L.gg_peer_links(self._c, _ptr(out))
+        if st != GG_OK:
+            raise self._err(st)
+        return out.reshape(M, M)
+
+    def info_line(self):
+        """The one-line summary galah would log at info! after distances()."""
+        buf = ctypes.create_string_buffer(1024)
+        st = _L.gg_info_line(self._c, buf, len(buf))
+        if st != GG_OK:
+            raise self._err(st)
+        return buf.value.decode()
+
     def timing_read(self, kernel):
         """-> dict(ms, launches, work) summed since timing_enable."""
         k = _KStats()
@@ -718,13 +750,17 @@ def distances(genome_fasta_paths, min_ani, num_kmers, kmer_length, sketch_cache_
     """src/finch.rs:26-75 -> SortedPairGenomeDistanceCache, computed on the GPU.
     sketch_cache_dir (not in galah) reuses sketches of
     unchanged genome files from earlier runs; the result is the same."""
+    log = logging.getLogger("galah")
     try:
         ctx = _context(int(kmer_length), int(num_kmers))
+        log.info("Sketching MinHash representations of each genome with finch ..")  # src/finch.rs:46
         pairs, ani = ctx.precluster_files(list(genome_fasta_paths), float(np.float32(min_ani)),
                                           cache_dir=sketch_cache_dir)
     except GalahGpuError as e:
         # src/finch.rs:50
         raise RuntimeError("Failed to sketch genomes with finch: %s" % e) from e
+    log.info("Finished sketching genomes")  # src/finch.rs:48
+    log.info(ctx.info_line())  # device count, phase times, fallbacks (gg_info_line)
     cache = SortedPairGenomeDistanceCache()
     for p, a in zip(pairs, ani):
         cache.insert((int(p["i"]), int(p["j"])), np.float32(a))

@@ -485,6 +485,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
           next.push_back(slot);
         }
         active.swap(next);
+        if (!active.empty()) ++c->fallbacks[GG_FALLBACK_SKETCH_RETRY];  // (a retry pass follows)
         continue;
       }
       // run table for the active genomes: on the first pass the batch's
@@ -575,6 +576,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
         next.push_back(slot);
       }
       active.swap(next);
+      if (!active.empty()) ++c->fallbacks[GG_FALLBACK_SKETCH_RETRY];
     }
   }
   c->clean_table = d_table;
@@ -1176,6 +1178,10 @@ void gg_destroy(gg_ctx* ctx) {
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   for (hipStream_t ps : ctx->peer_streams)
     if (ps) (void)hipStreamDestroy(ps);
+  for (hipEvent_t e : ctx->rep_start)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : ctx->rep_done)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->copy_done) (void)hipEventDestroy(ctx->copy_done);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
@@ -1306,6 +1312,54 @@ gg_status gg_pair_paths(const gg_ctx* ctx, uint64_t* paths) {
   for (int i = 0; i < GG_PATH_COUNT; ++i) paths[i] = ctx->pair_paths[i];
   for (const gg_ctx* m : ctx->devs)
     for (int i = 0; i < GG_PATH_COUNT; ++i) paths[i] += m->pair_paths[i];
+  return GG_OK;
+}
+
+gg_status gg_fallbacks(const gg_ctx* ctx, uint64_t* counts) {
+  if (!ctx || !counts) return fail(nullptr, GG_ERR_INVALID_ARG, "gg_fallbacks: null argument");
+  uint64_t paths[GG_PATH_COUNT];
+  gg_pair_paths(ctx, paths);
+  for (int i = 0; i < GG_FALLBACK_COUNT; ++i) counts[i] = ctx->fallbacks[i];
+  for (const gg_ctx* m : ctx->devs)
+    for (int i = 0; i < GG_FALLBACK_COUNT; ++i) counts[i] += m->fallbacks[i];
+  counts[GG_FALLBACK_INDEX_TO_GATE] = paths[GG_PATH_INDEX_ABANDONED];
+  counts[GG_FALLBACK_INDEX_FULL_SORT] = paths[GG_PATH_INDEX_FULL_SORT];
+  return GG_OK;
+}
+
+gg_status gg_peer_links(const gg_ctx* ctx, int* links) {
+  if (!ctx || !links) return fail(nullptr, GG_ERR_INVALID_ARG, "gg_peer_links: null argument");
+  const size_t M = ctx->devs.empty() ? 1 : ctx->devs.size();
+  for (size_t x = 0; x < M * M; ++x) links[x] = (M == 1 || x >= ctx->peer_direct.size()) ? 1 : ctx->peer_direct[x];
+  return GG_OK;
+}
+
+gg_status gg_info_line(const gg_ctx* ctx, char* buf, size_t cap) {
+  if (!ctx || !buf) return fail(nullptr, GG_ERR_INVALID_ARG, "gg_info_line: null argument");
+  if (cap == 0) return GG_OK;
+  std::string ords;
+  if (ctx->devs.empty()) {
+    ords = std::to_string(ctx->device);
+  } else {
+    for (size_t i = 0; i < ctx->devs.size(); ++i) ords += (i ? "," : "") + std::to_string(ctx->devs[i]->device);
+  }
+  uint64_t fb[GG_FALLBACK_COUNT];
+  gg_fallbacks(ctx, fb);
+  const size_t M = ctx->devs.empty() ? 1 : ctx->devs.size();
+  uint64_t staged_links = 0;
+  for (size_t x = 0; x < ctx->peer_direct.size(); ++x) staged_links += ctx->peer_direct[x] ? 0 : 1;
+  char line[512];
+  snprintf(line, sizeof line,
+           "galahgpu: %zu device(s) [%s]; sketch %.1f ms, replicate %.2f ms, pairs %.2f ms, merge %.2f ms; "
+           "fallbacks: index->gate %llu, index full sort %llu, host-staged peer copies %llu (links without peer "
+           "access %llu), sketch retry passes %llu",
+           M, ords.c_str(), ctx->phase_ms[GG_PHASE_SKETCH], ctx->phase_ms[GG_PHASE_REPLICATE],
+           ctx->phase_ms[GG_PHASE_PAIRS], ctx->phase_ms[GG_PHASE_MERGE], (unsigned long long)fb[0],
+           (unsigned long long)fb[1], (unsigned long long)fb[2], (unsigned long long)staged_links,
+           (unsigned long long)fb[3]);
+  const size_t n = std::min(cap - 1, strlen(line));
+  memcpy(buf, line, n);
+  buf[n] = 0;
   return GG_OK;
 }
 

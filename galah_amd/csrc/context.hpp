@@ -123,6 +123,15 @@ struct gg_ctx {
   // first use), so the copies from different peers run at once
   std::vector<hipStream_t> peer_streams;
   uint64_t pair_paths[GG_PATH_COUNT] = {};  // gg_pair_paths
+  // gg_fallbacks (the two index entries are read from pair_paths)
+  uint64_t fallbacks[GG_FALLBACK_COUNT] = {};
+  // multi-device context: [a * M + b] = 1 when member a reaches member b's
+  // memory directly (same device, or peer access enabled), gg_peer_links
+  std::vector<uint8_t> peer_direct;
+  // a member's replication events, per peer: copies started / done (device
+  // time of the copies, read after the pairs phase) and whether they are live
+  std::vector<hipEvent_t> rep_start, rep_done;
+  std::vector<char> rep_live;
   hipStream_t copy_stream = nullptr;  // run-table uploads beside work on `stream` (sketch_core)
   hipEvent_t copy_done = nullptr;
   // host threads for file ingest (<= 0: gg_pack_files' default)

@@ -105,17 +105,32 @@ void spans_of(std::vector<uint32_t>& rows, uint32_t owner, std::vector<RowSpan>&
 // Member mi copies every span it does not own from the owner's array.  The
 // copies from each owner go on a stream of their own: in one stream they
 // would run one after the other, and each peer is a different xGMI link (at
-// 8 devices, C3's 10 MB per peer, C4's 100 MB).
+// 8 devices, C3's 10 MB per peer, C4's 100 MB).  Nothing here waits on the
+// host: the member's compute stream waits on each peer stream's event, so
+// the host thread goes straight on to queue K2 (its table uploads and the
+// index build are queued behind the copies, not behind a host barrier), and
+// the copies' device time is read after the pairs phase (replicate_ms).
 gg_status replicate(gg_ctx* m, size_t mi, const std::vector<gg_ctx*>& ms, const std::vector<Rows>& rows,
-                    const std::vector<RowSpan>& spans) {
-  const size_t s = m->s;
-  if (m->peer_streams.size() < ms.size()) m->peer_streams.resize(ms.size(), nullptr);
-  std::vector<char> used(ms.size(), 0);
+                    const std::vector<RowSpan>& spans, const std::vector<uint8_t>& direct) {
+  const size_t s = m->s, M = ms.size();
+  if (m->peer_streams.size() < M) m->peer_streams.resize(M, nullptr);
+  if (m->rep_start.size() < M) {
+    m->rep_start.resize(M, nullptr);
+    m->rep_done.resize(M, nullptr);
+  }
+  m->rep_live.assign(M, 0);
   for (const RowSpan& sp : spans) {
     if (sp.owner == mi) continue;
     hipStream_t& ps = m->peer_streams[sp.owner];
     if (!ps) GG_HIP(m, hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
-    used[sp.owner] = 1;
+    if (!m->rep_live[sp.owner]) {
+      if (!m->rep_start[sp.owner]) {
+        GG_HIP(m, hipEventCreate(&m->rep_start[sp.owner]));
+        GG_HIP(m, hipEventCreate(&m->rep_done[sp.owner]));
+      }
+      GG_HIP(m, hipEventRecord(m->rep_start[sp.owner], ps));
+      m->rep_live[sp.owner] = 1;
+    }
     const gg_ctx* o = ms[sp.owner];
     uint64_t* dsk = rows[mi].sk + (size_t)sp.row0 * s;
     const uint64_t* ssk = rows[sp.owner].sk + (size_t)sp.row0 * s;
@@ -125,11 +140,27 @@ gg_status replicate(gg_ctx* m, size_t mi, const std::vector<gg_ctx*>& ms, const 
     // src == dst device is legal), so the one-GPU tests run the node's code
     GG_HIP(m, hipMemcpyPeerAsync(dsk, m->device, ssk, o->device, (size_t)sp.rows * s * sizeof(uint64_t), ps));
     GG_HIP(m, hipMemcpyPeerAsync(dl, m->device, sl, o->device, sp.rows * sizeof(uint32_t), ps));
+    if (!direct.empty() && !direct[mi * M + sp.owner]) m->fallbacks[GG_FALLBACK_PEER_STAGED] += 2;
   }
-  for (size_t o = 0; o < ms.size(); ++o)
-    if (used[o]) GG_HIP(m, hipStreamSynchronize(m->peer_streams[o]));
-  GG_HIP(m, hipStreamSynchronize(m->stream));
+  for (size_t o = 0; o < M; ++o)
+    if (m->rep_live[o]) {
+      GG_HIP(m, hipEventRecord(m->rep_done[o], m->peer_streams[o]));
+      GG_HIP(m, hipStreamWaitEvent(m->stream, m->rep_done[o], 0));
+    }
   return GG_OK;
+}
+
+// Device time of member m's last replication (first copy started to last
+// copy done, per peer stream; the largest), in ms.  After the member's
+// stream has been synchronised.
+double replicate_ms(gg_ctx* m) {
+  double worst = 0.0;
+  for (size_t o = 0; o < m->rep_live.size(); ++o) {
+    if (!m->rep_live[o]) continue;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, m->rep_start[o], m->rep_done[o]) == hipSuccess) worst = std::max(worst, (double)ms);
+  }
+  return worst;
 }
 
 bool pair_ij_less(const gg_pair& x, const gg_pair& y) { return x.i != y.i ? x.i < y.i : x.j < y.j; }
@@ -140,12 +171,6 @@ gg_status gather_pairs_merge(gg_ctx* c, const std::vector<gg_ctx*>& ms, const st
                              std::vector<gg_pair>& res) {
   const size_t M = ms.size();
   auto t0 = Clock::now();
-  if (M > 1) {
-    gg_status st = on_members(c, ms, [&](size_t i, gg_ctx* m) { return replicate(m, i, ms, rows, spans); });
-    if (st != GG_OK) return st;
-  }
-  c->phase_ms[GG_PHASE_REPLICATE] = ms_since(t0);
-  t0 = Clock::now();
   std::vector<std::vector<gg_pair>> part(M);
   // Which tiles each member evaluates.  When K2 takes the inverted index
   // (min_ani > 0: a pair needs a shared hash), a member's cost is mostly
@@ -163,10 +188,21 @@ gg_status gather_pairs_merge(gg_ctx* c, const std::vector<gg_ctx*>& ms, const st
     } else {
       gg_pair_partition(n, (uint32_t)M, (uint32_t)i, &tb, &te);
     }
+    // (replication queued first: K2's kernels wait for the copies on the device)
+    if (M > 1 && !spans.empty()) {
+      const gg_status r = replicate(m, i, ms, rows, spans, c->peer_direct);
+      if (r != GG_OK) return r;
+    }
     return pairs_range_to_host(m, rows[i].sk, rows[i].len, n, tb, te, min_ani, part[i], m->stream);
   });
   if (st != GG_OK) return st;
   c->phase_ms[GG_PHASE_PAIRS] = ms_since(t0);
+  // replicate: the copies' device time (they ran inside the pairs phase's
+  // wall time, ahead of each member's K2 kernels)
+  double rep = 0.0;
+  if (M > 1 && !spans.empty())
+    for (gg_ctx* m : ms) rep = std::max(rep, replicate_ms(m));
+  c->phase_ms[GG_PHASE_REPLICATE] = rep;
   t0 = Clock::now();
   // every member's part comes in (i, j) order (pairs_range_to_host: sorted
   // on the device, or few and sorted by the member's thread), then merged:
@@ -753,8 +789,10 @@ gg_ctx* gg_create_multi(int kmer_length, uint32_t sketch_size, uint64_t hash_see
   // direct xGMI peer access between every pair of members (a copy between
   // devices without it is staged through the host); the same loop runs for
   // repeated ordinals, where it is a no-op
-  for (int a : list)
-    for (int b : list) (void)enable_peer(a, b);
+  const size_t M = list.size();
+  c->peer_direct.assign(M * M, 0);
+  for (size_t a = 0; a < M; ++a)
+    for (size_t b = 0; b < M; ++b) c->peer_direct[a * M + b] = enable_peer(list[a], list[b]) ? 1 : 0;
   (void)hipSetDevice(list[0]);
   *status = GG_OK;
   return c;

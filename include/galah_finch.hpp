@@ -14,6 +14,8 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
+#include <functional>
 #include <map>
 #include <optional>
 #include <stdexcept>
@@ -85,6 +87,20 @@ inline int current_num_threads() {
   return n > 0 ? n : (int)std::max(1u, std::thread::hardware_concurrency());
 }
 
+// galah's info! log (env_logger, shown at the default level): the two lines
+// of src/finch.rs:46,48 plus one line from the library (gg_info_line: device
+// count, phase times, fallbacks).  The sink is replaceable (tests capture it);
+// the default writes to stderr as env_logger would.
+inline std::function<void(const std::string&)>& info_sink() {
+  static std::function<void(const std::string&)> sink = [](const std::string& line) {
+    std::fprintf(stderr, "[INFO] %s\n", line.c_str());
+  };
+  return sink;
+}
+inline void info(const std::string& line) {
+  if (info_sink()) info_sink()(line);
+}
+
 namespace detail {
 // sketch + all pairs + threshold on an existing context; takes ownership of ctx
 inline SortedPairGenomeDistanceCache distances_on(gg_ctx* ctx, const std::vector<std::string>& paths, float min_ani) {
@@ -96,12 +112,16 @@ inline SortedPairGenomeDistanceCache distances_on(gg_ctx* ctx, const std::vector
   gg_pair* pairs = nullptr;
   float* ani = nullptr;
   uint64_t n = 0;
+  info("Sketching MinHash representations of each genome with finch ..");  // src/finch.rs:46
   const gg_status st = gg_precluster_files(ctx, c_paths.data(), (uint32_t)c_paths.size(), min_ani, &pairs, &ani, &n);
   if (st != GG_OK) {
     std::string msg = gg_last_error(ctx);
     gg_destroy(ctx);
     throw std::runtime_error("Failed to sketch genomes with finch: " + msg);  // src/finch.rs:50
   }
+  info("Finished sketching genomes");  // src/finch.rs:48 (sketches and pairs come from one call here)
+  char line[1024];
+  if (gg_info_line(ctx, line, sizeof line) == GG_OK) info(line);
   SortedPairGenomeDistanceCache cache;
   for (uint64_t i = 0; i < n; ++i) cache.insert({pairs[i].i, pairs[i].j}, ani[i]);  // src/finch.rs:70
   gg_free(pairs);

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 4u
+#define GG_ABI_VERSION 5u
 
 typedef enum gg_status {
   GG_OK = 0,
@@ -346,6 +346,38 @@ enum {
   GG_PATH_COUNT = 5
 };
 gg_status gg_pair_paths(const gg_ctx* ctx, uint64_t* paths);
+
+/* ---- fallbacks, peer links and one log line ---------------------------- */
+/* None of these changes a result; each costs time, and galah would not see
+ * it otherwise.  Counts since the context was created, members summed:
+ *   GG_FALLBACK_INDEX_TO_GATE    K2 calls whose inverted index was abandoned
+ *                                for the gate kernel (gg_pair_paths[1])
+ *   GG_FALLBACK_INDEX_FULL_SORT  index calls rebuilt with the full 32-bit
+ *                                sort after a bucket overflowed (gg_pair_paths[4])
+ *   GG_FALLBACK_PEER_STAGED      sketch-row copies between two members on
+ *                                different devices WITHOUT direct peer access
+ *                                (the HIP runtime stages them through host
+ *                                memory; see gg_peer_links)
+ *   GG_FALLBACK_SKETCH_RETRY     K1 passes re-run for genomes whose first
+ *                                bottom-s threshold missed (exact either way) */
+enum {
+  GG_FALLBACK_INDEX_TO_GATE = 0,
+  GG_FALLBACK_INDEX_FULL_SORT = 1,
+  GG_FALLBACK_PEER_STAGED = 2,
+  GG_FALLBACK_SKETCH_RETRY = 3,
+  GG_FALLBACK_COUNT = 4
+};
+gg_status gg_fallbacks(const gg_ctx* ctx, uint64_t* counts /* [GG_FALLBACK_COUNT] */);
+/* links[a * M + b] (M = gg_device_count) for members a and b: 1 when member
+ * a's copies from member b go device to device (same device, or xGMI peer
+ * access enabled at gg_create_multi), 0 when they are staged through host
+ * memory.  A single-device context reports {1}. */
+gg_status gg_peer_links(const gg_ctx* ctx, int* links /* [M * M] */);
+/* One human-readable line for galah's info! log after distances(): device
+ * count and ordinals, the last fused call's phase times, and the fallback
+ * counts.  Writes at most cap bytes including the terminating NUL (the line
+ * is cut to fit).  Returns GG_ERR_INVALID_ARG for a null ctx or buf. */
+gg_status gg_info_line(const gg_ctx* ctx, char* buf, size_t cap);
 
 /* ---- benchmark support: synthetic clustered genomes on device ---------- */
 /* Genomes [first_genome, first_genome + n_genomes) of a synthetic set of

@@ -50,6 +50,11 @@ for st in $STAGES; do
     bench2r)  # the driver's launch shape on one GPU (two members of GPU 0)
       run bench_2rank 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
         --master-port 29511 bench.py --gpus 2 --devices 0,0 --steps 5 --warmup 2 --no-cpu-baseline || exit $? ;;
+    bench8r)  # the driver's 8-GPU launch shape on one GPU (eight members of GPU 0; ranks 1-7 join the barriers)
+      run bench_8rank 600 python3 -u -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29513 bench.py --gpus 8 --devices 0,0,0,0,0,0,0,0 --steps 10 --warmup 3 --no-cpu-baseline \
+        --no-files || exit $?
+      tail -n 1 "$OUT/bench_8rank.log" > "$OUT/bench_8rank.json" ;;
     bench_dist)  # one process per GPU layout (--mode dist) at world 1: the per-rank sketch + row-tile pairs path
       bench bench_dist 300 --mode dist --steps 20 --warmup 5 --no-cpu-baseline --no-files ;;
     bench_dist2)  # --mode dist at world 2 on one GPU: gloo all-gather through host memory (RCCL refuses two ranks on one GPU)

@@ -42,6 +42,13 @@ def host_cpu_info():
         pass
     info["cpu_model"] = model
     info["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
+    # CPUs this process can keep busy: the affinity mask, capped by the
+    # cgroup quota (the GPU box gives one GPU's job a 16-CPU quota of a
+    # 256-CPU host: threads beyond it are throttled, not added)
+    usable = info["affinity"] or 1
+    if quota is not None:
+        usable = max(1, min(usable, int(quota)))
+    info["usable"] = usable
     return info
 
 

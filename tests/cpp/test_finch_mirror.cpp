@@ -59,7 +59,16 @@ static void test_hello_world(const std::string& dir) {
   CHECK(galah::current_num_threads() == 2);
   galah::FinchPreclusterer p(0.9f, 1000, 21);
   CHECK(std::strcmp(p.method_name(), "finch") == 0);
+  std::vector<std::string> log;
+  galah::info_sink() = [&](const std::string& line) { log.push_back(line); };
   auto d1 = p.distances(paths);
+  // src/finch.rs:46,48 and the library's one line (device count, phases, fallbacks)
+  CHECK(log.size() == 3);
+  CHECK(log.size() == 3 && log[0] == "Sketching MinHash representations of each genome with finch ..");
+  CHECK(log.size() == 3 && log[1] == "Finished sketching genomes");
+  CHECK(log.size() == 3 && log[2].rfind("galahgpu: ", 0) == 0 && log[2].find("device(s)") != std::string::npos &&
+        log[2].find("fallbacks: index->gate 0, index full sort 0, host-staged peer copies 0") != std::string::npos);
+  galah::info_sink() = nullptr;
   galah::SortedPairGenomeDistanceCache e1;
   e1.insert({0, 1}, 0.9808188f);
   CHECK(d1 == e1);

@@ -44,10 +44,16 @@ def test_golden_pairs_exact(gpu_ctx, golden, min_ani):
     assert as_tuples(p) == expected_pairs_from_table(golden, min_ani)
 
 
-def test_finch_rs_hello_world(golden):
+def test_finch_rs_hello_world(golden, caplog):
     # src/finch.rs:85-107 through the reference-interface mirror
     paths = [golden["paths"][golden["names"].index(n)] for n in ("set1/1mbp.fna", "set1/500kb.fna")]
-    d1 = ga.distances(paths, 0.9, 1000, 21)
+    with caplog.at_level("INFO", logger="galah"):
+        d1 = ga.distances(paths, 0.9, 1000, 21)
+    # src/finch.rs:46,48 and the library's one line (devices, phases, fallbacks)
+    msgs = [r.getMessage() for r in caplog.records if r.name == "galah"]
+    assert msgs[:2] == ["Sketching MinHash representations of each genome with finch ..",
+                        "Finished sketching genomes"]
+    assert msgs[2].startswith("galahgpu: ") and "index->gate 0, index full sort 0" in msgs[2]
     e1 = ga.SortedPairGenomeDistanceCache()
     e1.insert((0, 1), np.float32(0.9808188))
     assert d1 == e1
@@ -436,6 +442,8 @@ def test_index_kernel_many_partners_and_long_runs(monkeypatch):
                 if split == "0":  # 2,999 partners never fit one map: abandoned for the gate kernel
                     assert ctx.pair_paths() == {"index": 0, "index_abandoned": 1, "gate": 1, "other": 0,
                                                 "index_full_sort": 0}
+                    assert ctx.fallbacks()["index_to_gate"] == 1
+                    assert "index->gate 1," in ctx.info_line()
         monkeypatch.delenv("GALAHGPU_INDEX_MAX_SPLIT")
     # 5,000 sketches that all hold one hash: a run of 5,000 > the run limit
     n = 5000
@@ -680,6 +688,9 @@ def test_index_bucket_overflow_falls_back_to_full_sort(monkeypatch):
     with ga.Context(k=21, sketch_size=s) as ctx:
         assert as_tuples(ctx.pairs(sk, lens, np.float32(0.87))) == exp
         assert ctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0, "index_full_sort": 1}
+        # the slow path is reported at galah's log level (gg_fallbacks, gg_info_line)
+        assert ctx.fallbacks()["index_full_sort"] == 1 and ctx.fallbacks()["index_to_gate"] == 0
+        assert "index full sort 1" in ctx.info_line()
 
 
 def test_device_run_table_same_as_host(gpu_ctx):

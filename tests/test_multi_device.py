@@ -41,6 +41,13 @@ def test_precluster_files_same_for_1_2_3_devices(golden):
                 assert a == np.float32(oracle.ani(int(r["common"]), int(r["total"])))
             ph = ctx.phase_times()
             assert ph["sketch"] > 0 and ph["pairs"] > 0
+            # every member pair reaches the other directly (one device here;
+            # on a node: xGMI peer access), so no copy is staged through host
+            assert (ctx.peer_links() == 1).all() and ctx.peer_links().shape == (len(devs), len(devs))
+            assert ctx.fallbacks()["peer_staged"] == 0
+            line = ctx.info_line()
+            assert line.startswith("galahgpu: %d device(s) [%s]" % (len(devs), ",".join(map(str, devs)))), line
+            assert "host-staged peer copies 0 (links without peer access 0)" in line
 
 
 def test_sketch_and_pairs_host_buffers_multi(golden):
