@@ -315,10 +315,11 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   const int grid = std::max(1, n_cu) * wg_per_cu;
 
   uint64_t* d_table;
-  uint32_t *d_flags, *d_status, *d_slot_list, *d_slot_genome;
+  uint32_t *d_flags, *d_count, *d_status, *d_slot_list, *d_slot_genome;
   uint64_t* d_tau;
   GG_HIP(c, scratch_t(c, "table", (size_t)max_batch * cap, &d_table));
   GG_HIP(c, scratch_t(c, "flags", max_batch, &d_flags));
+  GG_HIP(c, scratch_t(c, "cand_count", max_batch, &d_count));
   GG_HIP(c, scratch_t(c, "slot_list", max_batch, &d_slot_list));
   GG_HIP(c, scratch_t(c, "slot_genome", max_batch, &d_slot_genome));
   // what the host reads back, contiguous on the device and in pinned host
@@ -333,13 +334,15 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   d_status = reinterpret_cast<uint32_t*>(d_rb + rb_ix + max_batch);
   const uint32_t* h_status = reinterpret_cast<const uint32_t*>(h_rb + rb_ix + max_batch);
 
-  // batch 0's candidate sets are cleared on `stream` while the run table
-  // uploads on the copy stream (C5: 2.6 GB of sets, 58 MB of runs)
+  // every slot starts a call in append mode with an empty list (count 0,
+  // flags 0); the finalize leaves its slots so, so only new buffers are
+  // cleared (the table itself needs no clearing: a list is [0, count), and a
+  // slot's set is cleared by the finalize that switches it to set mode)
   const uint32_t nb0 = std::min(n_genomes, max_batch);
   const size_t batch_bytes = (size_t)nb0 * cap * sizeof(uint64_t);
   if (c->clean_table != d_table || c->clean_table_bytes < batch_bytes) {
-    GG_HIP(c, hipMemsetAsync(d_table, 0xFF, batch_bytes, st));
     GG_HIP(c, hipMemsetAsync(d_flags, 0, nb0 * sizeof(uint32_t), st));
+    GG_HIP(c, hipMemsetAsync(d_count, 0, nb0 * sizeof(uint32_t), st));
   }
   // (dirty until every batch's finalize has run; an error return leaves it so)
   c->clean_table = nullptr;
@@ -421,12 +424,13 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
     a.table = d_table;
     a.cap_log2 = geom.cap_log2;
     a.flags = d_flags;
+    a.count = d_count;
     a.seed = c->seed;
     if (c->timing) k1_timed = c->timed.size();
     GG_HIP(c, timed_launch(c, GG_KERNEL_SKETCH, 0, st, [&] { return launch_sketch_candidates(c->k, a, grid, st); }));
     GG_HIP(c, timed_launch(c, GG_KERNEL_FINALIZE, n_genomes, st, [&] {
       return launch_sketch_finalize(d_slot_list, n_genomes, d_slot_genome, d_tau, d_table, geom.cap_log2, d_flags,
-                                    c->s, geom.sort_pow2, d_row_of, d_out, d_lens, d_status, st, d_ix);
+                                    c->s, geom.sort_pow2, d_row_of, d_out, d_lens, d_status, d_count, st, d_ix);
     }));
   }
   // the index, and in one batch the first pass's taus and status (one batch:
@@ -479,6 +483,10 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
         std::vector<uint32_t> next;
         for (uint32_t slot : active) {
           if (status0[slot] == kSketchOk) continue;
+          if (status0[slot] == kSketchRetrySet) {  // the same tau, in set mode
+            next.push_back(slot);
+            continue;
+          }
           if (!advance_tau(ts[slot], status0[slot]))
             return fail(c, GG_ERR_INTERNAL, "bottom-s threshold search failed");
           h_tau[slot] = ts[slot].tau;
@@ -552,6 +560,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       a.table = d_table;
       a.cap_log2 = geom.cap_log2;
       a.flags = d_flags;
+      a.count = d_count;
       a.seed = c->seed;
       const int g = (int)std::min<uint64_t>((uint64_t)grid, std::max<uint64_t>(1, (sacc + 255) / 256));
       GG_HIP(c, timed_launch(c, GG_KERNEL_SKETCH, kacc, st,
@@ -559,7 +568,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       GG_HIP(c, timed_launch(c, GG_KERNEL_FINALIZE, active.size(), st, [&] {
         return launch_sketch_finalize(d_slot_list, (uint32_t)active.size(), d_slot_genome, d_tau,
                                       d_table, geom.cap_log2, d_flags, c->s,
-                                      geom.sort_pow2, d_row_of, d_out, d_lens, d_status, st);
+                                      geom.sort_pow2, d_row_of, d_out, d_lens, d_status, d_count, st);
       }));
       hp.mark("enqueue K1 + finalize");
       GG_HIP(c, hipMemcpyAsync(const_cast<uint32_t*>(h_status), d_status, nb * sizeof(uint32_t),
@@ -570,6 +579,10 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       std::vector<uint32_t> next;
       for (uint32_t slot : active) {
         if (status[slot] == kSketchOk) continue;
+        if (status[slot] == kSketchRetrySet) {  // the same tau, in set mode
+          next.push_back(slot);
+          continue;
+        }
         if (!advance_tau(ts[slot], status[slot]))
           return fail(c, GG_ERR_INTERNAL, "bottom-s threshold search failed");
         h_tau[slot] = ts[slot].tau;

@@ -20,11 +20,15 @@ enum SketchStatus : uint32_t {
   kSketchOk = 0,
   kSketchRetryLarger = 1,   // fewer than s distinct hashes <= tau, tau < 2^64-1
   kSketchRetrySmaller = 2,  // candidate set overflowed its limit
+  kSketchRetrySet = 3,      // the candidate list (append mode) held more than the finalize sorts
+                            // (duplicates count there): the same tau again in set mode
 };
 
 // flags[] bits
 constexpr uint32_t kFlagOverflow = 1u;
 constexpr uint32_t kFlagSawMax = 2u;
+constexpr uint32_t kFlagSetMode = 4u;  // the slot collects its candidates in a hash set (K1 inserts
+                                       // with atomicCAS) instead of appending them to a list
 
 // Largest number of candidates the finalize kernel sorts in LDS.
 constexpr uint32_t kSortCap = 16384;
@@ -48,6 +52,7 @@ struct SketchLaunch {
   uint64_t* table;             // [slots << cap_log2]
   uint32_t cap_log2;
   uint32_t* flags;             // [slots]
+  uint32_t* count;             // [slots] candidates appended (append mode; 0 between passes)
   uint64_t seed;
   // (first pass queued before the host has seen the run index) the segment
   // count on the device, and the run-table check: K1 does nothing if set
@@ -101,7 +106,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   uint32_t cap_log2,
                                   uint32_t* flags, uint32_t s,
                                   uint32_t sort_pow2, const uint32_t* row_of, uint64_t* out,
-                                  uint32_t* lens, uint32_t* status,
+                                  uint32_t* lens, uint32_t* status, uint32_t* count,
                                   hipStream_t st, const uint64_t* bad = nullptr);
 
 // pairs.hip

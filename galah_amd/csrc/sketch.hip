@@ -292,6 +292,45 @@ __device__ __forceinline__ void insert_candidate(uint64_t* __restrict__ tab,
   atomicOr(flags, kFlagOverflow);  // table full
 }
 
+// The candidates hv <= tau of the active lanes with `pass`, each of genome
+// slot sl.  Append mode (a slot's first pass): the slot's candidates are a
+// list [0, count) of its table region, one position per candidate from ONE
+// atomicAdd per group of lanes holding the same slot (a wave's drain is
+// almost always one genome: one atomic per ~32 candidates, and stores into
+// consecutive positions), duplicates included (the finalize collapses them).
+// Set mode (kFlagSetMode, after a list outgrew the finalize's sort): the
+// open-addressing set of insert_candidate, one atomicCAS per probe.  Both
+// are exact: every distinct hash <= tau is kept.  At s = 10000 (C5) the
+// candidates were ~1.3e8 memory-side atomicCAS per step in set mode.
+__device__ __forceinline__ void emit_candidates(bool pass, uint64_t hv, uint32_t sl, uint64_t* __restrict__ table,
+                                                uint32_t cap_log2, uint32_t* __restrict__ flags,
+                                                uint32_t* __restrict__ count) {
+  bool app = false;
+  if (pass) {
+    if ((flags[sl] & kFlagSetMode) || hv == kEmpty)
+      insert_candidate(table + ((uint64_t)sl << cap_log2), (1u << cap_log2) - 1u, flags + sl, hv);
+    else
+      app = true;
+  }
+  uint64_t pending = __ballot(app);
+  const uint32_t lane = __lane_id();
+  while (pending) {  // (uniform: a ballot of the active lanes)
+    const uint32_t lead = (uint32_t)__ffsll((unsigned long long)pending) - 1u;
+    const uint32_t lsl = __shfl(sl, lead);
+    const uint64_t grp = __ballot(app && sl == lsl);
+    uint32_t base = 0;
+    if (lane == lead) base = atomicAdd(&count[lsl], (uint32_t)__popcll(grp));
+    base = __shfl(base, lead);
+    if (app && sl == lsl) {
+      const uint32_t pos = base + (uint32_t)__popcll(grp & ((1ull << lane) - 1ull));
+      if (pos < (1u << cap_log2)) table[((uint64_t)sl << cap_log2) + pos] = hv;
+      else atomicOr(flags + sl, kFlagOverflow);  // (the finalize re-runs the slot in set mode)
+      app = false;
+    }
+    pending &= ~grp;
+  }
+}
+
 // Per-wave LDS queue of exact candidates (hash, genome slot).  Candidates
 // are rare (0.05% of k-mers at s = 1000, 0.4% at s = 10000) and arise in
 // scattered lanes; inserting each where it arises runs the atomicCAS probe
@@ -317,15 +356,26 @@ __device__ __forceinline__ uint64_t exact_hash(uint64_t f1, uint64_t f2) {
 // finaliser states; the drain finishes the hash and inserts it if <= tau.
 __device__ __forceinline__ void queue_push_mid(CandQueue& q, uint64_t f1, uint64_t f2, uint32_t slot,
                                                const uint64_t* __restrict__ tau, uint64_t* __restrict__ table,
-                                               uint32_t cap_log2, uint32_t* __restrict__ flags) {
+                                               uint32_t cap_log2, uint32_t* __restrict__ flags,
+                                               uint32_t* __restrict__ count) {
   const uint32_t pos = atomicAdd(&q.tail, 1u);
-  if (pos - __atomic_load_n(&q.head, __ATOMIC_RELAXED) < kQueue) {
+  const bool queued = pos - __atomic_load_n(&q.head, __ATOMIC_RELAXED) < kQueue;
+  if (queued) {
     q.f1[pos & (kQueue - 1)] = f1;
     q.f2[pos & (kQueue - 1)] = f2;
     q.slot[pos & (kQueue - 1)] = slot;
-  } else {  // ring full: finish and insert now
+  }
+  if (!queued) {  // ring full (rare): finish and emit this one now, on its own
     const uint64_t hv = exact_hash(f1, f2);
-    if (hv <= tau[slot]) insert_candidate(table + ((uint64_t)slot << cap_log2), (1u << cap_log2) - 1u, flags + slot, hv);
+    if (hv <= tau[slot]) {
+      if ((flags[slot] & kFlagSetMode) || hv == kEmpty) {
+        insert_candidate(table + ((uint64_t)slot << cap_log2), (1u << cap_log2) - 1u, flags + slot, hv);
+      } else {
+        const uint32_t at = atomicAdd(&count[slot], 1u);
+        if (at < (1u << cap_log2)) table[((uint64_t)slot << cap_log2) + at] = hv;
+        else atomicOr(flags + slot, kFlagOverflow);
+      }
+    }
   }
 }
 
@@ -334,19 +384,19 @@ __device__ __forceinline__ void queue_push_mid(CandQueue& q, uint64_t f1, uint64
 // their pushes.
 __device__ __forceinline__ void queue_drain(CandQueue& q, const uint64_t* __restrict__ tau,
                                             uint64_t* __restrict__ table, uint32_t cap_log2,
-                                            uint32_t* __restrict__ flags, uint32_t min_pending) {
+                                            uint32_t* __restrict__ flags, uint32_t* __restrict__ count,
+                                            uint32_t min_pending) {
   const uint32_t head = __atomic_load_n(&q.head, __ATOMIC_RELAXED);
   const uint32_t tail = __atomic_load_n(&q.tail, __ATOMIC_RELAXED);
   if (tail - head < min_pending || tail == head) return;
   const uint32_t end = tail - head < kQueue ? tail : head + kQueue;
-  const uint32_t cap_mask = (1u << cap_log2) - 1u;
   for (;;) {
     const uint32_t e = atomicAdd(&q.claim, 1u);
     if (e >= end) break;
     const uint32_t x = e & (kQueue - 1);
     const uint32_t sl = q.slot[x];
     const uint64_t hv = exact_hash(q.f1[x], q.f2[x]);
-    if (hv <= tau[sl]) insert_candidate(table + ((uint64_t)sl << cap_log2), cap_mask, flags + sl, hv);
+    emit_candidates(hv <= tau[sl], hv, sl, table, cap_log2, flags, count);
   }
   // every active lane is past its last claim here (lockstep): reopen the ring
   __atomic_store_n(&q.head, tail, __ATOMIC_RELAXED);
@@ -503,25 +553,33 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
           if (hs[j] <= thr && (uint32_t)(g * kGroup + j) < cnt)
-            queue_push_mid(q, f1[j], f2[j], slot, a.tau, a.table, a.cap_log2, a.flags);
+            queue_push_mid(q, f1[j], f2[j], slot, a.tau, a.table, a.cap_log2, a.flags, a.count);
         }
       }
     }
-    queue_drain(q, a.tau, a.table, a.cap_log2, a.flags, kQueueDrain);
+    queue_drain(q, a.tau, a.table, a.cap_log2, a.flags, a.count, kQueueDrain);
   }
-  queue_drain(q, a.tau, a.table, a.cap_log2, a.flags, 1);  // every lane of the wave is back
+  queue_drain(q, a.tau, a.table, a.cap_log2, a.flags, a.count, 1);  // every lane of the wave is back
 }
 
-// One workgroup per genome slot: gather the set into LDS, sort it, keep the
-// first s.  Writes status[] for the host retry loop.  The candidates are
-// distinct values spread uniformly over [0, tau], so they are sorted by
-// buckets of the top bits below tau (a counting sort: LDS histogram, scan,
-// scatter into the genome's own candidate table in HBM, which the next pass
-// re-initialises anyway, and back into LDS in bucket order), then every
-// value's place in its bucket (~4 values) is its rank among them: one thread
-// per value, a few LDS reads and compares (a register sorting network per
-// bucket ran 120 compare-exchanges whatever the bucket held, and the lanes
-// of a wave wait for the largest bucket among them).  Any block size up to
+// One workgroup per genome slot: gather the slot's candidates into LDS,
+// sort them, keep the first s distinct.  Writes status[] for the host retry
+// loop.  The candidates are values spread uniformly over [0, tau], so they
+// are sorted by buckets of the top bits below tau (a counting sort: LDS
+// histogram, scan, scatter into the genome's own table region in HBM, and
+// back into LDS in bucket order), then every value's place is the number of
+// distinct values below it: the distinct values of the buckets before its
+// own (a scan of per-bucket distinct counts) plus those below it in its
+// bucket (~4 values: a few LDS reads and compares).  A set-mode slot holds
+// distinct values; an append-mode list may repeat one (a k-mer that occurs
+// twice): only the first copy of a value in its bucket counts.
+//   append mode: the list is [0, count[slot]) of the table region; nothing
+//     to clear afterwards but the count; a list longer than the sort (or
+//     past the region) re-runs the slot at the same tau in set mode
+//     (kSketchRetrySet), its region cleared here for the set
+//   set mode: the set is the whole region (EMPTY = free), cleared afterwards
+// (C5: the list is ~1.3 s entries where the set was 2 x 16384 slots, read
+// and cleared: 2.6 GB each way per step.)  Any block size up to
 // kFinalizeMaxBlock.
 constexpr int kFinalizeMaxBlock = 1024;
 __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
@@ -530,7 +588,7 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
     uint32_t cap_log2,
     uint32_t* __restrict__ flags, uint32_t s, uint32_t sort_pow2, uint32_t nb_log2,
     const uint32_t* __restrict__ row_of, uint64_t* __restrict__ out, uint32_t* __restrict__ lens,
-    uint32_t* __restrict__ status, const uint64_t* __restrict__ bad) {
+    uint32_t* __restrict__ status, uint32_t* __restrict__ count, const uint64_t* __restrict__ bad) {
   extern __shared__ uint64_t buf[];  // [sort_pow2] values, then [1 << nb_log2] u32 bucket counters
   uint32_t* cnt = reinterpret_cast<uint32_t*>(buf + sort_pow2);
   __shared__ uint32_t fill;
@@ -540,97 +598,128 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
   // streamed file list land on their global rows)
   const uint32_t g = row_of ? row_of[slot_genome[slot]] : slot_genome[slot];
   const uint32_t f = flags[slot];
+  const bool setm = (f & kFlagSetMode) != 0;
+  const uint32_t listed = count[slot];
   const uint32_t T = blockDim.x, tid = threadIdx.x, lane = tid & 63;
   uint64_t* tab = table + ((uint64_t)slot << cap_log2);
   const uint32_t cap = 1u << cap_log2;
-  // every path leaves the slot's set empty and its flags clear for the next
-  // K1 launch (the host clears the sets only before their first use)
-  auto clear_slot = [&]() {
+  __syncthreads();  // (every thread has read flags[slot] and count[slot])
+  auto clear_set = [&]() {
     for (uint32_t i = tid; i < cap; i += T) tab[i] = kEmpty;
-    if (tid == 0) flags[slot] = 0u;
+  };
+  // every path leaves the slot ready for the next K1 pass: count 0, flags 0
+  // or kFlagSetMode (set mode next: the set cleared)
+  auto finish = [&](uint32_t st, bool set_next) {
+    if (set_next) clear_set();
+    if (tid == 0) {
+      flags[slot] = set_next ? kFlagSetMode : 0u;
+      count[slot] = 0u;
+      if (st != ~0u) {
+        status[slot] = st;
+        if (st != kSketchOk) lens[g] = 0;
+      }
+    }
   };
   if (bad && *bad != ~0ull) {  // (uniform) a bad run table: K1 did nothing, the caller's rows stay untouched
-    __syncthreads();
-    clear_slot();
+    finish(~0u, setm);
     return;
   }
-  if (f & kFlagOverflow) {
-    if (tid == 0) {
-      status[slot] = kSketchRetrySmaller;
-      lens[g] = 0;
-    }
-    __syncthreads();  // (every thread has read flags[slot])
-    clear_slot();
+  if (f & kFlagOverflow) {  // set: more distinct candidates than slots; list: past its region
+    finish(setm ? kSketchRetrySmaller : kSketchRetrySet, true);
     return;
   }
   const uint32_t NB = 1u << nb_log2;
-  if (tid == 0) fill = 0;
-  for (uint32_t i = tid; i < NB; i += T) cnt[i] = 0;
-  __syncthreads();
-  // gather: each thread 8 consecutive slots per step, all loads in flight
-  // at once (one workgroup per CU at s = 10000: with one load per thread per
-  // step the gather waited on HBM latency step after step), a wave prefix
-  // sum of the values found and one LDS atomic per wave
-  constexpr uint32_t kGatherV = 8;
-  const uint32_t steps = (cap + T * kGatherV - 1) / (T * kGatherV);
-  for (uint32_t it = 0; it < steps; ++it) {
-    const uint32_t i0 = (it * T + tid) * kGatherV;
-    uint64_t v[kGatherV];
+  uint32_t n;
+  if (!setm) {  // the list, coalesced
+    n = listed;
+    if (n > sort_pow2) {
+      finish(kSketchRetrySet, true);
+      return;
+    }
+    // 8 values per thread per step, all loads in flight at once (one load
+    // after another waited on HBM latency each: C5 finalize 1.8 -> 3.2 ms)
+    constexpr uint32_t kListV = 8;
+    for (uint32_t i0 = tid * kListV; i0 < n; i0 += T * kListV) {
+      uint64_t v[kListV];
 #pragma unroll
-    for (uint32_t j = 0; j < kGatherV; j += 2) {
-      if (i0 + j < cap) {
-        const ulonglong2 p = *(const ulonglong2*)(tab + i0 + j);
-        v[j] = p.x;
-        v[j + 1] = p.y;
-      } else {
-        v[j] = v[j + 1] = kEmpty;
+      for (uint32_t j = 0; j < kListV; j += 2) {
+        if (i0 + j + 1 < n) {
+          const ulonglong2 p = *(const ulonglong2*)(tab + i0 + j);
+          v[j] = p.x;
+          v[j + 1] = p.y;
+        } else if (i0 + j < n) {
+          v[j] = tab[i0 + j];
+        }
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kListV; ++j)
+        if (i0 + j < n) buf[i0 + j] = v[j];
+    }
+    for (uint32_t i = tid; i < NB; i += T) cnt[i] = 0;
+  } else {
+    if (tid == 0) fill = 0;
+    for (uint32_t i = tid; i < NB; i += T) cnt[i] = 0;
+    __syncthreads();
+    // gather: each thread 8 consecutive slots per step, all loads in flight
+    // at once (one workgroup per CU at s = 10000: with one load per thread per
+    // step the gather waited on HBM latency step after step), a wave prefix
+    // sum of the values found and one LDS atomic per wave
+    constexpr uint32_t kGatherV = 8;
+    const uint32_t steps = (cap + T * kGatherV - 1) / (T * kGatherV);
+    for (uint32_t it = 0; it < steps; ++it) {
+      const uint32_t i0 = (it * T + tid) * kGatherV;
+      uint64_t v[kGatherV];
+#pragma unroll
+      for (uint32_t j = 0; j < kGatherV; j += 2) {
+        if (i0 + j < cap) {
+          const ulonglong2 p = *(const ulonglong2*)(tab + i0 + j);
+          v[j] = p.x;
+          v[j + 1] = p.y;
+        } else {
+          v[j] = v[j + 1] = kEmpty;
+        }
+      }
+      uint32_t c = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < kGatherV; ++j) c += v[j] != kEmpty ? 1u : 0u;
+      uint32_t inc = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= (uint32_t)o) inc += y;
+      }
+      uint32_t base = 0;
+      if (lane == 63 && inc) base = atomicAdd(&fill, inc);
+      uint32_t at = __shfl(base, 63) + inc - c;
+#pragma unroll
+      for (uint32_t j = 0; j < kGatherV; ++j) {
+        if (v[j] != kEmpty) {
+          if (at < sort_pow2) buf[at] = v[j];
+          ++at;
+        }
       }
     }
-    uint32_t c = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < kGatherV; ++j) c += v[j] != kEmpty ? 1u : 0u;
-    uint32_t inc = c;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o);
-      if (lane >= (uint32_t)o) inc += y;
-    }
-    uint32_t base = 0;
-    if (lane == 63 && inc) base = atomicAdd(&fill, inc);
-    uint32_t at = __shfl(base, 63) + inc - c;
-#pragma unroll
-    for (uint32_t j = 0; j < kGatherV; ++j) {
-      if (v[j] != kEmpty) {
-        if (at < sort_pow2) buf[at] = v[j];
-        ++at;
-      }
+    __syncthreads();
+    n = fill;  // distinct candidates <= tau
+    if (n > sort_pow2) {  // cannot sort in LDS
+      finish(kSketchRetrySmaller, true);
+      return;
     }
   }
   __syncthreads();
-  const uint32_t n = fill;  // distinct candidates <= tau
   const uint64_t t = tau[slot];
-  uint32_t st = kSketchOk;
-  if (n > sort_pow2) st = kSketchRetrySmaller;  // cannot sort in LDS
-  else if (n < s && t != kEmpty) st = kSketchRetryLarger;
-  if (st != kSketchOk) {
-    if (tid == 0) {
-      status[slot] = st;
-      lens[g] = 0;
-    }
-    clear_slot();  // (the gather's reads are done: barrier above)
-    return;
-  }
   // bucket = the nb_log2 bits below tau's top bit (monotone in the value)
   const uint32_t tbits = 64 - __builtin_clzll(t | 1ull);
   const uint32_t shift = tbits > nb_log2 ? tbits - nb_log2 : 0u;
   for (uint32_t e = tid; e < n; e += T) atomicAdd(&cnt[(uint32_t)(buf[e] >> shift)], 1u);
   __syncthreads();
-  // exclusive scan of the counters: each thread a contiguous range, the
-  // ranges' totals scanned across waves
-  {
+  // exclusive scan of cnt's low halves (or high halves: hi) over the buckets:
+  // each thread a contiguous range, the ranges' totals scanned across waves;
+  // returns the total
+  auto scan = [&](bool hi) -> uint32_t {
     const uint32_t per = (NB + T - 1) / T;
     const uint32_t b0 = min(tid * per, NB), b1 = min(b0 + per, NB);
     uint32_t sum = 0;
-    for (uint32_t b = b0; b < b1; ++b) sum += cnt[b];
+    for (uint32_t b = b0; b < b1; ++b) sum += hi ? cnt[b] >> 16 : cnt[b] & 0xFFFFu;
     uint32_t inc = sum;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = __shfl_up(inc, o);
@@ -640,13 +729,23 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
     __syncthreads();
     uint32_t run = inc - sum;
     for (uint32_t w = 0; w < (tid >> 6); ++w) run += wsum[w];
+    uint32_t total = 0;
+    for (uint32_t w = 0; w < (T + 63) / 64; ++w) total += wsum[w];
     for (uint32_t b = b0; b < b1; ++b) {
       const uint32_t c = cnt[b];
-      cnt[b] = run;
-      run += c;
+      if (hi) {
+        cnt[b] = (c & 0xFFFFu) | (run << 16);
+        run += c >> 16;
+      } else {
+        cnt[b] = run;
+        run += c;
+      }
     }
-  }
-  __syncthreads();
+    __syncthreads();
+    return total;
+  };
+  // (n <= sort_pow2 <= 16384: positions and counts fit 16 bits)
+  scan(false);
   // scatter into the table (afterwards cnt[b] = end of bucket b), then back
   // into LDS in bucket order
   for (uint32_t e = tid; e < n; e += T) {
@@ -663,18 +762,74 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
       if (e0 + j * T < n) buf[e0 + j * T] = v[j];
   }
   __syncthreads();
-  clear_slot();  // (the table's values are all in LDS now)
-  // every value of a bucket that starts below s: its rank in the bucket
+  // the first copy of a value in its bucket: no equal value before it there
+  auto first_copy = [&](uint32_t b0, uint32_t e, uint64_t v) {
+    for (uint32_t q = b0; q < e; ++q)
+      if (buf[q] == v) return false;
+    return true;
+  };
+  // a list may repeat a value (a set never does): when it does, the
+  // distinct values per bucket go to cnt's high halves and are scanned,
+  // cnt[b] = end of bucket b | (distinct values before bucket b) << 16
+  if (tid == 0) fill = 0;  // (any repeat)
+  __syncthreads();
+  if (!setm) {
+    for (uint32_t e = tid; e < n; e += T) {
+      const uint64_t v = buf[e];
+      const uint32_t b = (uint32_t)(v >> shift);
+      if (!first_copy(b ? cnt[b - 1] : 0u, e, v)) fill = 1u;
+    }
+  }
+  __syncthreads();
+  const bool dups = fill != 0;
+  uint32_t distinct = n;
+  if (dups) {
+    for (uint32_t e = tid; e < n; e += T) {
+      const uint64_t v = buf[e];
+      const uint32_t b = (uint32_t)(v >> shift);
+      const uint32_t b0 = b ? cnt[b - 1] & 0xFFFFu : 0u;
+      if (first_copy(b0, e, v)) atomicAdd(&cnt[b], 1u << 16);
+    }
+    __syncthreads();
+    distinct = scan(true);
+  }
+  uint32_t st = kSketchOk;
+  if (distinct < s && t != kEmpty) st = kSketchRetryLarger;
+  if (st != kSketchOk) {
+    // (the table region held only the scatter's copies: a list needs no
+    // clearing, a set is cleared for its next pass)
+    finish(st, setm);
+    return;
+  }
+  if (setm) clear_set();  // (the table's values are all in LDS now)
+  // every first copy of a bucket whose distinct values start below s: its
+  // rank among the distinct values
   uint64_t* o = out + (uint64_t)g * s;
-  const uint32_t m = min(s, n);
-  for (uint32_t e = tid; e < n; e += T) {
-    const uint64_t v = buf[e];
-    const uint32_t b = (uint32_t)(v >> shift);
-    const uint32_t b0 = b ? cnt[b - 1] : 0u, b1 = cnt[b];
-    if (b0 >= m) continue;
-    uint32_t r = b0;
-    for (uint32_t q = b0; q < b1; ++q) r += buf[q] < v ? 1u : 0u;
-    if (r < m) o[r] = v;
+  const uint32_t m = min(s, distinct);
+  if (!dups) {  // every value distinct: its rank is its bucket's start plus the smaller values there
+    for (uint32_t e = tid; e < n; e += T) {
+      const uint64_t v = buf[e];
+      const uint32_t b = (uint32_t)(v >> shift);
+      const uint32_t b0 = b ? cnt[b - 1] : 0u, b1 = cnt[b];
+      if (b0 >= m) continue;
+      uint32_t r = b0;
+      for (uint32_t q = b0; q < b1; ++q) r += buf[q] < v ? 1u : 0u;
+      if (r < m) o[r] = v;
+    }
+  } else {  // the first copies only, ranked among the first copies
+    for (uint32_t e = tid; e < n; e += T) {
+      const uint64_t v = buf[e];
+      const uint32_t b = (uint32_t)(v >> shift);
+      const uint32_t b0 = b ? cnt[b - 1] & 0xFFFFu : 0u, b1 = cnt[b] & 0xFFFFu;
+      const uint32_t d0 = cnt[b] >> 16;
+      if (d0 >= m || !first_copy(b0, e, v)) continue;
+      uint32_t r = d0;
+      for (uint32_t q = b0; q < b1; ++q) {
+        const uint64_t x = buf[q];
+        if (x < v && first_copy(b0, q, x)) ++r;
+      }
+      if (r < m) o[r] = v;
+    }
   }
   uint32_t mm = m;
   if ((f & kFlagSawMax) && mm < s) {
@@ -684,6 +839,8 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
   if (tid == 0) {
     lens[g] = mm;
     status[slot] = kSketchOk;
+    flags[slot] = 0u;
+    count[slot] = 0u;
   }
 }
 
@@ -722,7 +879,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
                                   uint32_t cap_log2,
                                   uint32_t* flags, uint32_t s,
                                   uint32_t sort_pow2, const uint32_t* row_of, uint64_t* out,
-                                  uint32_t* lens, uint32_t* status,
+                                  uint32_t* lens, uint32_t* status, uint32_t* count,
                                   hipStream_t st, const uint64_t* bad) {
   if (n_slots == 0) return hipSuccess;
   // ~4 candidates per bucket
@@ -739,7 +896,7 @@ hipError_t launch_sketch_finalize(const uint32_t* slot_list, uint32_t n_slots,
   const int threads = sort_pow2 >= 4096 ? kFinalizeMaxBlock : 256;
   hipLaunchKernelGGL(sketch_finalize_kernel, dim3(n_slots), dim3(threads), lds, st,
                      slot_list, slot_genome, tau, table, cap_log2, flags, s,
-                     sort_pow2, nb_log2, row_of, out, lens, status, bad);
+                     sort_pow2, nb_log2, row_of, out, lens, status, count, bad);
   return hipGetLastError();
 }
 

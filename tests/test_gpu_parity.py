@@ -87,12 +87,37 @@ def test_edge_records_and_retry_paths(gpu_ctx):
         [rnd(250000)],
         [(b"ACGTTGCAAT" * 2000)],  # low-complexity
     ]
+    # part of a genome repeated (10-30% of its k-mers twice): the candidate
+    # list repeats those values and still fits the finalize's sort, which
+    # keeps the first copy of each (append mode, no set-mode retry)
+    for frac in (0.1, 0.3):
+        r = rnd(100000)
+        genomes.append([r, r[:int(len(r) * frac)]])
+        genomes.append([r + r[20000:20000 + int(len(r) * frac)]])
     pk = ga.pack_records(genomes)
     sk, lens = gpu_ctx.sketch(pk)
     for g, recs in enumerate(genomes):
         exp = oracle.sketch_records(recs) if recs else np.zeros(0, np.uint64)
         assert lens[g] == len(exp), g
         assert (sk[g][:lens[g]] == exp).all(), g
+
+
+def test_repeated_kmers_dedup_in_candidate_list():
+    """Genomes with 10-30% of their k-mers twice: each candidate list holds
+    those values twice, fits the finalize's sort and keeps one copy (the
+    first pass succeeds: no retry pass, no set mode), equal to the oracle."""
+    rng = np.random.default_rng(12)
+    rnd = lambda n: np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)].tobytes()
+    genomes = []
+    for frac in (0.1, 0.2, 0.3):
+        r = rnd(100000)
+        genomes += [[r, r[:int(len(r) * frac)]], [r + r[30000:30000 + int(len(r) * frac)]]]
+    with ga.Context(k=21, sketch_size=1000) as ctx:
+        sk, lens = ctx.sketch(ga.pack_records(genomes))
+        assert ctx.fallbacks()["sketch_retry"] == 0
+    for g, recs in enumerate(genomes):
+        exp = oracle.sketch_records(recs)
+        assert lens[g] == len(exp) == 1000 and (sk[g][:lens[g]] == exp).all(), g
 
 
 def test_other_k_and_s():
