@@ -153,8 +153,8 @@ def k2_pmc(config):
 
 # K2 kernels timed under GG_KERNEL_PAIRS / GG_KERNEL_PAIRS_INDEX (the passing
 # pairs' device sort is not: it is output handling, ~0.1 ms at C3)
-K2_TIMED = ("index_scan", "bucket_hist", "bucket_base", "index_fill", "sort_histogram", "sort_pass",
-            "bucket_bounds", "index_bucket", "index_pairs")
+K2_TIMED = ("index_scan", "bucket_hist", "bucket_base", "index_fill", "index_sort", "bucket_bounds", "index_bucket",
+            "index_pairs")
 
 
 def k2_algorithmic_bytes(d_sk, d_len, n, s):

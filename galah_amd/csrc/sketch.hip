@@ -379,13 +379,11 @@ __device__ __forceinline__ void queue_push_mid(CandQueue& q, uint64_t f1, uint64
   }
 }
 
-// Insert the queued candidates with the lanes that are active (all of them
-// at the end of the kernel).  Positions past head + kQueue were inserted by
-// their pushes.
-__device__ __forceinline__ void queue_drain(CandQueue& q, const uint64_t* __restrict__ tau,
-                                            uint64_t* __restrict__ table, uint32_t cap_log2,
-                                            uint32_t* __restrict__ flags, uint32_t* __restrict__ count,
-                                            uint32_t min_pending) {
+// Finish the queued candidates with the lanes that are active (all of them
+// at the end of the kernel), entry x of the ring by fn(x).  Positions past
+// head + kQueue were finished by their pushes.
+template <class F>
+__device__ __forceinline__ void queue_drain(CandQueue& q, uint32_t min_pending, F&& fn) {
   const uint32_t head = __atomic_load_n(&q.head, __ATOMIC_RELAXED);
   const uint32_t tail = __atomic_load_n(&q.tail, __ATOMIC_RELAXED);
   if (tail - head < min_pending || tail == head) return;
@@ -393,10 +391,7 @@ __device__ __forceinline__ void queue_drain(CandQueue& q, const uint64_t* __rest
   for (;;) {
     const uint32_t e = atomicAdd(&q.claim, 1u);
     if (e >= end) break;
-    const uint32_t x = e & (kQueue - 1);
-    const uint32_t sl = q.slot[x];
-    const uint64_t hv = exact_hash(q.f1[x], q.f2[x]);
-    emit_candidates(hv <= tau[sl], hv, sl, table, cap_log2, flags, count);
+    fn(e & (kQueue - 1));
   }
   // every active lane is past its last claim here (lockstep): reopen the ring
   __atomic_store_n(&q.head, tail, __ATOMIC_RELAXED);
@@ -495,6 +490,13 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
 
   const uint64_t seed = SEED0 ? 0ull : a.seed;
   uint32_t r = 0;
+  auto drain = [&](uint32_t min_pending) {
+    queue_drain(q, min_pending, [&](uint32_t x) {
+      const uint32_t sl = q.slot[x];
+      const uint64_t hv = exact_hash(q.f1[x], q.f2[x]);
+      emit_candidates(hv <= a.tau[sl], hv, sl, a.table, a.cap_log2, a.flags, a.count);
+    });
+  };
 
   for (uint64_t sg = c0 + threadIdx.x; sg < send; sg += kBlock) {
     r = find_run(a.run_sstart, a.n_runs, sg, r);
@@ -557,9 +559,9 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
         }
       }
     }
-    queue_drain(q, a.tau, a.table, a.cap_log2, a.flags, a.count, kQueueDrain);
+    drain(kQueueDrain);
   }
-  queue_drain(q, a.tau, a.table, a.cap_log2, a.flags, a.count, 1);  // every lane of the wave is back
+  drain(1);  // every lane of the wave is back
 }
 
 // One workgroup per genome slot: gather the slot's candidates into LDS,
@@ -629,36 +631,84 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
     return;
   }
   const uint32_t NB = 1u << nb_log2;
+  const uint64_t t = tau[slot];
+  // bucket = the nb_log2 bits below tau's top bit (monotone in the value)
+  const uint32_t tbits = 64 - __builtin_clzll(t | 1ull);
+  const uint32_t shift = tbits > nb_log2 ? tbits - nb_log2 : 0u;
+  // exclusive scan of cnt's low halves (or high halves: hi) over the buckets:
+  // each thread a contiguous range, the ranges' totals scanned across waves;
+  // returns the total
+  auto scan = [&](bool hi) -> uint32_t {
+    const uint32_t per = (NB + T - 1) / T;
+    const uint32_t b0 = min(tid * per, NB), b1 = min(b0 + per, NB);
+    uint32_t sum = 0;
+    for (uint32_t b = b0; b < b1; ++b) sum += hi ? cnt[b] >> 16 : cnt[b] & 0xFFFFu;
+    uint32_t inc = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if ((tid & 63) >= (uint32_t)o) inc += y;
+    }
+    if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+    __syncthreads();
+    uint32_t run = inc - sum;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) run += wsum[w];
+    uint32_t total = 0;
+    for (uint32_t w = 0; w < (T + 63) / 64; ++w) total += wsum[w];
+    for (uint32_t b = b0; b < b1; ++b) {
+      const uint32_t c = cnt[b];
+      if (hi) {
+        cnt[b] = (c & 0xFFFFu) | (run << 16);
+        run += c >> 16;
+      } else {
+        cnt[b] = run;
+        run += c;
+      }
+    }
+    __syncthreads();
+    return total;
+  };
+  // (n <= sort_pow2 <= 16384: positions and counts fit 16 bits)
   uint32_t n;
-  if (!setm) {  // the list, coalesced
+  for (uint32_t i = tid; i < NB; i += T) cnt[i] = 0;
+  if (!setm) {
+    // The list is read from HBM twice: for the bucket histogram, then to
+    // scatter each value straight to its bucket's place in LDS (a copy in
+    // LDS scattered through the table region and read back cost a write and
+    // a dependent read of the whole list).  8 values per thread per step,
+    // all loads in flight at once (one load after another waited on HBM
+    // latency each).
     n = listed;
     if (n > sort_pow2) {
       finish(kSketchRetrySet, true);
       return;
     }
-    // 8 values per thread per step, all loads in flight at once (one load
-    // after another waited on HBM latency each: C5 finalize 1.8 -> 3.2 ms)
     constexpr uint32_t kListV = 8;
-    for (uint32_t i0 = tid * kListV; i0 < n; i0 += T * kListV) {
-      uint64_t v[kListV];
+    auto list_pass = [&](auto&& fn) {
+      for (uint32_t i0 = tid * kListV; i0 < n; i0 += T * kListV) {
+        uint64_t v[kListV];
 #pragma unroll
-      for (uint32_t j = 0; j < kListV; j += 2) {
-        if (i0 + j + 1 < n) {
-          const ulonglong2 p = *(const ulonglong2*)(tab + i0 + j);
-          v[j] = p.x;
-          v[j + 1] = p.y;
-        } else if (i0 + j < n) {
-          v[j] = tab[i0 + j];
+        for (uint32_t j = 0; j < kListV; j += 2) {
+          if (i0 + j + 1 < n) {
+            const ulonglong2 p = *(const ulonglong2*)(tab + i0 + j);
+            v[j] = p.x;
+            v[j + 1] = p.y;
+          } else if (i0 + j < n) {
+            v[j] = tab[i0 + j];
+          }
         }
-      }
 #pragma unroll
-      for (uint32_t j = 0; j < kListV; ++j)
-        if (i0 + j < n) buf[i0 + j] = v[j];
-    }
-    for (uint32_t i = tid; i < NB; i += T) cnt[i] = 0;
+        for (uint32_t j = 0; j < kListV; ++j)
+          if (i0 + j < n) fn(v[j]);
+      }
+    };
+    __syncthreads();
+    list_pass([&](uint64_t v) { atomicAdd(&cnt[(uint32_t)(v >> shift)], 1u); });
+    __syncthreads();
+    scan(false);
+    list_pass([&](uint64_t v) { buf[atomicAdd(&cnt[(uint32_t)(v >> shift)], 1u)] = v; });
+    __syncthreads();  // (cnt[b] = end of bucket b)
   } else {
     if (tid == 0) fill = 0;
-    for (uint32_t i = tid; i < NB; i += T) cnt[i] = 0;
     __syncthreads();
     // gather: each thread 8 consecutive slots per step, all loads in flight
     // at once (one workgroup per CU at s = 10000: with one load per thread per
@@ -704,64 +754,26 @@ __global__ __launch_bounds__(kFinalizeMaxBlock) void sketch_finalize_kernel(
       finish(kSketchRetrySmaller, true);
       return;
     }
-  }
-  __syncthreads();
-  const uint64_t t = tau[slot];
-  // bucket = the nb_log2 bits below tau's top bit (monotone in the value)
-  const uint32_t tbits = 64 - __builtin_clzll(t | 1ull);
-  const uint32_t shift = tbits > nb_log2 ? tbits - nb_log2 : 0u;
-  for (uint32_t e = tid; e < n; e += T) atomicAdd(&cnt[(uint32_t)(buf[e] >> shift)], 1u);
-  __syncthreads();
-  // exclusive scan of cnt's low halves (or high halves: hi) over the buckets:
-  // each thread a contiguous range, the ranges' totals scanned across waves;
-  // returns the total
-  auto scan = [&](bool hi) -> uint32_t {
-    const uint32_t per = (NB + T - 1) / T;
-    const uint32_t b0 = min(tid * per, NB), b1 = min(b0 + per, NB);
-    uint32_t sum = 0;
-    for (uint32_t b = b0; b < b1; ++b) sum += hi ? cnt[b] >> 16 : cnt[b] & 0xFFFFu;
-    uint32_t inc = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(inc, o);
-      if ((tid & 63) >= (uint32_t)o) inc += y;
-    }
-    if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+    for (uint32_t e = tid; e < n; e += T) atomicAdd(&cnt[(uint32_t)(buf[e] >> shift)], 1u);
     __syncthreads();
-    uint32_t run = inc - sum;
-    for (uint32_t w = 0; w < (tid >> 6); ++w) run += wsum[w];
-    uint32_t total = 0;
-    for (uint32_t w = 0; w < (T + 63) / 64; ++w) total += wsum[w];
-    for (uint32_t b = b0; b < b1; ++b) {
-      const uint32_t c = cnt[b];
-      if (hi) {
-        cnt[b] = (c & 0xFFFFu) | (run << 16);
-        run += c >> 16;
-      } else {
-        cnt[b] = run;
-        run += c;
-      }
+    scan(false);
+    // scatter into the table (afterwards cnt[b] = end of bucket b), then back
+    // into LDS in bucket order
+    for (uint32_t e = tid; e < n; e += T) {
+      const uint64_t v = buf[e];
+      tab[atomicAdd(&cnt[(uint32_t)(v >> shift)], 1u)] = v;
     }
     __syncthreads();
-    return total;
-  };
-  // (n <= sort_pow2 <= 16384: positions and counts fit 16 bits)
-  scan(false);
-  // scatter into the table (afterwards cnt[b] = end of bucket b), then back
-  // into LDS in bucket order
-  for (uint32_t e = tid; e < n; e += T) {
-    const uint64_t v = buf[e];
-    tab[atomicAdd(&cnt[(uint32_t)(v >> shift)], 1u)] = v;
-  }
-  __syncthreads();
-  for (uint32_t e0 = tid; e0 < n; e0 += 4 * T) {
-    uint64_t v[4];
+    for (uint32_t e0 = tid; e0 < n; e0 += 4 * T) {
+      uint64_t v[4];
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) v[j] = e0 + j * T < n ? tab[e0 + j * T] : 0ull;
+      for (uint32_t j = 0; j < 4; ++j) v[j] = e0 + j * T < n ? tab[e0 + j * T] : 0ull;
 #pragma unroll
-    for (uint32_t j = 0; j < 4; ++j)
-      if (e0 + j * T < n) buf[e0 + j * T] = v[j];
+      for (uint32_t j = 0; j < 4; ++j)
+        if (e0 + j * T < n) buf[e0 + j * T] = v[j];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   // the first copy of a value in its bucket: no equal value before it there
   auto first_copy = [&](uint32_t b0, uint32_t e, uint64_t v) {
     for (uint32_t q = b0; q < e; ++q)
@@ -858,6 +870,7 @@ hipError_t launch_k(const SketchLaunch& a, int grid, hipStream_t st) {
 }  // namespace
 
 int sketch_segment_len(int k) { return k1_seg_len(k, kGroup); }
+
 
 hipError_t launch_sketch_candidates(int k, const SketchLaunch& a, int grid,
                                     hipStream_t st) {
