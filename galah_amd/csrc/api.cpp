@@ -462,6 +462,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
     const uint32_t g1 = std::min(n_genomes, g0 + max_batch);
     const uint32_t nb = g1 - g0;
     std::vector<TauSearch> ts(nb);
+    std::vector<uint8_t> set_mode(nb, 0);  // slots the finalize switched to set mode (kSketchRetrySet)
     std::vector<uint64_t> h_tau(nb);
     std::vector<uint32_t> h_slot_genome(nb), h_slot_list(nb);
     for (uint32_t i = 0; i < nb; ++i) {
@@ -484,6 +485,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
         for (uint32_t slot : active) {
           if (status0[slot] == kSketchOk) continue;
           if (status0[slot] == kSketchRetrySet) {  // the same tau, in set mode
+            set_mode[slot] = 1;
             next.push_back(slot);
             continue;
           }
@@ -561,6 +563,8 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       a.cap_log2 = geom.cap_log2;
       a.flags = d_flags;
       a.count = d_count;
+      a.any_set_mode = 0;
+      for (uint32_t slot : active) a.any_set_mode |= set_mode[slot];
       a.seed = c->seed;
       const int g = (int)std::min<uint64_t>((uint64_t)grid, std::max<uint64_t>(1, (sacc + 255) / 256));
       GG_HIP(c, timed_launch(c, GG_KERNEL_SKETCH, kacc, st,
@@ -580,6 +584,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
       for (uint32_t slot : active) {
         if (status[slot] == kSketchOk) continue;
         if (status[slot] == kSketchRetrySet) {  // the same tau, in set mode
+          set_mode[slot] = 1;
           next.push_back(slot);
           continue;
         }

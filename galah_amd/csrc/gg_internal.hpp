@@ -53,6 +53,7 @@ struct SketchLaunch {
   uint32_t cap_log2;
   uint32_t* flags;             // [slots]
   uint32_t* count;             // [slots] candidates appended (append mode; 0 between passes)
+  uint32_t any_set_mode = 0;   // some slot of the launch collects in set mode (flags[slot] & kFlagSetMode)
   uint64_t seed;
   // (first pass queued before the host has seen the run index) the segment
   // count on the device, and the run-table check: K1 does nothing if set

@@ -302,12 +302,12 @@ __device__ __forceinline__ void insert_candidate(uint64_t* __restrict__ tab,
 // open-addressing set of insert_candidate, one atomicCAS per probe.  Both
 // are exact: every distinct hash <= tau is kept.  At s = 10000 (C5) the
 // candidates were ~1.3e8 memory-side atomicCAS per step in set mode.
-__device__ __forceinline__ void emit_candidates(bool pass, uint64_t hv, uint32_t sl, uint64_t* __restrict__ table,
-                                                uint32_t cap_log2, uint32_t* __restrict__ flags,
-                                                uint32_t* __restrict__ count) {
+__device__ __forceinline__ void emit_candidates(bool pass, uint64_t hv, uint32_t sl, bool setm,
+                                                uint64_t* __restrict__ table, uint32_t cap_log2,
+                                                uint32_t* __restrict__ flags, uint32_t* __restrict__ count) {
   bool app = false;
   if (pass) {
-    if ((flags[sl] & kFlagSetMode) || hv == kEmpty)
+    if (setm || hv == kEmpty)
       insert_candidate(table + ((uint64_t)sl << cap_log2), (1u << cap_log2) - 1u, flags + sl, hv);
     else
       app = true;
@@ -340,11 +340,17 @@ __device__ __forceinline__ void emit_candidates(bool pass, uint64_t hv, uint32_t
 // must stay fully unrolled, and the lanes of a wave diverge at run
 // boundaries): a push takes a position with ds_add; a push that finds the
 // ring full inserts directly; a drain hands out entries with ds_add too.
+// An entry carries everything its drain needs (the k-mer's tau and its
+// slot's collection mode), so a drain reads no global memory before its
+// emit: with the tau and mode loads there, each drain waited on two
+// dependent global round trips before its append atomic (C5: ~4e6 drains).
 constexpr uint32_t kQueue = 64;
 constexpr uint32_t kQueueDrain = kQueue / 2;
+constexpr uint32_t kSlotSetMode = 1u << 31;  // slot field: the slot collects in set mode
 struct CandQueue {
   uint64_t f1[kQueue], f2[kQueue];  // fmix64_mid of h1 / h2: the exact test runs at the drain
-  uint32_t slot[kQueue];
+  uint64_t tau[kQueue];
+  uint32_t slot[kQueue];            // | kSlotSetMode
   uint32_t head, tail, claim;
 };
 
@@ -354,8 +360,8 @@ __device__ __forceinline__ uint64_t exact_hash(uint64_t f1, uint64_t f2) {
 
 // A k-mer whose high-word sum passed the prefilter: queued with its two
 // finaliser states; the drain finishes the hash and inserts it if <= tau.
-__device__ __forceinline__ void queue_push_mid(CandQueue& q, uint64_t f1, uint64_t f2, uint32_t slot,
-                                               const uint64_t* __restrict__ tau, uint64_t* __restrict__ table,
+__device__ __forceinline__ void queue_push_mid(CandQueue& q, uint64_t f1, uint64_t f2, uint32_t slot_mode,
+                                               uint64_t tau, uint64_t* __restrict__ table,
                                                uint32_t cap_log2, uint32_t* __restrict__ flags,
                                                uint32_t* __restrict__ count) {
   const uint32_t pos = atomicAdd(&q.tail, 1u);
@@ -363,12 +369,14 @@ __device__ __forceinline__ void queue_push_mid(CandQueue& q, uint64_t f1, uint64
   if (queued) {
     q.f1[pos & (kQueue - 1)] = f1;
     q.f2[pos & (kQueue - 1)] = f2;
-    q.slot[pos & (kQueue - 1)] = slot;
+    q.tau[pos & (kQueue - 1)] = tau;
+    q.slot[pos & (kQueue - 1)] = slot_mode;
   }
   if (!queued) {  // ring full (rare): finish and emit this one now, on its own
     const uint64_t hv = exact_hash(f1, f2);
-    if (hv <= tau[slot]) {
-      if ((flags[slot] & kFlagSetMode) || hv == kEmpty) {
+    const uint32_t slot = slot_mode & ~kSlotSetMode;
+    if (hv <= tau) {
+      if ((slot_mode & kSlotSetMode) || hv == kEmpty) {
         insert_candidate(table + ((uint64_t)slot << cap_log2), (1u << cap_log2) - 1u, flags + slot, hv);
       } else {
         const uint32_t at = atomicAdd(&count[slot], 1u);
@@ -492,9 +500,10 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
   uint32_t r = 0;
   auto drain = [&](uint32_t min_pending) {
     queue_drain(q, min_pending, [&](uint32_t x) {
-      const uint32_t sl = q.slot[x];
+      const uint32_t sm = q.slot[x];
       const uint64_t hv = exact_hash(q.f1[x], q.f2[x]);
-      emit_candidates(hv <= a.tau[sl], hv, sl, a.table, a.cap_log2, a.flags, a.count);
+      emit_candidates(hv <= q.tau[x], hv, sm & ~kSlotSetMode, (sm & kSlotSetMode) != 0, a.table, a.cap_log2,
+                      a.flags, a.count);
     });
   };
 
@@ -555,7 +564,8 @@ __global__ __launch_bounds__(kBlock, GG_K1_MIN_WAVES) void sketch_candidates_ker
 #pragma unroll
         for (int j = 0; j < kGroup; ++j) {
           if (hs[j] <= thr && (uint32_t)(g * kGroup + j) < cnt)
-            queue_push_mid(q, f1[j], f2[j], slot, a.tau, a.table, a.cap_log2, a.flags, a.count);
+            queue_push_mid(q, f1[j], f2[j], slot | ((a.any_set_mode && (a.flags[slot] & kFlagSetMode)) ? kSlotSetMode : 0u),
+                           tau, a.table, a.cap_log2, a.flags, a.count);
         }
       }
     }
