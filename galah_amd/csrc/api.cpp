@@ -627,6 +627,7 @@ gg_status ensure_cmin(gg_ctx* c, float min_ani, uint32_t** d_cmin, uint32_t** d_
   return GG_OK;
 }
 
+#if defined(GG_XCHECK)
 // Work items of the table kernels: runs of <= seg_tiles column tiles of one
 // tile row, inside tiles [tb, te).
 void build_segments(std::vector<PairSeg>& segs, uint64_t nb, uint64_t tb, uint64_t te, uint32_t seg_tiles) {
@@ -642,6 +643,7 @@ void build_segments(std::vector<PairSeg>& segs, uint64_t nb, uint64_t tb, uint64
     t = last;
   }
 }
+#endif
 
 // Gate kernel (pairs_gate.hip): tables for the tile rows of [tb, te), then
 // the column stream.  Work items are (tile row, row block, column segment)
@@ -927,7 +929,17 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
   const uint64_t nb = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
   te = std::min<uint64_t>(te, gg_pair_tiles(n));
   const uint64_t work = c->timing ? pairs_in_tiles(n, tb, te) : 0;
+#if defined(GG_XCHECK)
   int kern = (c->pairs_kernel == 1 && pairs_table_rows(c->s) == 0) ? 2 : c->pairs_kernel;
+#else
+  // the cross-check forms (table, merge) live in pairs.hip, which only the
+  // test build libgalahgpu_xcheck.so carries
+  if (c->pairs_kernel == 1 || c->pairs_kernel == 2)
+    return fail(c, GG_ERR_INVALID_ARG,
+                "GALAHGPU_PAIRS_KERNEL=table|merge: the cross-check kernels are built into "
+                "libgalahgpu_xcheck.so (tests) only");
+  int kern = c->pairs_kernel;
+#endif
   // auto (0) / index (4): the inverted index when no pair without a shared
   // hash can pass (min_ani > 0) and the packed (row, position) values fit
   // 32 bits; "auto" also leaves tiny sets to the gate kernel
@@ -946,6 +958,9 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
     kern = 0;
   }
   ++c->pair_paths[(kern == 0 || kern == 3) ? GG_PATH_GATE : GG_PATH_OTHER];
+  if (kern == 0 || kern == 3)
+    return pairs_gate(c, d_sk, d_lens, n, nb, tb, te, d_cmin, d_sufmin, d_out, cap, d_count, work, st);
+#if defined(GG_XCHECK)
   if (kern == 2) {
     PairsLaunch a;
     a.sketches = d_sk;
@@ -963,8 +978,6 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs(a, st); }));
     return GG_OK;
   }
-  if (kern == 0 || kern == 3)
-    return pairs_gate(c, d_sk, d_lens, n, nb, tb, te, d_cmin, d_sufmin, d_out, cap, d_count, work, st);
   build_segments(c->seg_host, nb, tb, te, kSegTiles);
   if (c->seg_host.empty()) return GG_OK;
   PairSeg* d_segs;
@@ -987,6 +1000,7 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS, work, st, [&] { return launch_pairs_table(b, st); }));
     return GG_OK;
   }
+#endif
   return GG_OK;
 }
 

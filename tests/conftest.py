@@ -61,6 +61,32 @@ def golden():
             "paths": [golden_path(n) for n in names]}
 
 
+_XCHECK = []
+
+
+def xcheck_module():
+    """galah_amd bound to libgalahgpu_xcheck.so: the product library plus the
+    cross-check pair kernels (GALAHGPU_PAIRS_KERNEL=table|merge, pairs.hip),
+    which the product libgalahgpu.so does not carry.  A second module object
+    over a second library in the same process (one HIP runtime)."""
+    if not _XCHECK:
+        import importlib.util
+        lib = os.path.join(ROOT, "galah_amd", "lib", "libgalahgpu_xcheck.so")
+        spec = importlib.util.spec_from_file_location("galah_amd_xcheck", os.path.join(ROOT, "galah_amd", "__init__.py"))
+        mod = importlib.util.module_from_spec(spec)
+        old = os.environ.get("GALAHGPU_LIB")
+        os.environ["GALAHGPU_LIB"] = lib
+        try:
+            spec.loader.exec_module(mod)
+        finally:
+            if old is None:
+                os.environ.pop("GALAHGPU_LIB")
+            else:
+                os.environ["GALAHGPU_LIB"] = old
+        _XCHECK.append(mod)
+    return _XCHECK[0]
+
+
 @pytest.fixture(scope="session")
 def gpu_ctx():
     import galah_amd

@@ -29,6 +29,7 @@ import pytest
 
 import galah_amd as ga
 import oracle
+from conftest import xcheck_module
 from test_host import ACGT
 
 pytestmark = pytest.mark.gpu
@@ -176,7 +177,8 @@ def check_config(ctx, d_words, runs, n, s, thr, genome_bases, spot):
     try:
         for kern in ("merge", "gate", "index"):
             os.environ["GALAHGPU_PAIRS_KERNEL"] = kern
-            with ga.Context(k=21, sketch_size=s) as mctx:
+            # (merge: the cross-check kernel of the test build)
+            with (xcheck_module() if kern == "merge" else ga).Context(k=21, sketch_size=s) as mctx:
                 bands[kern] = device_pairs(mctx, d_sk, d_len, n, tb, te, thr)
                 if kern == "index":
                     assert mctx.pair_paths() == {"index": 1, "index_abandoned": 0, "gate": 0, "other": 0,

@@ -9,6 +9,7 @@ import pytest
 
 import galah_amd as ga
 import oracle
+from conftest import xcheck_module
 from test_host import EDGE_RECORDS, packed_records, unpack_run
 
 pytestmark = pytest.mark.gpu
@@ -309,10 +310,23 @@ def test_gate_table_and_merge_kernels_match_oracle(monkeypatch, s, min_ani):
     got = {}
     for kern in ("gate", "table", "merge", "index", "auto"):
         monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", kern)
-        with ga.Context(k=21, sketch_size=s) as ctx:
+        # (table, merge: the cross-check kernels of the test build)
+        lib = xcheck_module() if kern in ("table", "merge") else ga
+        with lib.Context(k=21, sketch_size=s) as ctx:
             got[kern] = as_tuples(ctx.pairs(sk, lens, np.float32(min_ani)))
     for kern in got:
         assert got[kern] == exp, kern
+
+
+def test_product_refuses_cross_check_kernels(monkeypatch):
+    """GALAHGPU_PAIRS_KERNEL=table|merge names kernels the product library
+    does not carry: the call fails loudly instead of running another form."""
+    sk, lens = random_sketch_set(np.random.default_rng(1), 40, 100, 3)
+    for kern in ("table", "merge"):
+        monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", kern)
+        with ga.Context(k=21, sketch_size=100) as ctx:
+            with pytest.raises(ga.GalahGpuError, match="libgalahgpu_xcheck.so"):
+                ctx.pairs(sk, lens, np.float32(0.5))
 
 
 def test_c5_mixed_sizes_s10000(gpu_ctx, monkeypatch):
@@ -363,7 +377,7 @@ def test_c5_mixed_sizes_s10000(gpu_ctx, monkeypatch):
     exp = [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in o]
     assert [x for x in as_tuples(p) if x[1] < sub] == exp
     monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "merge")
-    with ga.Context(k=21, sketch_size=s) as ctx:
+    with xcheck_module().Context(k=21, sketch_size=s) as ctx:
         assert as_tuples(ctx.pairs(sk[:sub], ln[:sub], thr)) == exp
 
 

@@ -60,6 +60,26 @@ def test_no_oracle_in_product_library():
         assert b"oracle_sketch" not in f.read()
 
 
+def test_cross_check_kernels_only_in_test_library():
+    """pairs.hip's table / merge kernels (independent K2 forms the parity
+    tests compare against) are built into libgalahgpu_xcheck.so only: the
+    product carries the default index and gate kernels, and the test library
+    exports the same C ABI."""
+    import subprocess
+    from conftest import xcheck_module
+    with open(ga.LIB_PATH, "rb") as f:
+        prod = f.read()
+    assert b"pairs_merge_kernel" not in prod and b"pairs_table_kernel" not in prod
+    assert b"index_pairs_kernel" in prod and b"pairs_gate_kernel" in prod
+    gx = xcheck_module()
+    with open(gx.LIB_PATH, "rb") as f:
+        assert b"pairs_merge_kernel" in f.read()
+    a = subprocess.run(["nm", "-D", "--defined-only", ga.LIB_PATH], capture_output=True, text=True).stdout
+    b = subprocess.run(["nm", "-D", "--defined-only", gx.LIB_PATH], capture_output=True, text=True).stdout
+    exported = lambda t: sorted(x.split()[-1] for x in t.splitlines() if " T gg_" in x)
+    assert exported(a) == exported(b) and len(exported(a)) >= len(ga.EXPORTED_SYMBOLS)
+
+
 def test_create_without_device_fails_loudly():
     import torch
     if torch.cuda.is_available():
