@@ -422,22 +422,38 @@ def files_leg(a, device, steps):
         print("[bench] files leg: wrote %d gzip FASTA files (%.2f GB) in %.1f s" % (n, out["gz_bytes"] / 1e9,
               out["write_s"]), file=sys.stderr, flush=True)
         thr = ga.parse_percentage(a.min_ani)
-        with ga.Context(k=21, sketch_size=1000, seed=0, device=device, host_threads=T) as ctx:
-            ctx.precluster_files(paths[:16], thr)  # warm-up (device, library, threads)
-            times, found, ph = [], 0, {p: 0.0 for p in ga.PHASES}
-            for _ in range(max(1, steps)):
-                t1 = time.perf_counter()
-                pairs, _ani = ctx.precluster_files(paths, thr)
-                times.append(time.perf_counter() - t1)
-                found = len(pairs)
-                for p, v in ctx.phase_times().items():
-                    ph[p] += v
-        t = float(np.median(times))
         bases = n * glen
-        out.update({"steps": len(times), "s_per_call_median": round(t, 4), "s_per_call": [round(x, 4) for x in times],
+
+        def timed(inflate):
+            """gg_precluster_files over the paths, GALAHGPU_INFLATE=inflate."""
+            os.environ["GALAHGPU_INFLATE"] = inflate
+            try:
+                with ga.Context(k=21, sketch_size=1000, seed=0, device=device, host_threads=T) as ctx:
+                    ctx.precluster_files(paths[:16], thr)  # warm-up (device, library, threads)
+                    times, found, ph = [], 0, {p: 0.0 for p in ga.PHASES}
+                    for _ in range(max(1, steps)):
+                        t1 = time.perf_counter()
+                        pairs, _ani = ctx.precluster_files(paths, thr)
+                        times.append(time.perf_counter() - t1)
+                        found = len(pairs)
+                        for p, v in ctx.phase_times().items():
+                            ph[p] += v
+                    fb = ctx.fallbacks()["inflate_host"]
+            finally:
+                os.environ.pop("GALAHGPU_INFLATE", None)
+            t = float(np.median(times))
+            return {"steps": len(times), "s_per_call_median": round(t, 4), "s_per_call": [round(x, 4) for x in times],
                     "gbases_per_s": round(bases / t / 1e9, 3), "genome_pairs_per_s": round(n * (n - 1) / 2 / t, 1),
-                    "pairs_found": int(found),
-                    "phase_ms": {p: round(v / len(times), 2) for p, v in ph.items()}})
+                    "pairs_found": int(found), "phase_ms": {p: round(v / len(times), 2) for p, v in ph.items()},
+                    "inflate_host_batches": fb}, pairs
+
+        host, hp = timed("host")
+        out.update(host)
+        t = host["s_per_call_median"]
+        # the same files inflated on the GPU (inflate.hip): the host threads only read
+        dev, dp = timed("device")
+        dev["same_pairs_as_host"] = bool(np.array_equal(hp, dp))
+        out["device_inflate"] = dev
         probe = os.path.join(ROOT, "scripts", "gunzip_probe")
         if os.path.exists(probe):
             r = subprocess.run([probe, str(T)] + paths, capture_output=True, text=True, timeout=300)
@@ -449,7 +465,9 @@ def files_leg(a, device, steps):
             else:
                 out["pure_decode_error"] = r.stderr[-300:]
         out["note"] = ("kernel-only headline vs this: the same path from gzip files on %d host threads; galah's "
-                       "distances() starts from these paths (src/finch.rs:47)" % T)
+                       "distances() starts from these paths (src/finch.rs:47); top level: gunzip + parse + pack on "
+                       "the host threads (GALAHGPU_INFLATE=host); device_inflate: gzip bytes to the GPU, inflated "
+                       "and parsed there (inflate.hip, parse.hip)" % T)
     finally:
         shutil.rmtree(d, ignore_errors=True)
     return out

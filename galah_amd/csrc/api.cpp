@@ -1384,11 +1384,11 @@ gg_status gg_info_line(const gg_ctx* ctx, char* buf, size_t cap) {
   snprintf(line, sizeof line,
            "galahgpu: %zu device(s) [%s]; sketch %.1f ms, replicate %.2f ms, pairs %.2f ms, merge %.2f ms; "
            "fallbacks: index->gate %llu, index full sort %llu, host-staged peer copies %llu (links without peer "
-           "access %llu), sketch retry passes %llu",
+           "access %llu), sketch retry passes %llu, host-inflated batches %llu",
            M, ords.c_str(), ctx->phase_ms[GG_PHASE_SKETCH], ctx->phase_ms[GG_PHASE_REPLICATE],
            ctx->phase_ms[GG_PHASE_PAIRS], ctx->phase_ms[GG_PHASE_MERGE], (unsigned long long)fb[0],
            (unsigned long long)fb[1], (unsigned long long)fb[2], (unsigned long long)staged_links,
-           (unsigned long long)fb[3]);
+           (unsigned long long)fb[3], (unsigned long long)fb[4]);
   const size_t n = std::min(cap - 1, strlen(line));
   memcpy(buf, line, n);
   buf[n] = 0;

@@ -197,6 +197,14 @@ gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d
                               uint64_t tb, uint64_t te, float min_ani, std::vector<gg_pair>& res,
                               hipStream_t st);
 
+// A batch of files inflated on m's device (inflate_host.cpp): h_in (pinned,
+// in_bytes) holds files[f]'s bytes; *d_text receives the batch's FASTA text,
+// file f at foff[f] (16-byte aligned, gaps '\n').  *ok = false (status GG_OK)
+// when the device path does not take the batch: the caller decodes it on the
+// host.  Synchronises m->stream.
+gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const std::vector<InflateFile>& files,
+                        uint8_t** d_text, std::vector<uint64_t>& foff, bool* ok);
+
 template <typename T>
 T* copy_out(const std::vector<T>& v) {
   T* p = (T*)malloc(std::max<size_t>(v.size(), 1) * sizeof(T));

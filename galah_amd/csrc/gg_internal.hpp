@@ -234,6 +234,65 @@ struct ParseLaunch {
 hipError_t parse_batch_pass(int pass, const ParseLaunch& p, hipStream_t st);
 uint32_t parse_block_bytes();
 
+// inflate.hip: gzip members inflated on the device (inflate_core.hpp).  All
+// pointers are device memory.  The batch holds each file's deflate data
+// from word file_word[f] (file_bits[f] bits), followed by >= 3 words of
+// padding.
+struct InflateSearch {
+  const uint32_t* in;
+  const uint64_t* file_word;
+  const uint64_t* file_bits;
+  const uint32_t* chunk_file;  // [n_chunks]
+  const uint64_t* chunk_bit0;  // [n_chunks] first bit searched
+  uint32_t chunk_bits;         // bits searched per chunk
+  uint32_t n_chunks;
+  uint64_t* start;             // [n_chunks] first block header found (~0: none)
+};
+struct InflateDecode {
+  const uint32_t* in;
+  const uint64_t* file_word;
+  const uint64_t* file_bits;
+  const uint32_t* lane_file;   // [n_lanes]
+  const uint64_t* lane_start;  // [n_lanes] a block start
+  const uint64_t* lane_end;    // [n_lanes] the next lane's start (~0: the file's last lane)
+  uint32_t n_lanes;
+  uint32_t* tok;               // tokens of lane l at tok_off[l] (a multiple of 4), at most tok_cap[l]
+  const uint64_t* tok_off;
+  const uint64_t* tok_cap;
+  uint32_t* status;            // [n_lanes] inflate::DecodeStatus
+  uint64_t* n_tok;             // [n_lanes]
+  uint64_t* out_len;           // [n_lanes] bytes the lane's tokens stand for
+  uint64_t* last_end;          // [n_lanes] bit after the lane's last block
+  uint32_t* bfinal;            // [n_lanes] the lane decoded the stream's last block
+};
+struct InflatePlace {
+  const uint32_t* tok;
+  const uint64_t* tok_off;
+  const uint64_t* n_tok;
+  const uint32_t* lane_file;
+  const uint64_t* lane_out;    // [n_lanes] text position of the lane's first byte
+  const uint64_t* file_text;   // [n_files] text position of the file's first byte
+  uint32_t n_lanes;
+  uint32_t* val;               // [text_len] literal (0x80000000 | byte) or the position copied
+  uint32_t* flags;             // bit 0: a distance before its file's start, bit 1: a runaway chain
+};
+// one file of an inflate batch (inflate_host.cpp): its bytes at
+// [data_off, data_off + data_len) of the batch (data_off 4-byte aligned):
+// the deflate data of a gzip member with its trailer's isize and crc, or
+// plain text (gz false)
+struct InflateFile {
+  uint64_t data_off = 0, data_len = 0;
+  uint32_t isize = 0, crc = 0;
+  bool gz = false;
+};
+bool gzip_member(const uint8_t* buf, size_t n, size_t* data_off, size_t* data_len, uint32_t* isize, uint32_t* crc);
+hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st);
+hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st);
+// place + resolve (text[0, text_len), val pre-set to literal '\n') + CRC-32 per file
+hipError_t launch_inflate_place(const InflatePlace& a, uint64_t text_len, uint8_t* text, uint32_t n_files,
+                                const uint64_t* file_text, const uint64_t* file_len, uint32_t* crc,
+                                hipStream_t st);
+
 struct IndexBuild {
   const uint64_t* sketches;
   const uint32_t* lens;
@@ -354,8 +413,10 @@ class PackStream {
   // raw: the workers only read (and gunzip) each file and keep its FASTA
   // text for the device parser (parse.hip); FASTQ files are rewritten as
   // FASTA records on the way.  Otherwise they pack on the host.
+  // keep_gzip (raw streams): gzip files are kept as read, compressed, for
+  // the device inflate (inflate_host.cpp); get_raw reports them with *gz.
   PackStream(const char* const* paths, uint32_t n, int k, int n_threads, uint64_t budget_bytes,
-             bool stamp_files = false, bool raw = false);
+             bool stamp_files = false, bool raw = false, bool keep_gzip = false);
   ~PackStream();
   PackStream(const PackStream&) = delete;
   PackStream& operator=(const PackStream&) = delete;
@@ -364,7 +425,7 @@ class PackStream {
   gg_status get(uint32_t i, const std::vector<uint32_t>** words, const std::vector<gg_run>** runs,
                 std::string* err);
   // raw streams: genome i's FASTA text.  Valid until release(i).
-  gg_status get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err);
+  gg_status get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err, bool* gz = nullptr);
   // The file's size and mtime as stat'ed just before it was read (valid
   // after get(i) succeeded; the streams are built with stamp_files).
   FileStamp stamp(uint32_t i);
@@ -379,6 +440,11 @@ class PackStream {
   struct Impl;
   std::unique_ptr<Impl> p_;
 };
+
+// The FASTA text of a gzip file's bytes as the raw streams give it (host
+// gunzip, FASTQ records rewritten): the host fallback of the device inflate.
+gg_status host_text_from_gzip(const std::vector<uint8_t>& gz, const char* name, std::vector<uint8_t>& text,
+                              std::string& err);
 
 // api.cpp helpers used by pack.cpp
 void set_thread_error(const std::string& msg);

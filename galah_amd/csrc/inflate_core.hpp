@@ -1,0 +1,517 @@
+// DEFLATE (RFC 1951) decoding primitives shared by the device inflate
+// (inflate.hip) and its host-side tests: one lane decodes one run of
+// blocks; nothing here allocates or synchronises.
+//
+// The device path inflates many gzip members at once without decoding any
+// stream from its start serially:
+//   1. search  every ~CH compressed bytes of a stream, the first bit position
+//              where a valid dynamic-block header parses (block_header_ok)
+//   2. decode   one lane per found start: Huffman-decode its blocks into
+//               tokens (literal byte, or match length + distance) until it
+//               lands exactly on the next start; back-references are not
+//               resolved here, so no lane needs the window of the lanes
+//               before it
+//   3. place / resolve  (inflate.hip) token output positions by prefix sums,
+//               every output byte a literal or a pointer to an earlier
+//               byte, pointers followed to their literal
+// A search hit that is not a block boundary is never landed on by the lane
+// before it (decode reports the overrun and the host drops that start), so
+// the output never depends on the search being right.
+#pragma once
+
+#include <cstdint>
+
+#if defined(__HIPCC__)
+#define GG_HD __host__ __device__ __forceinline__
+#else
+#define GG_HD inline
+#endif
+
+namespace gg {
+namespace inflate {
+
+// The DEFLATE stream of one gzip member, as 32-bit little-endian words with
+// at least two words of padding after its last byte; bit positions count
+// from the member's first deflate byte, LSB first (RFC 1951 3.1.1).
+struct Bits {
+  const uint32_t* w;
+  // the 32 stream bits starting at pos, the first in bit 0
+  GG_HD uint32_t peek(uint64_t pos) const {
+    const uint64_t i = pos >> 5;
+    const uint32_t sh = (uint32_t)pos & 31u;
+    const uint64_t v = ((uint64_t)w[i + 1] << 32) | w[i];
+    return (uint32_t)(v >> sh);
+  }
+  GG_HD uint32_t get(uint64_t& pos, uint32_t n) const {  // n <= 25
+    const uint32_t v = peek(pos) & ((1u << n) - 1u);
+    pos += n;
+    return v;
+  }
+};
+
+// The same stream read forward through three cached words: the symbol loop
+// peeks 32 bits per symbol from registers and loads one word per 32 bits
+// consumed, ahead of its use (a Bits::peek per symbol waited on two loads).
+struct Cursor {
+  const uint32_t* w;
+  uint64_t pos;
+  uint64_t wi;  // word of pos
+  uint32_t a, b, c;  // words wi, wi + 1, wi + 2
+  GG_HD void seek(uint64_t p) {
+    pos = p;
+    wi = p >> 5;
+    a = w[wi];
+    b = w[wi + 1];
+    c = w[wi + 2];
+  }
+  GG_HD uint32_t peek() const {
+    const uint32_t sh = (uint32_t)pos & 31u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(b, a, sh);
+#else
+    return sh ? (a >> sh) | (b << (32 - sh)) : a;
+#endif
+  }
+  GG_HD void skip(uint32_t n) {  // n <= 32
+    pos += n;
+    if ((pos >> 5) != wi) {
+      a = b;
+      b = c;
+      ++wi;
+      c = w[wi + 2];
+    }
+  }
+  GG_HD uint32_t get(uint32_t n) {  // n <= 31
+    const uint32_t v = peek() & ((1u << n) - 1u);
+    skip(n);
+    return v;
+  }
+};
+
+GG_HD uint32_t rev15(uint32_t v) {  // the low 15 bits in reverse order: a left-justified 15-bit code
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_bitreverse32(v) >> 17;
+#else
+  uint32_t r = 0;
+  for (int i = 0; i < 15; ++i) r |= ((v >> i) & 1u) << (14 - i);
+  return r;
+#endif
+}
+
+constexpr int kMaxBits = 15;
+constexpr int kLitSyms = 288;   // lit/len alphabet (286 codable + 2 reserved)
+constexpr int kDistSyms = 32;   // distance alphabet (30 codable + 2 reserved)
+constexpr int kClSyms = 19;     // code-length alphabet
+constexpr uint32_t kWindow = 32768;
+
+// Canonical Huffman code (RFC 1951 3.2.2) for decoding: a left-justified
+// 15-bit code x has length L = the smallest l with x < limit[l], and symbol
+// sym[base[L] + (x >> (15 - L))].
+struct Canon {
+  uint32_t limit[kMaxBits + 1];
+  int32_t base[kMaxBits + 1];
+};
+
+// Counts per length -> limits and bases.  Returns 0 complete, 1 incomplete,
+// -1 over-subscribed.  max_len receives the longest length used (0: none).
+GG_HD int canon_from_counts(const uint32_t (&count)[kMaxBits + 1], Canon& c, int& max_len) {
+  int left = 1;
+  max_len = 0;
+  for (int l = 1; l <= kMaxBits; ++l) {
+    left = (left << 1) - (int)count[l];
+    if (left < 0) return -1;
+    if (count[l]) max_len = l;
+  }
+  uint32_t first = 0, offs = 0;
+  for (int l = 1; l <= kMaxBits; ++l) {
+    c.limit[l] = (first + count[l]) << (kMaxBits - l);
+    c.base[l] = (int32_t)offs - (int32_t)first;
+    offs += count[l];
+    first = (first + count[l]) << 1;
+  }
+  c.limit[0] = 0;
+  c.base[0] = 0;
+  return left == 0 ? 0 : 1;
+}
+
+// Length of the code whose left-justified 15 bits are x (kMaxBits + 1: no
+// such code, x past an incomplete code's last one).
+GG_HD int code_len(const Canon& c, uint32_t x) {
+  int L = 1;
+#pragma unroll
+  for (int l = 1; l < kMaxBits; ++l) L += x >= c.limit[l] ? 1 : 0;
+  return x >= c.limit[kMaxBits] ? kMaxBits + 1 : L;
+}
+
+// zlib's inflate_table acceptance: complete, or incomplete only when the
+// longest code has length 1 (a lone symbol); no symbols at all is accepted
+// for the distance code (a block without matches) and refused elsewhere.
+GG_HD bool code_ok(int r, int max_len, bool allow_empty) {
+  if (r < 0) return false;
+  if (max_len == 0) return allow_empty;
+  return r == 0 || max_len == 1;
+}
+
+// RFC 1951 3.2.5 length and distance tables
+GG_HD uint32_t len_base(uint32_t i) {  // lit/len symbol 257 + i
+  constexpr uint16_t b[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                              31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+  return b[i];
+}
+GG_HD uint32_t len_extra(uint32_t i) { return i < 8 || i == 28 ? 0u : (i - 4) >> 2; }
+GG_HD uint32_t dist_base(uint32_t d) {
+  constexpr uint16_t b[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
+                              193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+  return b[d];
+}
+GG_HD uint32_t dist_extra(uint32_t d) { return d < 4 ? 0u : (d - 2) >> 1; }
+
+constexpr uint8_t kClOrder[kClSyms] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
+
+// The code-length code of a dynamic header: its 19 lengths (packed 3 bits
+// each into cl_lens), its canonical code and the symbols sorted.
+struct ClCode {
+  Canon c{};
+  uint8_t sym[kClSyms];
+};
+
+// Reads HCLEN + 4 code-length-code lengths at pos; false if the code is not
+// complete (zlib refuses an incomplete code-length code).
+GG_HD bool read_cl_code(const Bits& in, uint64_t& pos, uint32_t hclen, ClCode& cl) {
+  uint32_t lens[kClSyms];
+#pragma unroll
+  for (int i = 0; i < kClSyms; ++i) lens[i] = 0;
+  for (uint32_t i = 0; i < hclen; ++i) lens[kClOrder[i]] = in.get(pos, 3);
+  uint32_t count[kMaxBits + 1];
+#pragma unroll
+  for (int l = 0; l <= kMaxBits; ++l) count[l] = 0;
+#pragma unroll
+  for (int i = 0; i < kClSyms; ++i) count[lens[i]] += 1;
+  count[0] = 0;
+  int max_len;
+  if (canon_from_counts(count, cl.c, max_len) != 0) return false;  // incomplete or over-subscribed
+  uint32_t offs[8];
+  uint32_t o = 0;
+#pragma unroll
+  for (int l = 0; l < 8; ++l) {
+    offs[l] = o;
+    if (l) o += count[l];
+  }
+#pragma unroll
+  for (int s = 0; s < kClSyms; ++s)
+    if (lens[s]) cl.sym[offs[lens[s]]++] = (uint8_t)s;
+  return true;
+}
+
+GG_HD int decode_sym(const Bits& in, uint64_t& pos, const Canon& c, const uint8_t* sym8, const uint16_t* sym16) {
+  const uint32_t x = rev15(in.peek(pos));
+  const int L = code_len(c, x);
+  if (L > kMaxBits) return -1;
+  pos += (uint32_t)L;
+  const int idx = c.base[L] + (int)(x >> (kMaxBits - L));
+  return sym8 ? sym8[idx] : sym16[idx];
+}
+
+// Walks the lit/len + distance code lengths of a dynamic header (after the
+// code-length code), calling f(symbol index, length) for each nonzero
+// length; false on a malformed sequence.
+template <class F>
+GG_HD bool walk_lengths(const Bits& in, uint64_t& pos, const ClCode& cl, uint32_t n, F&& f) {
+  uint32_t i = 0, prev = 0;
+  while (i < n) {
+    const int s = decode_sym(in, pos, cl.c, cl.sym, nullptr);
+    if (s < 0) return false;
+    if (s < 16) {
+      if (s) f(i, (uint32_t)s);
+      prev = (uint32_t)s;
+      ++i;
+      continue;
+    }
+    uint32_t rep, val = 0;
+    if (s == 16) {
+      if (i == 0) return false;
+      rep = 3 + in.get(pos, 2);
+      val = prev;
+    } else if (s == 17) {
+      rep = 3 + in.get(pos, 3);
+    } else {
+      rep = 11 + in.get(pos, 7);
+    }
+    if (i + rep > n) return false;
+    if (val)
+      for (uint32_t r = 0; r < rep; ++r) f(i + r, val);
+    i += rep;
+    if (s != 16) prev = 0;
+  }
+  return true;
+}
+
+// Is there a valid dynamic-block header at pos?  (The search's test: a
+// complete code-length code, length sequence in range, an end-of-block
+// code, lit/len and distance codes zlib accepts.)  On success pos is moved
+// past the header.
+GG_HD bool block_header_ok(const Bits& in, uint64_t& pos) {
+  const uint32_t h = in.peek(pos);
+  if (((h >> 1) & 3u) != 2u) return false;  // BTYPE 10: dynamic Huffman
+  const uint32_t hlit = ((h >> 3) & 31u) + 257u, hdist = ((h >> 8) & 31u) + 1u, hclen = ((h >> 13) & 15u) + 4u;
+  if (hlit > 286 || hdist > 30) return false;
+  uint64_t p = pos + 17;
+  ClCode cl;
+  if (!read_cl_code(in, p, hclen, cl)) return false;
+  uint32_t lc[kMaxBits + 1], dc[kMaxBits + 1];
+#pragma unroll
+  for (int l = 0; l <= kMaxBits; ++l) lc[l] = dc[l] = 0;
+  bool eob = false;
+  if (!walk_lengths(in, p, cl, hlit + hdist, [&](uint32_t i, uint32_t len) {
+        if (i < hlit) {
+          lc[len] += 1;
+          if (i == 256) eob = true;
+        } else {
+          dc[len] += 1;
+        }
+      }))
+    return false;
+  if (!eob) return false;
+  Canon c{};
+  int ml = 0;
+  int r = canon_from_counts(lc, c, ml);
+  if (!code_ok(r, ml, false)) return false;
+  r = canon_from_counts(dc, c, ml);
+  if (!code_ok(r, ml, true)) return false;
+  pos = p;
+  return true;
+}
+
+// One lane's tables for its current block.  The limits are indexed by
+// constants only (code_len unrolled: registers on the device); the bases and
+// the symbols sorted by (length, value) are indexed by data, so they live in
+// the Store (host: arrays; device: the lane's LDS):
+//   int32_t& lbase(int), dbase(int); uint16_t& lsym(int); uint8_t& dsym(int)
+template <class Store>
+struct LaneTables {
+  uint32_t llim[kMaxBits + 1], dlim[kMaxBits + 1];
+  Store s;
+  GG_HD void set_lit(const Canon& c) {
+#pragma unroll
+    for (int l = 0; l <= kMaxBits; ++l) {
+      llim[l] = c.limit[l];
+      s.lbase(l) = c.base[l];
+    }
+  }
+  GG_HD void set_dist(const Canon& c) {
+#pragma unroll
+    for (int l = 0; l <= kMaxBits; ++l) {
+      dlim[l] = c.limit[l];
+      s.dbase(l) = c.base[l];
+    }
+  }
+  GG_HD int lit(Cursor& cur) {
+    const uint32_t x = rev15(cur.peek());
+    int L = 1;
+#pragma unroll
+    for (int l = 1; l < kMaxBits; ++l) L += x >= llim[l] ? 1 : 0;
+    if (x >= llim[kMaxBits]) return -1;
+    cur.skip((uint32_t)L);
+    return s.lsym(s.lbase(L) + (int)(x >> (kMaxBits - L)));
+  }
+  GG_HD int dist(Cursor& cur) {
+    const uint32_t x = rev15(cur.peek());
+    int L = 1;
+#pragma unroll
+    for (int l = 1; l < kMaxBits; ++l) L += x >= dlim[l] ? 1 : 0;
+    if (x >= dlim[kMaxBits]) return -1;
+    cur.skip((uint32_t)L);
+    return s.dsym(s.dbase(L) + (int)(x >> (kMaxBits - L)));
+  }
+};
+
+// Host store: plain arrays.
+struct ArrayStore {
+  int32_t lb[kMaxBits + 1], db[kMaxBits + 1];
+  uint16_t ls[kLitSyms];
+  uint8_t ds[kDistSyms];
+  int32_t& lbase(int l) { return lb[l]; }
+  int32_t& dbase(int l) { return db[l]; }
+  uint16_t& lsym(int i) { return ls[i]; }
+  uint8_t& dsym(int i) { return ds[i]; }
+};
+
+// Reads the block header at pos and builds the lane's tables.  Returns
+// btype (0 stored, 1 fixed, 2 dynamic) or -1 on a malformed header; bfinal
+// receives the BFINAL bit.  For a stored block pos ends at its first data
+// byte and stored_len receives LEN.
+template <class Store>
+GG_HD int read_block_header(const Bits& in, uint64_t& pos, LaneTables<Store>& t, uint32_t& bfinal,
+                            uint32_t& stored_len) {
+  const uint32_t h = in.peek(pos);
+  bfinal = h & 1u;
+  const uint32_t btype = (h >> 1) & 3u;
+  if (btype == 0) {
+    pos = (pos + 3 + 7) & ~7ull;
+    const uint32_t v = in.peek(pos);
+    const uint32_t len = v & 0xFFFFu, nlen = v >> 16;
+    if ((len ^ nlen) != 0xFFFFu) return -1;
+    pos += 32;
+    stored_len = len;
+    return 0;
+  }
+  uint32_t lc[kMaxBits + 1], dc[kMaxBits + 1];
+#pragma unroll
+  for (int l = 0; l <= kMaxBits; ++l) lc[l] = dc[l] = 0;
+  int ml = 0;
+  Canon c{};
+  if (btype == 1) {  // fixed codes (RFC 1951 3.2.6)
+    pos += 3;
+    lc[7] = 24;
+    lc[8] = 152;
+    lc[9] = 112;
+    dc[5] = 32;
+    canon_from_counts(lc, c, ml);
+    t.set_lit(c);
+    canon_from_counts(dc, c, ml);
+    t.set_dist(c);
+    uint32_t o7 = 0, o8 = 24, o9 = 176;
+    for (uint32_t sy = 0; sy < (uint32_t)kLitSyms; ++sy) {
+      if (sy <= 143) t.s.lsym((int)o8++) = (uint16_t)sy;
+      else if (sy <= 255) t.s.lsym((int)o9++) = (uint16_t)sy;
+      else if (sy <= 279) t.s.lsym((int)o7++) = (uint16_t)sy;
+      else t.s.lsym((int)o8++) = (uint16_t)sy;
+    }
+    for (uint32_t d = 0; d < (uint32_t)kDistSyms; ++d) t.s.dsym((int)d) = (uint8_t)d;
+    return 1;
+  }
+  if (btype != 2) return -1;
+  const uint32_t hlit = ((h >> 3) & 31u) + 257u, hdist = ((h >> 8) & 31u) + 1u, hclen = ((h >> 13) & 15u) + 4u;
+  if (hlit > 286 || hdist > 30) return -1;
+  uint64_t p = pos + 17;
+  ClCode cl;
+  if (!read_cl_code(in, p, hclen, cl)) return -1;
+  const uint64_t lens_at = p;
+  bool eob = false;
+  // pass 1: counts per length
+  if (!walk_lengths(in, p, cl, hlit + hdist, [&](uint32_t i, uint32_t len) {
+        if (i < hlit) {
+          lc[len] += 1;
+          if (i == 256) eob = true;
+        } else {
+          dc[len] += 1;
+        }
+      }))
+    return -1;
+  if (!eob) return -1;
+  int r = canon_from_counts(lc, c, ml);
+  if (!code_ok(r, ml, false)) return -1;
+  t.set_lit(c);
+  r = canon_from_counts(dc, c, ml);
+  if (!code_ok(r, ml, true)) return -1;
+  t.set_dist(c);
+  // pass 2: symbols sorted by (length, value) (the lengths are walked again
+  // instead of being stored)
+  uint32_t lo[kMaxBits + 1], doff[kMaxBits + 1];
+  uint32_t a = 0, b = 0;
+#pragma unroll
+  for (int l = 1; l <= kMaxBits; ++l) {
+    lo[l] = a;
+    doff[l] = b;
+    a += lc[l];
+    b += dc[l];
+  }
+  uint64_t q = lens_at;
+  walk_lengths(in, q, cl, hlit + hdist, [&](uint32_t i, uint32_t len) {
+    if (i < hlit) t.s.lsym((int)lo[len]++) = (uint16_t)i;
+    else t.s.dsym((int)doff[len]++) = (uint8_t)(i - hlit);
+  });
+  pos = p;
+  return 2;
+}
+
+// Token: a literal byte (bit 31 clear) or a match, bit 31 set, length in
+// bits 15..23 (3..258), distance - 1 in bits 0..14.
+GG_HD uint32_t tok_match(uint32_t len, uint32_t dist) { return 0x80000000u | (len << 15) | (dist - 1u); }
+GG_HD bool tok_is_match(uint32_t t) { return (t >> 31) != 0; }
+GG_HD uint32_t tok_len(uint32_t t) { return tok_is_match(t) ? (t >> 15) & 0x1FFu : 1u; }
+GG_HD uint32_t tok_dist(uint32_t t) { return (t & 0x7FFFu) + 1u; }
+
+enum DecodeStatus : uint32_t {
+  kDecOk = 0,          // landed on `end` (or ended the stream with BFINAL when end = ~0)
+  kDecOverrun = 1,     // passed `end` without landing on it: `end` is not a block boundary
+  kDecBad = 2,         // malformed data
+  kDecFull = 3,        // token capacity exceeded
+  kDecFinalEarly = 4,  // the stream's last block ended before `end`
+};
+
+// Decodes blocks from pos until a block ends exactly at `end` (~0: until
+// the BFINAL block), writing tokens through emit(t) (returns false when
+// full).  out_len receives the bytes the tokens stand for, last_end the bit
+// position after the last decoded block.
+template <class Store, class Emit>
+GG_HD uint32_t decode_blocks(const Bits& in, uint64_t pos, uint64_t end, uint64_t limit_bits, LaneTables<Store>& t,
+                             Emit&& emit, uint64_t& out_len, uint64_t& last_end, uint32_t& bfinal_seen) {
+  out_len = 0;
+  bfinal_seen = 0;
+  last_end = pos;
+  for (;;) {
+    if (pos == end) {
+      last_end = pos;
+      return kDecOk;
+    }
+    if (pos > end || pos >= limit_bits) {
+      last_end = pos;
+      return kDecOverrun;
+    }
+    uint32_t bfinal = 0, stored = 0;
+    const int bt = read_block_header(in, pos, t, bfinal, stored);
+    if (bt < 0) {
+      last_end = pos;
+      return kDecBad;
+    }
+    if (bt == 0) {
+      for (uint32_t i = 0; i < stored; ++i)
+        if (!emit(in.get(pos, 8))) return kDecFull;
+      out_len += stored;
+    } else {
+      Cursor cur{in.w};
+      cur.seek(pos);
+      for (;;) {
+        if (cur.pos >= limit_bits) {
+          last_end = cur.pos;
+          return kDecBad;
+        }
+        const int sy = t.lit(cur);
+        if (sy < 0) {
+          last_end = cur.pos;
+          return kDecBad;
+        }
+        if (sy < 256) {
+          if (!emit((uint32_t)sy)) return kDecFull;
+          out_len += 1;
+          continue;
+        }
+        if (sy == 256) break;
+        const uint32_t li = (uint32_t)sy - 257u;
+        if (li >= 29) {
+          last_end = cur.pos;
+          return kDecBad;
+        }
+        const uint32_t len = len_base(li) + cur.get(len_extra(li));
+        const int d = t.dist(cur);
+        if (d < 0 || d >= 30) {
+          last_end = cur.pos;
+          return kDecBad;
+        }
+        const uint32_t dist = dist_base((uint32_t)d) + cur.get(dist_extra((uint32_t)d));
+        if (!emit(tok_match(len, dist))) return kDecFull;
+        out_len += len;
+      }
+      pos = cur.pos;
+    }
+    if (bfinal) {
+      bfinal_seen = 1;
+      last_end = pos;
+      return end == ~0ull ? kDecOk : kDecFinalEarly;
+    }
+  }
+}
+
+}  // namespace inflate
+}  // namespace gg

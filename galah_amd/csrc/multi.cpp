@@ -281,6 +281,12 @@ gg_status pairs_with_ani(gg_ctx* c, const std::vector<gg_pair>& res, gg_pair** p
 constexpr uint32_t kBatchGenomes = 32;          // genomes per K1 batch
 constexpr uint64_t kBatchWords = 64ull << 20;   // or 1 Gbases of packed words, whichever first
 constexpr uint64_t kBatchText = 1ull << 30;     // raw (device-parsed) batches: 1 GiB of FASTA text
+// device-inflate batches: up to 4096 files, 384 MiB of gzip data or 1.5 GiB
+// of text (the inflate's parallel units are the streams' blocks, ~30 per
+// 3 Mbp genome: a batch needs hundreds of files to fill the GPU)
+constexpr uint32_t kBatchGenomesGz = 4096;
+constexpr uint64_t kBatchGzBytes = 384ull << 20;
+constexpr uint64_t kBatchGzText = 3ull << 29;
 
 // memcpy on up to T threads (staging copies of a batch into pinned memory:
 // one thread moves ~10 GB/s, a batch of FASTA text is up to 1 GiB)
@@ -310,6 +316,14 @@ void parallel_copy(void* dst, const void* src, size_t bytes, int T) {
 // words) through host memory and PCIe, so the host packer stays the default.
 bool device_parse() {
   const char* e = getenv("GALAHGPU_PARSE");
+  return e && strcmp(e, "device") == 0;
+}
+
+// GALAHGPU_INFLATE=device: gzip files go to the device compressed and are
+// inflated there (inflate.hip), then parsed there (parse.hip); the host
+// threads only read files.
+bool device_inflate() {
+  const char* e = getenv("GALAHGPU_INFLATE");
   return e && strcmp(e, "device") == 0;
 }
 
@@ -446,6 +460,122 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   return GG_OK;
 }
 
+// Grows m's pinned staging buffer to hold `need` bytes, keeping its first
+// `keep` bytes (at most ~2x need, up to `hint`).
+gg_status grow_pinned(gg_ctx* m, size_t need, size_t keep, size_t hint) {
+  if (need <= m->pinned_bytes) return GG_OK;
+  std::vector<uint8_t> kept((const uint8_t*)m->pinned, (const uint8_t*)m->pinned + keep);
+  void* stage;
+  GG_HIP(m, pinned(m, std::max(need, std::min<size_t>(2 * need, hint)), &stage));
+  if (keep) memcpy(stage, kept.data(), keep);
+  return GG_OK;
+}
+
+// One device-inflate batch of the streamed file list (GALAHGPU_INFLATE=
+// device): files [b0, b1) of the stream are staged as read (gzip files
+// compressed, each positioned so its deflate data starts on a 4-byte
+// boundary), inflated on m's device (inflate_host.cpp) and parsed there.
+// The batch is cut early at kBatchGzBytes of gzip data or kBatchGzText of
+// text (the rest goes back through cursor); row_of receives one row per
+// file taken.  A batch the device inflate does not take is decoded on the
+// host threads instead (counted in GG_FALLBACK_INFLATE_HOST).
+gg_status inflate_files_batch(gg_ctx* m, PackStream& stream, uint32_t b0, uint32_t b1, std::mutex& cursor_mu,
+                              uint32_t& cursor, bool& stop, bool& file_error, int copy_threads, uint32_t** d_words,
+                              uint64_t* nw, std::vector<gg_run>& runs, std::vector<uint32_t>& row_of,
+                              const std::vector<uint32_t>& miss_at, const char* const* names) {
+  struct Held {
+    uint64_t pos, len;
+    bool gz;
+  };
+  std::vector<InflateFile> files;
+  std::vector<Held> held;
+  uint64_t at = 0, gz_bytes = 0, text_est = 0;
+  bool host_only = false;
+  for (uint32_t i = b0; i < b1; ++i) {
+    const std::vector<uint8_t>* tx;
+    bool gz = false;
+    std::string err;
+    const gg_status gs = stream.get_raw(i, &tx, &err, &gz);
+    if (gs != GG_OK) {
+      std::lock_guard<std::mutex> lk(cursor_mu);
+      if (!stop) file_error = true;
+      return fail(m, gs, err);
+    }
+    InflateFile f;
+    size_t doff = 0, dlen = tx->size();
+    uint32_t isz = 0, crc = 0;
+    const bool member = gz && gzip_member(tx->data(), tx->size(), &doff, &dlen, &isz, &crc);
+    if (gz && !member) host_only = true;  // (a gzip header this path does not read: the host decodes)
+    const uint64_t p = (at + doff + 3) / 4 * 4 - doff;
+    gg_status ps = grow_pinned(m, p + tx->size() + 16, at, 2 * kBatchGzBytes);
+    if (ps != GG_OK) return ps;
+    parallel_copy((uint8_t*)m->pinned + p, tx->data(), tx->size(), copy_threads);
+    f.gz = member;
+    f.data_off = p + doff;
+    f.data_len = dlen;
+    f.isize = isz;
+    f.crc = crc;
+    files.push_back(f);
+    held.push_back(Held{p, tx->size(), gz});
+    at = p + tx->size();
+    gz_bytes += gz ? tx->size() : 0;
+    text_est += member ? isz : tx->size();
+    row_of.push_back(miss_at[i]);
+    stream.release(i);
+    if ((gz_bytes >= kBatchGzBytes || text_est >= kBatchGzText) && i + 1 < b1) {  // cut the batch here
+      std::lock_guard<std::mutex> lk(cursor_mu);
+      if (cursor == b1) {
+        cursor = i + 1;
+        b1 = i + 1;
+      }
+    }
+  }
+  uint8_t* d_text = nullptr;
+  std::vector<uint64_t> foff;
+  bool ok = false;
+  if (!host_only) {
+    const gg_status is = inflate_batch(m, (const uint8_t*)m->pinned, at, files, &d_text, foff, &ok);
+    if (is != GG_OK) return is;
+  }
+  if (!ok) {  // the host decodes this batch (and reports a corrupt file)
+    ++m->fallbacks[GG_FALLBACK_INFLATE_HOST];
+    const size_t nf = files.size();
+    std::vector<std::vector<uint8_t>> texts(nf);
+    std::vector<gg_status> sts(nf, GG_OK);
+    std::vector<std::string> errs(nf);
+    std::vector<std::thread> th;
+    const int T = std::max(1, std::min<int>(copy_threads, (int)nf));
+    auto work = [&](int t) {
+      for (size_t f = (size_t)t; f < nf; f += (size_t)T) {
+        const uint8_t* b = (const uint8_t*)m->pinned + held[f].pos;
+        if (held[f].gz) {
+          const std::vector<uint8_t> gzb(b, b + held[f].len);
+          sts[f] = host_text_from_gzip(gzb, names[b0 + f], texts[f], errs[f]);
+        } else {
+          texts[f].assign(b, b + held[f].len);
+        }
+      }
+    };
+    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+    for (size_t f = 0; f < nf; ++f)
+      if (sts[f] != GG_OK) {
+        std::lock_guard<std::mutex> lk(cursor_mu);
+        if (!stop) file_error = true;
+        return fail(m, sts[f], errs[f]);
+      }
+    foff.assign(nf + 1, 0);
+    for (size_t f = 0; f < nf; ++f) foff[f + 1] = foff[f] + (texts[f].size() + 15) / 16 * 16;
+    std::vector<uint8_t> all(foff[nf], '\n');
+    for (size_t f = 0; f < nf; ++f) memcpy(all.data() + foff[f], texts[f].data(), texts[f].size());
+    GG_HIP(m, scratch_t(m, "stage_text", std::max<uint64_t>(foff[nf], 16) + 16, &d_text));
+    if (foff[nf]) GG_HIP(m, hipMemcpyAsync(d_text, all.data(), foff[nf], hipMemcpyHostToDevice, m->stream));
+    GG_HIP(m, hipStreamSynchronize(m->stream));
+  }
+  return parse_raw_batch(m, d_text, foff, d_words, nw, runs);
+}
+
 // Sketches of paths[0..n) into every member's full array (rows[i]); spans
 // receives the rows each member sketched.  Genomes with a valid entry in
 // cache_dir are read from it (every member receives those rows from the
@@ -502,10 +632,12 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
   const uint32_t nm = (uint32_t)miss.size();
   // in-flight packed genomes: ~2 batches per member, at least 1 GiB
   const uint64_t budget = std::max<uint64_t>(1ull << 30, 2ull * M * kBatchWords * sizeof(uint32_t));
-  const bool raw = device_parse();
+  const bool gz_dev = device_inflate();
+  const bool raw = gz_dev || device_parse();
   // staging copies per member: the host threads shared among the members
   const int copy_threads = std::max(1, std::min(16, ingest_threads(c->host_threads)) / (int)M);
-  PackStream stream(miss.data(), nm, c->k, c->host_threads, budget, cache_dir != nullptr, raw);
+  PackStream stream(miss.data(), nm, c->k, c->host_threads, gz_dev ? std::max<uint64_t>(budget, 3 * kBatchGzBytes) : budget,
+                    cache_dir != nullptr, raw, gz_dev);
   std::mutex cursor_mu;
   uint32_t cursor = 0;
   bool stop = false;        // a member failed: the others take no more batches
@@ -537,7 +669,7 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
         std::lock_guard<std::mutex> lk(cursor_mu);
         if (stop || cursor >= nm) break;
         b0 = cursor;
-        b1 = std::min(nm, b0 + kBatchGenomes);
+        b1 = std::min(nm, b0 + (gz_dev ? kBatchGenomesGz : kBatchGenomes));
         cursor = b1;
       }
       // assemble the batch in the pinned staging buffer
@@ -546,7 +678,11 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
       uint64_t nw = 0;
       uint32_t g = 0;
       uint32_t* d_words = nullptr;
-      if (raw) {  // FASTA text -> device parser
+      if (gz_dev) {  // gzip -> device inflate -> device parser
+        const gg_status gs = inflate_files_batch(m, stream, b0, b1, cursor_mu, cursor, stop, file_error, copy_threads,
+                                                 &d_words, &nw, runs, row_of, miss_at, miss.data());
+        if (gs != GG_OK) return gs;
+      } else if (raw) {  // FASTA text -> device parser
         std::vector<uint64_t> foff(1, 0);
         for (uint32_t i = b0; i < b1; ++i) {
           const std::vector<uint8_t>* tx;
@@ -586,6 +722,7 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
         const gg_status ps = parse_raw_batch(m, d_text, foff, &d_words, &nw, runs);
         if (ps != GG_OK) return ps;
       }
+      if (gz_dev) b1 = b0 + (uint32_t)row_of.size();  // (the batch may have been cut)
       for (uint32_t i = b0; !raw && i < b1; ++i, ++g) {
         const std::vector<uint32_t>* w;
         const std::vector<gg_run>* rr;

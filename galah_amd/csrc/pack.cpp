@@ -75,7 +75,8 @@ __attribute__((target("sse4.1"))) inline uint32_t pack16(const uint8_t* p, uint3
 // Packs the runs of ONE genome; bases start at word 0 of its own buffer.
 struct GenomePacker {
   int k;
-  std::vector<uint8_t> text;  // raw streams: the FASTA text (parse.hip)
+  std::vector<uint8_t> text;  // raw streams: the FASTA text (parse.hip), or the gzip file itself (gz)
+  bool gz = false;
   std::vector<uint32_t> words;
   std::vector<gg_run> runs;  // base relative to this genome's first word
   uint64_t n_bases = 0;
@@ -492,6 +493,7 @@ struct PackStream::Impl {
   uint64_t budget;
   bool stamping = false;
   bool raw = false;
+  bool keep_gzip = false;
   std::vector<FileStamp> stamps;
   std::mutex mu;
   std::condition_variable cv_done;   // a genome finished packing
@@ -526,6 +528,15 @@ struct PackStream::Impl {
       if (!paths[i]) {
         s = GG_ERR_INVALID_ARG;
         e = "null path";
+      } else if (raw && keep_gzip) {  // gzip files stay compressed (device inflate)
+        if (!read_raw(paths[i], buf, e)) {
+          s = GG_ERR_IO;
+        } else if (buf.size() >= 2 && buf[0] == 0x1f && buf[1] == 0x8b) {
+          gp->gz = true;
+          gp->text.swap(buf);
+        } else {
+          s = raw_text(buf, paths[i], gp->text, e);
+        }
       } else if (!read_file(paths[i], buf, e)) {
         s = GG_ERR_IO;
       } else if (raw) {
@@ -549,11 +560,12 @@ struct PackStream::Impl {
 };
 
 PackStream::PackStream(const char* const* paths, uint32_t n, int k, int n_threads, uint64_t budget_bytes,
-                       bool stamp_files, bool raw)
+                       bool stamp_files, bool raw, bool keep_gzip)
     : p_(new Impl()) {
   Impl& m = *p_;
   m.stamping = stamp_files;
   m.raw = raw;
+  m.keep_gzip = keep_gzip;
   m.stamps.resize(stamp_files ? n : 0);
   m.paths = paths;
   m.n = n;
@@ -600,7 +612,7 @@ gg_status PackStream::get(uint32_t i, const std::vector<uint32_t>** words, const
   return GG_OK;
 }
 
-gg_status PackStream::get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err) {
+gg_status PackStream::get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err, bool* gz) {
   Impl& m = *p_;
   std::unique_lock<std::mutex> lk(m.mu);
   m.cv_done.wait(lk, [&] { return m.state[i] >= 2 || (m.stop && m.state[i] == 0); });
@@ -613,7 +625,47 @@ gg_status PackStream::get_raw(uint32_t i, const std::vector<uint8_t>** text, std
     return m.st[i];
   }
   *text = &m.g[i]->text;
+  if (gz) *gz = m.g[i]->gz;
   return GG_OK;
+}
+
+gg_status host_text_from_gzip(const std::vector<uint8_t>& gz, const char* name, std::vector<uint8_t>& text,
+                              std::string& err) {
+  std::vector<uint8_t> buf;
+  if (deflate_lib().ok) {
+    if (!gunzip_libdeflate(gz, buf, name, err)) return GG_ERR_IO;
+  } else {  // zlib, all members
+    z_stream zs{};
+    if (inflateInit2(&zs, 15 + 32) != Z_OK) {
+      err = "zlib: out of memory";
+      return GG_ERR_OUT_OF_MEMORY;
+    }
+    zs.next_in = const_cast<uint8_t*>(gz.data());
+    zs.avail_in = (uInt)gz.size();
+    buf.resize(std::max<size_t>(gz.size() * 4, 1 << 16));
+    size_t out = 0;
+    for (;;) {
+      if (out == buf.size()) buf.resize(buf.size() * 2);
+      zs.next_out = buf.data() + out;
+      zs.avail_out = (uInt)std::min<size_t>(buf.size() - out, 1u << 30);
+      const uInt room = zs.avail_out;
+      const int r = inflate(&zs, Z_NO_FLUSH);
+      out += room - zs.avail_out;
+      if (r == Z_STREAM_END) {
+        if (zs.avail_in < 18) break;  // (trailing bytes shorter than a member)
+        inflateReset(&zs);  // the next member
+        continue;
+      }
+      if ((r != Z_OK && r != Z_BUF_ERROR) || (r == Z_BUF_ERROR && zs.avail_in == 0)) {
+        inflateEnd(&zs);
+        err = std::string("gzip decode error in ") + name;
+        return GG_ERR_IO;
+      }
+    }
+    buf.resize(out);
+    inflateEnd(&zs);
+  }
+  return raw_text(buf, name, text, err);
 }
 
 FileStamp PackStream::stamp(uint32_t i) {

@@ -359,13 +359,19 @@ gg_status gg_pair_paths(const gg_ctx* ctx, uint64_t* paths);
  *                                (the HIP runtime stages them through host
  *                                memory; see gg_peer_links)
  *   GG_FALLBACK_SKETCH_RETRY     K1 passes re-run for genomes whose first
- *                                bottom-s threshold missed (exact either way) */
+ *                                bottom-s threshold missed (exact either way)
+ *   GG_FALLBACK_INFLATE_HOST     file batches the device gzip inflate
+ *                                (GALAHGPU_INFLATE=device) handed back to the
+ *                                host threads (several members per file,
+ *                                FASTQ, a stream it could not chain, a CRC
+ *                                mismatch) */
 enum {
   GG_FALLBACK_INDEX_TO_GATE = 0,
   GG_FALLBACK_INDEX_FULL_SORT = 1,
   GG_FALLBACK_PEER_STAGED = 2,
   GG_FALLBACK_SKETCH_RETRY = 3,
-  GG_FALLBACK_COUNT = 4
+  GG_FALLBACK_INFLATE_HOST = 4,
+  GG_FALLBACK_COUNT = 5
 };
 gg_status gg_fallbacks(const gg_ctx* ctx, uint64_t* counts /* [GG_FALLBACK_COUNT] */);
 /* links[a * M + b] (M = gg_device_count) for members a and b: 1 when member

@@ -1,0 +1,204 @@
+// Host test of the DEFLATE core of the device inflate
+// (galah_amd/csrc/inflate_core.hpp): every gzip file given is decoded
+//   (a) serially from its first block, and
+//   (b) as the device does it: block starts searched every `chunk` bytes,
+//       one independent decode per start (an overrun drops the start it
+//       passed), tokens placed by prefix sums and back-references followed
+//       to their literals,
+// and both must equal zlib's output byte for byte.  Prints one JSON line per
+// file (blocks, starts found, starts dropped).  Built by tests/cpp/Makefile,
+// run by tests/test_inflate.py.
+#include <zlib.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../galah_amd/csrc/inflate_core.hpp"
+
+using namespace gg::inflate;
+
+static bool read_all(const char* path, std::vector<uint8_t>& out) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return false;
+  uint8_t buf[1 << 16];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) out.insert(out.end(), buf, buf + n);
+  fclose(f);
+  return true;
+}
+
+static bool zlib_gunzip(const std::vector<uint8_t>& gz, std::vector<uint8_t>& out) {
+  z_stream s{};
+  if (inflateInit2(&s, 15 + 16) != Z_OK) return false;
+  s.next_in = const_cast<uint8_t*>(gz.data());
+  s.avail_in = (uInt)gz.size();
+  uint8_t buf[1 << 16];
+  int r;
+  do {
+    s.next_out = buf;
+    s.avail_out = sizeof buf;
+    r = inflate(&s, Z_NO_FLUSH);
+    if (r != Z_OK && r != Z_STREAM_END) {
+      inflateEnd(&s);
+      return false;
+    }
+    out.insert(out.end(), buf, buf + (sizeof buf - s.avail_out));
+  } while (r != Z_STREAM_END);
+  inflateEnd(&s);
+  return true;
+}
+
+// offset of the deflate data of the gzip member at the start of gz (RFC 1952)
+static long gzip_data_offset(const std::vector<uint8_t>& gz) {
+  if (gz.size() < 18 || gz[0] != 0x1f || gz[1] != 0x8b || gz[2] != 8) return -1;
+  const uint8_t flg = gz[3];
+  size_t p = 10;
+  if (flg & 4) p += 2 + (gz[p] | (gz[p + 1] << 8));
+  if (flg & 8) {
+    while (p < gz.size() && gz[p]) ++p;
+    ++p;
+  }
+  if (flg & 16) {
+    while (p < gz.size() && gz[p]) ++p;
+    ++p;
+  }
+  if (flg & 2) p += 2;
+  return p < gz.size() ? (long)p : -1;
+}
+
+static void expand(const std::vector<uint32_t>& toks, std::vector<uint8_t>& out) {
+  for (uint32_t t : toks) {
+    if (!tok_is_match(t)) {
+      out.push_back((uint8_t)t);
+    } else {
+      const uint32_t len = tok_len(t), dist = tok_dist(t);
+      const size_t from = out.size() - dist;
+      for (uint32_t i = 0; i < len; ++i) out.push_back(out[from + i]);
+    }
+  }
+}
+
+int main(int argc, char** argv) {
+  int failures = 0;
+  uint32_t chunk = 4096;
+  int first = 1;
+  if (argc > 2 && std::string(argv[1]) == "--chunk") {
+    chunk = (uint32_t)atoi(argv[2]);
+    first = 3;
+  }
+  for (int a = first; a < argc; ++a) {
+    std::vector<uint8_t> gz, want;
+    if (!read_all(argv[a], gz) || !zlib_gunzip(gz, want)) {
+      fprintf(stderr, "%s: unreadable\n", argv[a]);
+      ++failures;
+      continue;
+    }
+    const long off = gzip_data_offset(gz);
+    const size_t nbytes = gz.size() - (size_t)off;
+    std::vector<uint32_t> words((nbytes + 3) / 4 + 4, 0);
+    memcpy(words.data(), gz.data() + off, nbytes);
+    const Bits in{words.data()};
+    const uint64_t limit_bits = (uint64_t)nbytes * 8;
+    LaneTables<ArrayStore> tab;
+    // (a) serially
+    std::vector<uint32_t> toks;
+    uint64_t out_len = 0, last_end = 0;
+    uint32_t bf = 0;
+    const uint32_t st = decode_blocks(in, 0, ~0ull, limit_bits, tab,
+                                      [&](uint32_t t) {
+                                        toks.push_back(t);
+                                        return true;
+                                      },
+                                      out_len, last_end, bf);
+    std::vector<uint8_t> got;
+    expand(toks, got);
+    if (st != kDecOk || got != want || out_len != want.size()) {
+      fprintf(stderr, "%s: serial decode differs (status %u, %zu vs %zu bytes)\n", argv[a], st, got.size(), want.size());
+      ++failures;
+      continue;
+    }
+    // (b) as the device: starts, independent decodes, place + resolve
+    std::vector<uint64_t> starts{0};
+    for (uint64_t c = chunk; c < nbytes; c += chunk) {
+      for (uint64_t p = c * 8; p < std::min<uint64_t>((c + chunk) * 8, limit_bits); ++p) {
+        uint64_t q = p;
+        if (block_header_ok(in, q)) {
+          starts.push_back(p);
+          break;
+        }
+      }
+    }
+    const size_t found = starts.size();
+    size_t dropped = 0;
+    std::vector<std::vector<uint32_t>> part;
+    std::vector<uint64_t> part_len;
+    for (;;) {  // drop the starts a lane overran, until every lane lands
+      part.assign(starts.size(), {});
+      part_len.assign(starts.size(), 0);
+      bool again = false;
+      for (size_t b = 0; b < starts.size() && !again; ++b) {
+        const uint64_t end = b + 1 < starts.size() ? starts[b + 1] : ~0ull;
+        uint64_t ol, le;
+        uint32_t fin;
+        const uint32_t r = decode_blocks(in, starts[b], end, limit_bits, tab,
+                                         [&](uint32_t t) {
+                                           part[b].push_back(t);
+                                           return true;
+                                         },
+                                         ol, le, fin);
+        part_len[b] = ol;
+        if (r == kDecOverrun) {
+          starts.erase(starts.begin() + (long)b + 1);
+          ++dropped;
+          again = true;
+        } else if (r != kDecOk) {
+          fprintf(stderr, "%s: lane %zu status %u\n", argv[a], b, r);
+          ++failures;
+          starts.clear();
+          break;
+        }
+      }
+      if (!again) break;
+    }
+    if (starts.empty()) continue;
+    // place: every byte a literal (bit 31) or a pointer to an earlier byte
+    std::vector<uint32_t> val;
+    for (size_t b = 0; b < part.size(); ++b)
+      for (uint32_t t : part[b]) {
+        if (!tok_is_match(t)) {
+          val.push_back(0x80000000u | t);
+        } else {
+          const uint32_t len = tok_len(t), dist = tok_dist(t);
+          const size_t at = val.size();
+          for (uint32_t i = 0; i < len; ++i) val.push_back((uint32_t)(at + i - dist));
+        }
+      }
+    std::vector<uint8_t> got2(val.size());
+    size_t max_chain = 0;
+    for (size_t i = 0; i < val.size(); ++i) {
+      uint32_t v = val[i];
+      size_t chain = 0;
+      while (!(v >> 31)) {
+        v = val[v];
+        ++chain;
+      }
+      max_chain = std::max(max_chain, chain);
+      got2[i] = (uint8_t)v;
+    }
+    if (got2 != want) {
+      fprintf(stderr, "%s: chunked decode differs\n", argv[a]);
+      ++failures;
+      continue;
+    }
+    printf("{\"file\": \"%s\", \"bytes\": %zu, \"gz_bytes\": %zu, \"starts_found\": %zu, \"starts_dropped\": %zu, "
+           "\"lanes\": %zu, \"tokens\": %zu, \"max_chain\": %zu}\n",
+           argv[a], want.size(), gz.size(), found, dropped, starts.size(), toks.size(), max_chain);
+  }
+  if (failures) {
+    fprintf(stderr, "%d failure(s)\n", failures);
+    return 1;
+  }
+  return 0;
+}

@@ -1,0 +1,159 @@
+"""The device gzip inflate (galah_amd/csrc/inflate.hip, inflate_core.hpp;
+GALAHGPU_INFLATE=device): gzip FASTA goes to the GPU compressed and is
+inflated there.
+
+CPU: the DEFLATE core (the bit-level decoding the kernels run) decodes every
+stream both serially and as the device does -- block starts searched every
+`chunk` bytes, one independent decode per start, back-references placed as
+pointers and followed -- and both equal zlib, for the reference's test
+genomes and for streams of every block type and zlib strategy.
+
+GPU: sketches and pairs with the device inflate equal the host path and the
+committed golden table; the cases it hands back to the host (several gzip
+members, FASTQ, a corrupt stream) give the host path's result or error and
+are counted."""
+import gzip
+import json
+import os
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+import galah_amd as ga
+import oracle
+from conftest import GOLD_DATA, ROOT
+
+BIN = os.path.join(ROOT, "tests", "cpp", "build", "test_inflate_core")
+
+
+def golden_gz():
+    out = []
+    for d, _, fs in os.walk(GOLD_DATA):
+        out += [os.path.join(d, f) for f in sorted(fs) if f.endswith(".gz")]
+    return sorted(out)
+
+
+def synthetic_streams(tmp):
+    rng = np.random.default_rng(8)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    seq = acgt[rng.integers(0, 4, 400000)].tobytes()
+    fa = b"".join(b">rec%d header text\n" % i + b"\n".join(seq[j:j + 60] for j in range(i * 20000, (i + 1) * 20000, 60))
+                  + b"\n" for i in range(20))
+    paths = []
+
+    def put(name, data, level=6, strategy=zlib.Z_DEFAULT_STRATEGY):
+        c = zlib.compressobj(level, zlib.DEFLATED, 31, 8, strategy)
+        p = os.path.join(tmp, name)
+        with open(p, "wb") as f:
+            f.write(c.compress(data) + c.flush())
+        paths.append(p)
+
+    for lvl in (0, 1, 6, 9):
+        put("l%d.fa.gz" % lvl, fa, lvl)
+    for name, strat in (("huff", zlib.Z_HUFFMAN_ONLY), ("rle", zlib.Z_RLE), ("fixed", zlib.Z_FIXED)):
+        put(name + ".fa.gz", fa, 6, strat)
+    put("nrun.fa.gz", fa.replace(b"ACGTA", b"NNNNNNNNNNNNNN"))
+    put("tiny.fa.gz", b">x\nACGT\n")
+    put("empty.gz", b"")
+    put("binary.gz", rng.integers(0, 256, 200000, dtype=np.uint8).tobytes())
+    return paths
+
+
+@pytest.fixture(scope="module")
+def core_binary():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")])
+    return BIN
+
+
+@pytest.mark.parametrize("chunk", [4096, 300])
+def test_core_chunked_decode_equals_zlib(core_binary, tmp_path, chunk):
+    paths = golden_gz() + synthetic_streams(str(tmp_path))
+    r = subprocess.run([core_binary, "--chunk", str(chunk)] + paths, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rows = [json.loads(x) for x in r.stdout.splitlines()]
+    assert len(rows) == len(paths)
+    # the search finds block starts in the multi-block streams
+    big = [x for x in rows if x["file"].endswith("l6.fa.gz") or "abisko4" in x["file"]]
+    assert big and all(x["starts_found"] > 1 for x in big)
+
+
+# ---------------------------------------------------------------------------
+def sketch_files(paths, monkeypatch, inflate, k=21, s=1000):
+    monkeypatch.setenv("GALAHGPU_INFLATE", inflate)
+    with ga.Context(k=k, sketch_size=s) as ctx:
+        sk, lens, _ = ctx.sketch_files([str(p) for p in paths])
+        fb = ctx.fallbacks()
+    return sk, lens, fb
+
+
+@pytest.mark.gpu
+def test_device_inflate_golden(golden, monkeypatch):
+    sk, lens, fb = sketch_files(golden["paths"], monkeypatch, "device")
+    assert fb["inflate_host"] == 0
+    assert (lens == golden["lens"]).all()
+    for g in range(len(lens)):
+        assert (sk[g][:lens[g]] == golden["sketches"][g][:lens[g]]).all(), golden["names"][g]
+    monkeypatch.setenv("GALAHGPU_INFLATE", "device")
+    thr = ga.parse_percentage(90)
+    with ga.Context(k=21, sketch_size=1000) as ctx:
+        pairs, ani = ctx.precluster_files(golden["paths"], thr)
+        assert ctx.fallbacks()["inflate_host"] == 0
+    exp = [(i, j, c, t) for (i, j, c, t, a) in golden["pairs"] if oracle.ani(c, t) >= np.float64(np.float32(thr))]
+    assert [(int(r["i"]), int(r["j"]), int(r["common"]), int(r["total"])) for r in pairs] == exp
+
+
+@pytest.mark.gpu
+def test_device_inflate_streams_and_handbacks(tmp_path, monkeypatch):
+    """Every block type and zlib strategy, several gzip members, FASTQ, plain
+    FASTA beside gzip files, many files in one batch: the host path's
+    sketches; the members / FASTQ batches are handed back and counted."""
+    rng = np.random.default_rng(3)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    paths = [p for p in synthetic_streams(str(tmp_path)) if not p.endswith(("empty.gz", "binary.gz"))]
+    for i in range(60):  # many small genomes in one batch
+        seq = acgt[rng.integers(0, 4, int(rng.integers(20000, 300000)))].tobytes()
+        p = tmp_path / ("g%02d.fna.gz" % i)
+        p.write_bytes(gzip.compress(b">g%d\n" % i + b"\n".join(seq[j:j + 80] for j in range(0, len(seq), 80)) + b"\n"))
+        paths.append(str(p))
+    plain = tmp_path / "plain.fa"
+    plain.write_bytes(b">p\n" + acgt[rng.integers(0, 4, 50000)].tobytes() + b"\n")
+    paths.append(str(plain))
+    hsk, hl, _ = sketch_files(paths, monkeypatch, "host")
+    dsk, dl, fb = sketch_files(paths, monkeypatch, "device")
+    assert fb["inflate_host"] == 0
+    assert (dl == hl).all() and all((dsk[g][:dl[g]] == hsk[g][:hl[g]]).all() for g in range(len(paths)))
+    # several members (bgzip-like) and FASTQ: the batch goes back to the host
+    seq = acgt[rng.integers(0, 4, 100000)].tobytes()
+    multi = tmp_path / "multi.fa.gz"
+    multi.write_bytes(gzip.compress(b">m\n" + seq[:50000]) + gzip.compress(seq[50000:] + b"\n"))
+    fq = tmp_path / "reads.fq.gz"
+    fq.write_bytes(gzip.compress(b"@r1\n" + seq[:5000] + b"\n+\n" + b"I" * 5000 + b"\n"))
+    for extra in (multi, fq):
+        ps = paths[:3] + [str(extra)]
+        hsk, hl, _ = sketch_files(ps, monkeypatch, "host")
+        dsk, dl, fb = sketch_files(ps, monkeypatch, "device")
+        assert fb["inflate_host"] == 1, extra
+        assert (dl == hl).all() and all((dsk[g][:dl[g]] == hsk[g][:hl[g]]).all() for g in range(len(ps)))
+
+
+@pytest.mark.gpu
+def test_device_inflate_corrupt_and_empty_fail_as_host(tmp_path, monkeypatch):
+    rng = np.random.default_rng(4)
+    seq = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 200000)].tobytes()
+    good = gzip.compress(b">c\n" + seq + b"\n")
+    bad = bytearray(good)
+    bad[len(bad) // 2] ^= 0x55  # inside the deflate data: a CRC or stream error
+    cases = {"corrupt.fa.gz": bytes(bad), "empty.fa.gz": gzip.compress(b""), "truncated.fa.gz": good[:len(good) // 2]}
+    for name, data in cases.items():
+        p = tmp_path / name
+        p.write_bytes(data)
+        errs = {}
+        for mode in ("host", "device"):
+            monkeypatch.setenv("GALAHGPU_INFLATE", mode)
+            with ga.Context(k=21, sketch_size=1000) as ctx:
+                with pytest.raises(ga.GalahGpuError) as e:
+                    ctx.sketch_files([str(p)])
+                errs[mode] = (e.value.status, str(e.value))
+        assert errs["device"] == errs["host"], name
