@@ -11,6 +11,8 @@
 // (libdeflate, which also reports a corrupt file).  So the device path
 // changes no result, only where the bytes are inflated.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "context.hpp"
@@ -47,6 +49,18 @@ bool gzip_member(const uint8_t* buf, size_t n, size_t* data_off, size_t* data_le
 }
 
 namespace {
+// GALAHGPU_INFLATE_DEBUG=1: why a batch went back to the host, on stderr
+bool inflate_debug() {
+  static const bool on = [] {
+    const char* e = getenv("GALAHGPU_INFLATE_DEBUG");
+    return e && *e == '1';
+  }();
+  return on;
+}
+gg_status hand_back(const char* why, uint32_t f) {
+  if (inflate_debug()) fprintf(stderr, "[inflate] batch handed back to the host: %s (file %u of the batch)\n", why, f);
+  return GG_OK;
+}
 constexpr uint32_t kChunkBytes = 4096;  // search granularity: a zlib -6 block of FASTA is ~25-30 KB
 constexpr int kMaxRelaunch = 8;         // decode passes that may drop wrong starts before giving up
 }  // namespace
@@ -119,7 +133,7 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   uint32_t *d_lfile = nullptr, *d_tok = nullptr;
   uint64_t *d_toff = nullptr, *d_res = nullptr;
   for (int pass = 0;; ++pass) {
-    if (pass >= kMaxRelaunch) return GG_OK;  // (ok = false: the host decodes the batch)
+    if (pass >= kMaxRelaunch) return hand_back("block starts did not chain", 0);  // (ok = false)
     lane_file.clear();
     lane_start.clear();
     lane_end.clear();
@@ -130,9 +144,9 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
       for (size_t i = 0; i < starts[f].size(); ++i) {
         const uint64_t s0 = starts[f][i];
         const uint64_t e = i + 1 < starts[f].size() ? starts[f][i + 1] : ~0ull;
-        // a token takes >= 1 bit; FASTA averages ~14 bits per token at zlib -6:
-        // half the bits bound every realistic block (a full lane reports it)
-        const uint64_t cap = ((e == ~0ull ? fbits[f] : e) - s0) / 2 + 64;
+        // every symbol takes >= 1 bit: one token per bit bounds every lane
+        // (literal-heavy DNA blocks reach ~0.5 tokens per bit)
+        const uint64_t cap = ((e == ~0ull ? fbits[f] : e) - s0) + 64;
         lane_file.push_back(f);
         lane_start.push_back(s0);
         lane_end.push_back(e);
@@ -200,7 +214,10 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
         }
         keep.push_back(starts[f][i]);
         if (status[l] == inflate::kDecOverrun && i + 1 < starts[f].size()) drop_next = true;
-        else if (status[l] != inflate::kDecOk) return GG_OK;  // malformed / full / a second member: host path
+        else if (status[l] != inflate::kDecOk)  // malformed / full / a second member: host path
+          return hand_back(status[l] == inflate::kDecFull ? "token capacity"
+                           : status[l] == inflate::kDecFinalEarly ? "stream ended early (several members?)"
+                                                                  : "malformed stream", f);
       }
       starts[f].swap(keep);
     }
@@ -220,16 +237,16 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
         lane_out[l] = flen[f];
         flen[f] += out_len[l];
         if (i + 1 == starts[f].size()) {
-          if (!bfin[l] || (last_end[l] + 7) / 8 != files[f].data_len) return GG_OK;
+          if (!bfin[l] || (last_end[l] + 7) / 8 != files[f].data_len) return hand_back("not one member", f);
         }
       }
-      if ((uint32_t)flen[f] != files[f].isize) return GG_OK;
+      if ((uint32_t)flen[f] != files[f].isize) return hand_back("ISIZE", f);
     }
   }
   foff.assign(nf + 1, 0);
   for (uint32_t f = 0; f < nf; ++f) foff[f + 1] = foff[f] + (flen[f] + 15) / 16 * 16;
   const uint64_t text_len = foff[nf];
-  if (text_len >= (1ull << 31)) return GG_OK;  // (the pointers of inflate_resolve_kernel are 31-bit)
+  if (text_len >= (1ull << 31)) return hand_back("batch text over 2 GiB", 0);  // (31-bit resolve pointers)
   for (size_t l = 0; l < lane_out.size(); ++l) lane_out[l] += foff[lane_file[l]];
   uint32_t *d_val, *d_flags, *d_crc;
   uint64_t *d_lout, *d_ftext, *d_flen;
@@ -270,10 +287,10 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   std::vector<uint32_t> chk(2 * (size_t)nf + 1);
   GG_HIP(m, hipMemcpyAsync(chk.data(), d_flags, chk.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   GG_HIP(m, hipStreamSynchronize(st));
-  if (chk[0]) return GG_OK;
+  if (chk[0]) return hand_back(chk[0] & 1 ? "distance before the file start" : "pointer chain", 0);
   for (uint32_t f = 0; f < nf; ++f)
     if (files[f].gz && (chk[1 + f] != files[f].crc || chk[1 + nf + f] != '>'))  // (FASTQ, malformed: the host path)
-      return GG_OK;
+      return hand_back(chk[1 + f] != files[f].crc ? "CRC-32" : "not FASTA", f);
   *ok = true;
   return GG_OK;
 }

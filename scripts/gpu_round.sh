@@ -35,6 +35,14 @@ for st in $STAGES; do
       rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     hostinfo)  # the host's CPUs as this process sees them (nproc, affinity, cgroup quota)
       run hostinfo 60 python3 -u scripts/host_cpus.py || exit $? ;;
+    inflate)  # device gzip inflate tests (GALAHGPU_INFLATE=device)
+      run gpu_tests_inflate 400 python3 -u -m pytest tests/test_inflate.py -m gpu -v --timeout 300 --timeout-method thread
+      rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
+    inflate_probe)  # device vs host gzip inflate on C2-like files (reasons for a hand-back on stderr)
+      GALAHGPU_INFLATE_DEBUG=1 run inflate_probe 600 python3 -u scripts/inflate_probe.py ${PROBE_FILES:-200} 3 || exit $? ;;
+    inflate_prof)  # kernel trace + stats of the device inflate probe
+      PROBE_MODES=device run inflate_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o inflate -- \
+        python3 -u scripts/inflate_probe.py ${PROBE_FILES:-200} 2 || exit $? ;;
     smoke)
       run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)       bench bench_c3 600 --steps 20 --warmup 5 ;;
