@@ -259,6 +259,8 @@ struct InflateDecode {
   uint32_t* tok;               // tokens of lane l at tok_off[l] (a multiple of 4), at most tok_cap[l]
   const uint64_t* tok_off;
   const uint64_t* tok_cap;
+  uint32_t* scr;               // speculative sub-span tokens of lane l at scr_off[l] (inflate::decode_scratch)
+  const uint64_t* scr_off;
   uint32_t* status;            // [n_lanes] inflate::DecodeStatus
   uint64_t* n_tok;             // [n_lanes]
   uint64_t* out_len;           // [n_lanes] bytes the lane's tokens stand for
@@ -288,10 +290,13 @@ struct InflateFile {
 bool gzip_member(const uint8_t* buf, size_t n, size_t* data_off, size_t* data_len, uint32_t* isize, uint32_t* crc);
 hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st);
 hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st);
-// place + resolve (text[0, text_len), val pre-set to literal '\n') + CRC-32 per file
+// expand + resolve (text[0, text_len), val pre-set to literal '\n') + CRC-32 per file
+// (file f's 4 KB segments are seg_first[f] .. seg_first[f + 1] - 1; crc
+// receives n_files CRCs, then each file's first byte)
+constexpr uint32_t kInflateCrcSeg = 4096;
 hipError_t launch_inflate_place(const InflatePlace& a, uint64_t text_len, uint8_t* text, uint32_t n_files,
-                                const uint64_t* file_text, const uint64_t* file_len, uint32_t* crc,
-                                hipStream_t st);
+                                const uint64_t* file_text, const uint64_t* file_len, const uint32_t* seg_first,
+                                uint32_t n_segs, uint32_t* seg_crc, uint32_t* crc, hipStream_t st);
 
 struct IndexBuild {
   const uint64_t* sketches;

@@ -10,19 +10,21 @@
 //   inflate_search_kernel   one wave per ~4 KB chunk of compressed data: the
 //                           first bit position where a dynamic block header
 //                           parses (64 positions per step, one per lane)
-//   inflate_decode_kernel   one lane per found start: Huffman-decode into
-//                           tokens until landing on the next start (its own
-//                           tables in LDS, 4 tokens per 16-byte store)
-//   inflate_place_kernel    one workgroup per lane: token output offsets by
-//                           a block scan, every output byte written as a
-//                           literal or a pointer to the earlier byte it
-//                           copies (the 32 KB window is never needed)
-//   inflate_resolve_kernel  pointers followed to their literals, 16 bytes per
-//                           thread, each resolved byte written back (later
-//                           chains through it stop there)
-//   inflate_crc_kernel      one workgroup per file: CRC-32 of the text
-//                           (segments, folded with x^(8n) mod P), checked with
-//                           ISIZE against the gzip trailer by the host
+//   inflate_decode_kernel   one wave per found start: each block's header
+//                           by lane 0, its body split into 64 sub-spans
+//                           decoded at once and chained by resynchronisation
+//                           (inflate_core.hpp decode_span) into tokens, until
+//                           landing on the next start
+//   inflate_expand_kernel   one workgroup per segment, in order: token output
+//                           offsets by a block scan, the bytes of each step
+//                           built in LDS (back-references inside the segment
+//                           copied, those before it left as pointers)
+//   inflate_resolve_kernel  pointers (into earlier segments only) followed to
+//                           their literals, 16 bytes per thread
+//   inflate_crc_seg_kernel  CRC-32 of every 4 KB of text, one thread each
+//   inflate_crc_fold_kernel per file its segments' CRCs folded with x^(8n)
+//                           mod P; checked with ISIZE against the gzip
+//                           trailer by the host
 #include "device_util.hpp"
 #include "gg_internal.hpp"
 #include "inflate_core.hpp"
@@ -32,29 +34,51 @@ namespace {
 
 using namespace inflate;
 
-constexpr int kSearchWaves = 4;  // chunks per search workgroup (one wave each)
+constexpr int kSearchWaves = 4;       // chunks per search workgroup (one wave each)
+constexpr uint32_t kSearchStep = 1024;  // positions filtered before the candidates are checked
 
+// One wave per chunk: positions in steps of kSearchStep, 64 at a time
+// through the register-only filter (block_header_quick); the survivors, in
+// order, in LDS; then checked fully one per lane (block_header_ok).  The
+// first that passes is the chunk's start.
 __global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(InflateSearch a) {
-  const uint32_t c = blockIdx.x * kSearchWaves + (threadIdx.x >> 6);
+  __shared__ uint32_t cand[kSearchWaves][kSearchStep];
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t c = blockIdx.x * kSearchWaves + wv;
   const uint32_t lane = threadIdx.x & 63u;
   if (c >= a.n_chunks) return;
+  uint32_t* cw = cand[wv];
   const uint32_t f = a.chunk_file[c];
   const Bits in{a.in + a.file_word[f]};
   const uint64_t b0 = a.chunk_bit0[c];
   const uint64_t b1 = min(b0 + (uint64_t)a.chunk_bits, a.file_bits[f]);
+  const uint64_t lt = (1ull << lane) - 1ull;
   uint64_t found = ~0ull;
-  for (uint64_t p0 = b0; p0 < b1; p0 += 64) {  // (uniform per wave)
-    const uint64_t p = p0 + lane;
-    bool ok = false;
-    if (p < b1) {
-      uint64_t q = p;
-      ok = block_header_ok(in, q);
+  for (uint64_t s0 = b0; s0 < b1 && found == ~0ull; s0 += kSearchStep) {  // (uniform per wave)
+    uint32_t nc = 0;
+    for (uint32_t r = 0; r < kSearchStep; r += 64) {
+      const uint64_t p = s0 + r + lane;
+      const bool pass = p < b1 && block_header_quick(in, p);
+      const uint64_t m = __ballot(pass);
+      if (pass) cw[nc + (uint32_t)__popcll(m & lt)] = (uint32_t)(p - s0);
+      nc += (uint32_t)__popcll(m);
     }
-    const uint64_t m = __ballot(ok);
-    if (m) {
-      found = p0 + (uint64_t)(__ffsll((unsigned long long)m) - 1);
-      break;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t k0 = 0; k0 < nc; k0 += 64) {
+      bool ok = false;
+      uint64_t p = 0;
+      if (k0 + lane < nc) {
+        p = s0 + cw[k0 + lane];
+        uint64_t q = p;
+        ok = block_header_ok(in, q);
+      }
+      const uint64_t m = __ballot(ok);
+      if (m) {
+        found = s0 + cw[k0 + (uint32_t)__ffsll((unsigned long long)m) - 1u];
+        break;
+      }
     }
+    __builtin_amdgcn_wave_barrier();
   }
   if (lane == 0) a.start[c] = found;
 }
@@ -70,93 +94,359 @@ struct LdsStore {
   __device__ uint8_t& dsym(int i) { return ds[i]; }
 };
 
-constexpr int kDecodeLanes = 64;  // one wave per workgroup: its lanes' tables fill ~47 KB of LDS
+constexpr uint32_t kSpanLanes = 64;  // one wave per segment, one sub-span per lane
 
-__global__ __launch_bounds__(kDecodeLanes) void inflate_decode_kernel(InflateDecode a) {
-  __shared__ int32_t lb[kDecodeLanes][kMaxBits + 1], db[kDecodeLanes][kMaxBits + 1];
-  __shared__ uint16_t ls[kDecodeLanes][kLitSyms];
-  __shared__ uint8_t ds[kDecodeLanes][kDistSyms];
-  const uint32_t t = threadIdx.x;
-  const uint32_t lane = blockIdx.x * kDecodeLanes + t;
-  if (lane >= a.n_lanes) return;
-  LaneTables<LdsStore> tab;
-  tab.s = LdsStore{lb[t], db[t], ls[t], ds[t]};
-  const uint32_t f = a.lane_file[lane];
-  const Bits in{a.in + a.file_word[f]};
-  uint32_t* out = a.tok + a.tok_off[lane];
-  const uint64_t cap = a.tok_cap[lane];
-  uint64_t n = 0;
-  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;  // the last 4 tokens (a 16-byte store every 4)
-  auto emit = [&](uint32_t tk) -> bool {
-    if (n >= cap) return false;
+// A lane's tokens to its scratch area: the last 4 held for one 16-byte store
+// (the area is 16-byte aligned).
+struct TokSink {
+  uint32_t* p;
+  uint32_t cap;
+  uint32_t k = 0;
+  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  __device__ bool operator()(uint32_t tk) {
+    if (k >= cap) return false;
     w0 = w1;
     w1 = w2;
     w2 = w3;
     w3 = tk;
-    ++n;
-    if ((n & 3u) == 0) *(uint4*)(out + n - 4) = make_uint4(w0, w1, w2, w3);
+    ++k;
+    if ((k & 3u) == 0) *(uint4*)(p + k - 4) = make_uint4(w0, w1, w2, w3);
     return true;
-  };
-  uint64_t out_len = 0, last_end = 0;
-  uint32_t fin = 0;
-  uint32_t st = decode_blocks(in, a.lane_start[lane], a.lane_end[lane], a.file_bits[f], tab, emit, out_len, last_end,
-                              fin);
-  if (st == kDecOk && n >= cap && cap) st = kDecOk;  // (exactly full is fine)
-  const uint32_t r = (uint32_t)(n & 3u);  // tokens not yet stored: the last r
-  if (r >= 1) out[n - 1] = w3;
-  if (r >= 2) out[n - 2] = w2;
-  if (r >= 3) out[n - 3] = w1;
-  a.status[lane] = st;
-  a.n_tok[lane] = n;
-  a.out_len[lane] = out_len;
-  a.last_end[lane] = last_end;
-  a.bfinal[lane] = fin;
+  }
+  __device__ void flush() {
+    const uint32_t r = k & 3u;
+    if (r >= 1) p[k - 1] = w3;
+    if (r >= 2) p[k - 2] = w2;
+    if (r >= 3) p[k - 3] = w1;
+  }
+};
+
+// One wave per segment (a found block start up to the next one).  Per block:
+// lane 0 reads the header into the wave's LDS tables; the body is split into
+// up to 64 sub-spans decoded at once, each lane from the start of its span
+// (usually inside a symbol) into its own scratch, recording checkpoints
+// (inflate_core.hpp decode_span).  A lane whose first checkpoint is not the
+// symbol start the lane before ended on decodes again from there until one
+// of its checkpoints agrees with the first decode.  The right spans up to
+// the one that decoded end-of-block are the block; their tokens are copied
+// to the segment's tokens.
+__global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecode a) {
+  __shared__ int32_t lb[kMaxBits + 1], db[kMaxBits + 1];
+  __shared__ uint32_t slim[2][kMaxBits + 1];
+  __shared__ uint16_t ls[kLitSyms];
+  __shared__ uint8_t ds[kDistSyms];
+  __shared__ uint64_t sE[kSpanLanes];
+  __shared__ uint32_t sSt[kSpanLanes];
+  __shared__ uint64_t s_body0, s_stored;
+  __shared__ int32_t s_bt;
+  __shared__ uint32_t s_bfinal;
+  const uint32_t j = threadIdx.x;
+  const uint32_t seg = blockIdx.x;
+  if (seg >= a.n_lanes) return;
+  LaneTables<LdsStore> tab;
+  tab.s = LdsStore{lb, db, ls, ds};
+  const uint32_t f = a.lane_file[seg];
+  const Bits in{a.in + a.file_word[f]};
+  const uint64_t limit = a.file_bits[f];
+  const uint64_t end = a.lane_end[seg];  // ~0: the file's last segment (ends with the BFINAL block)
+  const bool final_seg = end == ~0ull;
+  uint32_t* out = a.tok + a.tok_off[seg];
+  const uint64_t cap = a.tok_cap[seg];
+  uint32_t* scr_all = a.scr + a.scr_off[seg];
+  uint64_t pos = a.lane_start[seg];  // (uniform)
+  uint64_t n_out = 0, out_bytes = 0;
+  uint32_t status = kDecOk, fin = 0;
+  for (;;) {
+    if (pos == end) {
+      status = kDecOk;
+      break;
+    }
+    if (pos > end || pos >= limit) {
+      status = kDecOverrun;
+      break;
+    }
+    if (j == 0) {
+      uint64_t q = pos;
+      uint32_t bf = 0, stl = 0;
+      const int bt = read_block_header(in, q, tab, bf, stl);
+      s_bt = bt;
+      s_bfinal = bf;
+      s_body0 = q;
+      s_stored = stl;
+#pragma unroll
+      for (int l = 0; l <= kMaxBits; ++l) {
+        slim[0][l] = tab.llim[l];
+        slim[1][l] = tab.dlim[l];
+      }
+    }
+    __syncthreads();
+    const int bt = s_bt;
+    const uint32_t bfinal = s_bfinal;
+    const uint64_t body0 = s_body0;
+    if (bt < 0) {
+      status = kDecBad;
+      pos = body0;
+      break;
+    }
+    if (bt == 0) {  // stored: its bytes as literal tokens
+      const uint64_t stl = s_stored;
+      if (body0 + 8 * stl > limit) {
+        status = kDecBad;
+        break;
+      }
+      if (n_out + stl > cap) {
+        status = kDecFull;
+        break;
+      }
+      const uint8_t* src = (const uint8_t*)in.w + body0 / 8;
+      for (uint64_t i = j; i < stl; i += kSpanLanes) out[n_out + i] = src[i];
+      n_out += stl;
+      out_bytes += stl;
+      pos = body0 + 8 * stl;
+    } else {
+#pragma unroll
+      for (int l = 0; l <= kMaxBits; ++l) {
+        tab.llim[l] = slim[0][l];
+        tab.dlim[l] = slim[1][l];
+      }
+      const uint64_t span_end = final_seg ? limit : end;
+      uint64_t L;
+      uint32_t nsub;
+      span_layout(body0, span_end, kSpanLanes, L, nsub);
+      const bool act = j < nsub;
+      const uint64_t S = body0 + j * L;
+      const uint64_t R = j + 1 == nsub ? span_end : S + L;
+      const uint64_t capL = span_cap(L), ncks = span_cks(L);
+      uint32_t* A = scr_all + j * span_words(L);  // first decode
+      uint32_t* B = A + capL;                     // second decode
+      uint64_t* ck = (uint64_t*)(B + capL);       // the first decode's checkpoints
+      // the first decode, from S
+      uint32_t na = 0, nck = 0, sa = kSpanRange;
+      uint64_t ba = 0, Ea = S;
+      if (act) {
+        TokSink sink{A, (uint32_t)capL};
+        sa = decode_span(in, S, S, R, tab, sink,
+                         [&](uint32_t k, uint64_t c) {
+                           if (k < ncks) {
+                             ck[k] = c;
+                             nck = k + 1;
+                           }
+                           return true;
+                         },
+                         na, ba, Ea);
+        sink.flush();
+      }
+      uint64_t first = act && nck ? S + ck_off(ck[0]) : ~0ull;
+      bool redone = false;
+      int synced = -1;
+      uint32_t nb = 0, sb = kSpanRange;
+      uint64_t bb = 0, Eb = 0;
+      uint32_t c_end = 0;
+      bool overrun = false;
+      for (;;) {
+        const uint64_t E = redone && synced < 0 ? Eb : Ea;
+        const uint32_t st = redone && synced < 0 ? sb : sa;
+        sE[j] = E;
+        sSt[j] = st;
+        __syncthreads();
+        const uint64_t eprev = j ? sE[j - 1] : 0;
+        const uint32_t sprev = j ? sSt[j - 1] : kSpanRange;
+        const bool ok = act && (j == 0 || (sprev == kSpanRange && first == eprev));
+        const uint64_t okb = __ballot(ok), termb = __ballot(act && st != kSpanRange);
+        const uint64_t vmask = nsub >= 64 ? ~0ull : (1ull << nsub) - 1ull;
+        const uint64_t notok = ~okb & vmask;
+        const uint32_t c = notok ? (uint32_t)__ffsll((unsigned long long)notok) - 1u : 64u;
+        const uint32_t t = termb ? (uint32_t)__ffsll((unsigned long long)termb) - 1u : 64u;
+        if (t < c) {  // the chain of right spans ends with span t's end-of-block (or bad code)
+          c_end = t;
+          break;
+        }
+        if (c >= nsub) {  // every span right, none ended the block: it runs past the segment
+          overrun = true;
+          c_end = nsub - 1;
+          break;
+        }
+        __syncthreads();  // (sE / sSt read before the next round writes them)
+        if (act && j >= c && !ok && sprev == kSpanRange) {
+          // the second decode, from the true start, until a checkpoint agrees
+          redone = true;
+          synced = -1;
+          first = eprev;
+          TokSink sink{B, (uint32_t)capL};
+          sb = decode_span(in, eprev, S, R, tab, sink,
+                           [&](uint32_t k, uint64_t cc) {
+                             if (k < nck && ck_off(cc) == ck_off(ck[k])) {
+                               synced = (int)k;
+                               return false;
+                             }
+                             return true;
+                           },
+                           nb, bb, Eb);
+          sink.flush();
+        }
+      }
+      const uint64_t e_end = sE[c_end];
+      const uint32_t st_end = sSt[c_end];
+      if (overrun) {
+        status = kDecOverrun;
+        pos = e_end;
+        break;
+      }
+      if (st_end == kSpanBad) {
+        status = kDecBad;
+        pos = e_end;
+        break;
+      }
+      // this span's tokens: [p1, p1 + n1) then [p2, p2 + n2)
+      const uint32_t* p1 = A;
+      const uint32_t* p2 = A;
+      uint32_t n1 = 0, n2 = 0;
+      uint64_t vbytes = 0;
+      if (j <= c_end) {
+        if (!redone) {
+          const uint64_t c0 = ck[0];
+          p1 = A + ck_tok(c0);
+          n1 = na - ck_tok(c0);
+          vbytes = ba - ck_bytes(c0);
+        } else {
+          p1 = B;
+          n1 = nb;
+          vbytes = bb;
+          if (synced >= 0) {
+            const uint64_t ck_s = ck[synced];
+            p2 = A + ck_tok(ck_s);
+            n2 = na - ck_tok(ck_s);
+            vbytes += ba - ck_bytes(ck_s);
+          }
+        }
+      }
+      const uint32_t valid = n1 + n2;
+      uint32_t incl = valid;
+      uint64_t tb = vbytes;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (j >= (uint32_t)o) incl += y;
+        tb += __shfl_xor(tb, o);
+      }
+      const uint32_t total = __shfl(incl, 63);
+      if (n_out + total > cap) {
+        status = kDecFull;
+        break;
+      }
+      uint32_t* dst = out + n_out + (incl - valid);
+      for (uint32_t i = 0; i < n1; ++i) dst[i] = p1[i];
+      for (uint32_t i = 0; i < n2; ++i) dst[n1 + i] = p2[i];
+      n_out += total;
+      out_bytes += tb;
+      pos = e_end;
+      __syncthreads();  // (the LDS tables and spans are rewritten for the next block)
+    }
+    if (bfinal) {
+      fin = 1;
+      status = final_seg ? kDecOk : kDecFinalEarly;
+      break;
+    }
+  }
+  if (j == 0) {
+    a.status[seg] = status;
+    a.n_tok[seg] = n_out;
+    a.out_len[seg] = out_bytes;
+    a.last_end[seg] = pos;
+    a.bfinal[seg] = fin;
+  }
 }
 
-// One workgroup per decode lane: tiles of 256 tokens, each token's output
-// offset by a block scan of the token lengths, literals written as
-// 0x80000000 | byte and match bytes as the batch position they copy.
-constexpr int kPlaceThreads = 256;
-__global__ __launch_bounds__(kPlaceThreads) void inflate_place_kernel(InflatePlace a) {
-  __shared__ uint32_t wsum[kPlaceThreads / 64];
-  __shared__ uint32_t tile_base;
-  const uint32_t lane = blockIdx.x;
+// One workgroup per segment, its output written in order in steps of up to
+// 256 tokens / kExpandBytes bytes: every byte of a step staged in LDS as a
+// literal (0x80000000 | byte), a position before the segment (a pointer the
+// resolve pass follows: the segment before is not expanded yet), the value of
+// an earlier step's byte (read back from val: a literal or such a pointer),
+// or kIntra | the step byte it copies; kIntra pointers are then followed
+// inside the step by pointer jumping, and the step goes to val in one
+// coalesced pass.  So pointers left in val reach only into earlier segments
+// and the resolve chains are short.
+constexpr int kExpandThreads = 256;
+constexpr uint32_t kExpandBytes = 8192;
+constexpr uint32_t kIntra = 0x40000000u;  // (batch text < 2^30 bytes: pointers leave bit 30 clear)
+__global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflatePlace a) {
+  __shared__ uint32_t v[kExpandBytes];
+  __shared__ uint32_t s_take, s_bytes;
+  __shared__ uint32_t wsum[kExpandThreads / 64];
+  const uint32_t seg = blockIdx.x;
   const uint32_t tid = threadIdx.x, ln = tid & 63u, wave = tid >> 6;
-  const uint32_t* tok = a.tok + a.tok_off[lane];
-  const uint64_t n = a.n_tok[lane];
-  const uint64_t text0 = a.file_text[a.lane_file[lane]];  // the file's first text position
-  uint64_t base = a.lane_out[lane];
+  const uint32_t* tok = a.tok + a.tok_off[seg];
+  const uint64_t n = a.n_tok[seg];
+  const uint64_t o0 = a.lane_out[seg];                     // the segment's first text position
+  const uint64_t f0 = a.file_text[a.lane_file[seg]];      // its file's
+  uint64_t base = o0;
   bool bad = false;
-  for (uint64_t t0 = 0; t0 < n; t0 += kPlaceThreads) {
+  for (uint64_t t0 = 0; t0 < n;) {
     const uint64_t ti = t0 + tid;
     const uint32_t tk = ti < n ? tok[ti] : 0u;
     const uint32_t len = ti < n ? tok_len(tk) : 0u;
     uint32_t inc = len;
+#pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = __shfl_up(inc, o);
       if (ln >= (uint32_t)o) inc += y;
     }
     if (ln == 63) wsum[wave] = inc;
+    if (tid == 0) {
+      s_take = 0;
+      s_bytes = 0;
+    }
     __syncthreads();
-    uint32_t before = inc - len;
-    for (uint32_t w = 0; w < wave; ++w) before += wsum[w];
-    if (tid == kPlaceThreads - 1) tile_base = before + len;
-    const uint64_t pos = base + before;
-    if (ti < n) {
+    for (uint32_t w = 0; w < wave; ++w) inc += wsum[w];
+    const uint32_t before = inc - len;
+    const bool take = ti < n && inc <= kExpandBytes;  // (a prefix of the threads; thread 0 always)
+    const uint32_t c = (uint32_t)__popcll(__ballot(take));
+    const uint32_t last = __shfl(inc, c ? c - 1 : 0);  // this wave's bytes up to its last token taken
+    if (c && ln == 0) {
+      atomicAdd(&s_take, c);
+      atomicMax(&s_bytes, last);
+    }
+    if (take) {
       if (!tok_is_match(tk)) {
-        a.val[pos] = 0x80000000u | tk;
+        v[before] = 0x80000000u | tk;
       } else {
         const uint32_t dist = tok_dist(tk);
-        if (pos < text0 + dist) {
+        const uint64_t p = base + before;
+        if (p < f0 + dist) {
           bad = true;  // a distance before the file's first byte
+          for (uint32_t k = 0; k < len; ++k) v[before + k] = 0x80000000u | '\n';
         } else {
-          for (uint32_t j = 0; j < len; ++j) a.val[pos + j] = (uint32_t)(pos + j - dist);
+          const uint64_t src = p - dist;
+          for (uint32_t k = 0; k < len; ++k) {
+            const uint64_t s = src + k;
+            uint32_t x;
+            if (s >= base) x = kIntra | (uint32_t)(s - base);
+            else if (s < o0) x = (uint32_t)s;
+            else x = __hip_atomic_load(&a.val[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            v[before + k] = x;
+          }
         }
       }
     }
     __syncthreads();
-    base += tile_base;
+    const uint32_t nb = s_bytes, nt = s_take;
+    for (;;) {  // kIntra pointers followed inside the step (each points to an earlier byte)
+      bool more = false;
+      for (uint32_t i = tid; i < nb; i += kExpandThreads) {
+        const uint32_t x = v[i];
+        if ((x & 0xC0000000u) == kIntra) {
+          const uint32_t y = v[x & 0x3FFFFFFFu];
+          v[i] = y;
+          more |= (y & 0xC0000000u) == kIntra;
+        }
+      }
+      if (!__syncthreads_or(more)) break;
+    }
+    for (uint32_t i = tid; i < nb; i += kExpandThreads) a.val[base + i] = v[i];
+    __threadfence();
     __syncthreads();
+    base += nb;
+    t0 += nt;
   }
   if (bad) atomicOr(a.flags, 1u);
 }
@@ -217,22 +507,70 @@ __device__ uint32_t crc_x8n(uint64_t n, const uint32_t* __restrict__ x2k) {  // 
   return p;
 }
 
+// CRC-32 in two kernels: every kCrcSeg-byte segment of every file on its
+// own thread (slicing-by-8, tables in LDS, 16-byte loads), then per file the
+// segments folded in order, crc(A || B) = x^(8|B|) crc(A) ^ crc(B).
+constexpr uint32_t kCrcSeg = kInflateCrcSeg;
 constexpr int kCrcThreads = 256;
-constexpr uint64_t kCrcSeg = 16384;  // bytes per thread per round
-__global__ __launch_bounds__(kCrcThreads) void inflate_crc_kernel(const uint8_t* __restrict__ text,
-                                                                  const uint64_t* __restrict__ file_text,
-                                                                  const uint64_t* __restrict__ file_len,
-                                                                  uint32_t* __restrict__ crc_out) {
-  __shared__ uint32_t table[256];
-  __shared__ uint32_t x2k[64];
-  __shared__ uint32_t seg[kCrcThreads];
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < 256; i += kCrcThreads) {
+__global__ __launch_bounds__(kCrcThreads) void inflate_crc_seg_kernel(const uint8_t* __restrict__ text,
+                                                                      const uint64_t* __restrict__ file_text,
+                                                                      const uint64_t* __restrict__ file_len,
+                                                                      const uint32_t* __restrict__ seg_first,
+                                                                      uint32_t n_files, uint32_t n_segs,
+                                                                      uint32_t* __restrict__ seg_crc) {
+  __shared__ uint32_t T[8][256];
+  {
+    const uint32_t i = threadIdx.x;  // (kCrcThreads == 256: one table index per thread)
     uint32_t c = i;
     for (int k = 0; k < 8; ++k) c = c & 1 ? (c >> 1) ^ kCrcPoly : c >> 1;
-    table[i] = c;
+    T[0][i] = c;
   }
-  if (tid == 0) {  // x^(2^k) mod P
+  __syncthreads();
+  {  // T[t][i]: byte i followed by t zero bytes
+    const uint32_t i = threadIdx.x;
+    uint32_t c = T[0][i];
+    for (int t = 1; t < 8; ++t) {
+      c = (c >> 8) ^ T[0][c & 0xFFu];
+      T[t][i] = c;
+    }
+  }
+  __syncthreads();
+  const uint32_t g = blockIdx.x * kCrcThreads + threadIdx.x;
+  if (g >= n_segs) return;
+  uint32_t lo = 0, hi = n_files;  // the file: seg_first[f] <= g < seg_first[f + 1]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (seg_first[mid] <= g) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t f = lo;
+  const uint64_t off = (uint64_t)(g - seg_first[f]) * kCrcSeg;
+  const uint32_t len = (uint32_t)min<uint64_t>(kCrcSeg, file_len[f] - off);
+  const uint8_t* p = text + file_text[f] + off;  // (16-byte aligned)
+  uint32_t c = 0xFFFFFFFFu;
+  uint32_t i = 0;
+  for (; i + 16 <= len; i += 16) {
+    const uint4 v = *(const uint4*)(p + i);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int h = 0; h < 4; h += 2) {
+      const uint32_t a = w[h] ^ c, b = w[h + 1];
+      c = T[7][a & 0xFFu] ^ T[6][(a >> 8) & 0xFFu] ^ T[5][(a >> 16) & 0xFFu] ^ T[4][a >> 24] ^ T[3][b & 0xFFu] ^
+          T[2][(b >> 8) & 0xFFu] ^ T[1][(b >> 16) & 0xFFu] ^ T[0][b >> 24];
+    }
+  }
+  for (; i < len; ++i) c = T[0][(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+  seg_crc[g] = ~c;
+}
+
+__global__ __launch_bounds__(64) void inflate_crc_fold_kernel(const uint8_t* __restrict__ text,
+                                                              const uint64_t* __restrict__ file_text,
+                                                              const uint64_t* __restrict__ file_len,
+                                                              const uint32_t* __restrict__ seg_first,
+                                                              const uint32_t* __restrict__ seg_crc, uint32_t n_files,
+                                                              uint32_t* __restrict__ crc_out) {
+  __shared__ uint32_t x2k[64];
+  if (threadIdx.x == 0) {  // x^(2^k) mod P
     uint32_t p = 1u << 30;  // x^1
     for (int k = 0; k < 64; ++k) {
       x2k[k] = p;
@@ -240,31 +578,18 @@ __global__ __launch_bounds__(kCrcThreads) void inflate_crc_kernel(const uint8_t*
     }
   }
   __syncthreads();
-  const uint32_t f = blockIdx.x;
-  const uint8_t* t = text + file_text[f];
+  const uint32_t f = blockIdx.x * 64 + threadIdx.x;
+  if (f >= n_files) return;
   const uint64_t len = file_len[f];
+  const uint32_t xseg = crc_x8n(kCrcSeg, x2k);
   uint32_t crc = 0;  // of the bytes so far (standard CRC-32; 0 for none)
-  for (uint64_t r0 = 0; r0 < len; r0 += kCrcSeg * kCrcThreads) {
-    const uint64_t s0 = r0 + tid * kCrcSeg;
-    const uint64_t s1 = min(s0 + kCrcSeg, len);
-    uint32_t c = 0xFFFFFFFFu;
-    for (uint64_t i = s0; i < s1; ++i) c = table[(c ^ t[i]) & 0xFFu] ^ (c >> 8);
-    seg[tid] = s0 < s1 ? ~c : 0u;
-    __syncthreads();
-    if (tid == 0) {  // crc(A || B) = x^(8|B|) crc(A) ^ crc(B)
-      for (uint32_t k = 0; k < kCrcThreads; ++k) {
-        const uint64_t a0 = r0 + k * kCrcSeg;
-        if (a0 >= len) break;
-        const uint64_t bl = min(kCrcSeg, len - a0);
-        crc = crc_mul(crc_x8n(bl, x2k), crc) ^ seg[k];
-      }
-    }
-    __syncthreads();
+  for (uint32_t g = seg_first[f]; g < seg_first[f + 1]; ++g) {
+    const uint64_t off = (uint64_t)(g - seg_first[f]) * kCrcSeg;
+    const uint64_t bl = min<uint64_t>(kCrcSeg, len - off);
+    crc = crc_mul(bl == kCrcSeg ? xseg : crc_x8n(bl, x2k), crc) ^ seg_crc[g];
   }
-  if (tid == 0) {
-    crc_out[f] = crc;
-    crc_out[gridDim.x + f] = len ? t[0] : 0u;  // (the caller checks the format: FASTA starts with '>')
-  }
+  crc_out[f] = crc;
+  crc_out[n_files + f] = len ? text[file_text[f]] : 0u;  // (the caller checks the format: FASTA starts with '>')
 }
 
 }  // namespace
@@ -278,15 +603,14 @@ hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st) {
 
 hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st) {
   if (a.n_lanes == 0) return hipSuccess;
-  hipLaunchKernelGGL(inflate_decode_kernel, dim3((a.n_lanes + kDecodeLanes - 1) / kDecodeLanes), dim3(kDecodeLanes),
-                     0, st, a);
+  hipLaunchKernelGGL(inflate_decode_kernel, dim3(a.n_lanes), dim3(kSpanLanes), 0, st, a);
   return hipGetLastError();
 }
 
 hipError_t launch_inflate_place(const InflatePlace& a, uint64_t text_len, uint8_t* text, uint32_t n_files,
-                                const uint64_t* file_text, const uint64_t* file_len, uint32_t* crc,
-                                hipStream_t st) {
-  if (a.n_lanes) hipLaunchKernelGGL(inflate_place_kernel, dim3(a.n_lanes), dim3(kPlaceThreads), 0, st, a);
+                                const uint64_t* file_text, const uint64_t* file_len, const uint32_t* seg_first,
+                                uint32_t n_segs, uint32_t* seg_crc, uint32_t* crc, hipStream_t st) {
+  if (a.n_lanes) hipLaunchKernelGGL(inflate_expand_kernel, dim3(a.n_lanes), dim3(kExpandThreads), 0, st, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint64_t groups = (text_len + 15) / 16;
@@ -295,8 +619,14 @@ hipError_t launch_inflate_place(const InflatePlace& a, uint64_t text_len, uint8_
                        dim3(256), 0, st, a.val, text, text_len, a.flags);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (n_files) hipLaunchKernelGGL(inflate_crc_kernel, dim3(n_files), dim3(kCrcThreads), 0, st, text, file_text,
-                                  file_len, crc);
+  if (n_segs)
+    hipLaunchKernelGGL(inflate_crc_seg_kernel, dim3((n_segs + kCrcThreads - 1) / kCrcThreads), dim3(kCrcThreads), 0,
+                       st, text, file_text, file_len, seg_first, n_files, n_segs, seg_crc);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (n_files)
+    hipLaunchKernelGGL(inflate_crc_fold_kernel, dim3((n_files + 63) / 64), dim3(64), 0, st, text, file_text, file_len,
+                       seg_first, seg_crc, n_files, crc);
   return hipGetLastError();
 }
 

@@ -214,7 +214,8 @@ GG_HD int decode_sym(const Bits& in, uint64_t& pos, const Canon& c, const uint8_
 
 // Walks the lit/len + distance code lengths of a dynamic header (after the
 // code-length code), calling f(symbol index, length) for each nonzero
-// length; false on a malformed sequence.
+// length (f returns false to stop: the walk then fails); false on a
+// malformed sequence.
 template <class F>
 GG_HD bool walk_lengths(const Bits& in, uint64_t& pos, const ClCode& cl, uint32_t n, F&& f) {
   uint32_t i = 0, prev = 0;
@@ -222,7 +223,7 @@ GG_HD bool walk_lengths(const Bits& in, uint64_t& pos, const ClCode& cl, uint32_
     const int s = decode_sym(in, pos, cl.c, cl.sym, nullptr);
     if (s < 0) return false;
     if (s < 16) {
-      if (s) f(i, (uint32_t)s);
+      if (s && !f(i, (uint32_t)s)) return false;
       prev = (uint32_t)s;
       ++i;
       continue;
@@ -239,7 +240,8 @@ GG_HD bool walk_lengths(const Bits& in, uint64_t& pos, const ClCode& cl, uint32_
     }
     if (i + rep > n) return false;
     if (val)
-      for (uint32_t r = 0; r < rep; ++r) f(i + r, val);
+      for (uint32_t r = 0; r < rep; ++r)
+        if (!f(i + r, val)) return false;
     i += rep;
     if (s != 16) prev = 0;
   }
@@ -250,11 +252,28 @@ GG_HD bool walk_lengths(const Bits& in, uint64_t& pos, const ClCode& cl, uint32_
 // complete code-length code, length sequence in range, an end-of-block
 // code, lit/len and distance codes zlib accepts.)  On success pos is moved
 // past the header.
-GG_HD bool block_header_ok(const Bits& in, uint64_t& pos) {
+// The search's first filter, from registers only: BTYPE 10 (dynamic), HLIT
+// and HDIST in range, and a complete code-length code (its Kraft sum over
+// the 3-bit lengths, sum 2^(7 - len) = 128).  Passes ~1% of positions.
+GG_HD bool block_header_quick(const Bits& in, uint64_t pos) {
   const uint32_t h = in.peek(pos);
   if (((h >> 1) & 3u) != 2u) return false;  // BTYPE 10: dynamic Huffman
+  if (((h >> 3) & 31u) > 29u || ((h >> 8) & 31u) > 29u) return false;  // HLIT <= 286, HDIST <= 30
+  const uint32_t hclen = ((h >> 13) & 15u) + 4u;
+  const uint64_t f = (uint64_t)in.peek(pos + 17) | ((uint64_t)in.peek(pos + 49) << 32);
+  uint32_t kraft = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < (uint32_t)kClSyms; ++i) {
+    const uint32_t l = (uint32_t)(f >> (3 * i)) & 7u;
+    kraft += (i < hclen && l) ? 128u >> l : 0u;
+  }
+  return kraft == 128u;
+}
+
+GG_HD bool block_header_ok(const Bits& in, uint64_t& pos) {
+  if (!block_header_quick(in, pos)) return false;
+  const uint32_t h = in.peek(pos);
   const uint32_t hlit = ((h >> 3) & 31u) + 257u, hdist = ((h >> 8) & 31u) + 1u, hclen = ((h >> 13) & 15u) + 4u;
-  if (hlit > 286 || hdist > 30) return false;
   uint64_t p = pos + 17;
   ClCode cl;
   if (!read_cl_code(in, p, hclen, cl)) return false;
@@ -262,13 +281,19 @@ GG_HD bool block_header_ok(const Bits& in, uint64_t& pos) {
 #pragma unroll
   for (int l = 0; l <= kMaxBits; ++l) lc[l] = dc[l] = 0;
   bool eob = false;
+  // Kraft sums in units of 2^-15: an over-subscribed code stops the walk
+  // (most positions that pass the code-length code fail within a few lengths)
+  uint32_t kl = 0, kd = 0;
   if (!walk_lengths(in, p, cl, hlit + hdist, [&](uint32_t i, uint32_t len) {
         if (i < hlit) {
           lc[len] += 1;
           if (i == 256) eob = true;
-        } else {
-          dc[len] += 1;
+          kl += 1u << (kMaxBits - len);
+          return kl <= (1u << kMaxBits);
         }
+        dc[len] += 1;
+        kd += 1u << (kMaxBits - len);
+        return kd <= (1u << kMaxBits);
       }))
     return false;
   if (!eob) return false;
@@ -396,6 +421,7 @@ GG_HD int read_block_header(const Bits& in, uint64_t& pos, LaneTables<Store>& t,
         } else {
           dc[len] += 1;
         }
+        return true;
       }))
     return -1;
   if (!eob) return -1;
@@ -420,6 +446,7 @@ GG_HD int read_block_header(const Bits& in, uint64_t& pos, LaneTables<Store>& t,
   walk_lengths(in, q, cl, hlit + hdist, [&](uint32_t i, uint32_t len) {
     if (i < hlit) t.s.lsym((int)lo[len]++) = (uint16_t)i;
     else t.s.dsym((int)doff[len]++) = (uint8_t)(i - hlit);
+    return true;
   });
   pos = p;
   return 2;
@@ -511,6 +538,122 @@ GG_HD uint32_t decode_blocks(const Bits& in, uint64_t pos, uint64_t end, uint64_
       return end == ~0ull ? kDecOk : kDecFinalEarly;
     }
   }
+}
+
+// One sub-span of a block body, decoded speculatively.  The device splits a
+// block's body [body0, span_end) into up to 64 sub-spans of L bits, one
+// lane each, all decoded at once with the block's tables, each from its
+// span's start S (usually inside a symbol) until the first symbol start at
+// or past its span's end R (or the end-of-block symbol, or an invalid code).
+//
+// Chaining.  Decoding is deterministic from a symbol start, and a decode
+// begun inside a symbol falls onto the true symbol starts after a while
+// (a median of ~150 bits on FASTA; a few never do within a span).  The
+// decode records checkpoints: for k = 0, 1, ..., the first symbol start at
+// or after S + 64k, with the tokens and bytes emitted before it.  The lane
+// before ends at E, the true first symbol start at or after S:
+//   - checkpoint 0 at E: this lane was right from its start (its tokens
+//     before E dropped);
+//   - otherwise the lane decodes again from E, comparing each of its
+//     checkpoints with the first decode's: at the first that agrees both
+//     decodes are on the same symbol start, so the second stops there and
+//     the first decode's tokens from that checkpoint on complete it.
+// Each such round makes the first lane not yet right right, and one round
+// almost always fixes all of them.
+enum SpanStatus : uint32_t {
+  kSpanRange = 0,   // reached range_end (stop: the first symbol start >= range_end)
+  kSpanEob = 1,     // decoded the end-of-block symbol (stop: the bit after it)
+  kSpanBad = 2,     // an invalid code or length/distance symbol
+  kSpanSynced = 3,  // ck() returned false at a checkpoint (stop: that symbol start)
+};
+constexpr uint32_t kCkBits = 64;  // checkpoint spacing: > the longest symbol (15 + 5 + 15 + 13 bits)
+
+// A checkpoint: its symbol start's offset past S + 64k (< 64), the tokens
+// before it (24 bits) and the bytes they stand for (32 bits).
+GG_HD uint64_t ck_pack(uint32_t off, uint32_t n, uint64_t bytes) {
+  return (uint64_t)off | ((uint64_t)n << 8) | (bytes << 32);
+}
+GG_HD uint32_t ck_off(uint64_t c) { return (uint32_t)c & 0xFFu; }
+GG_HD uint32_t ck_tok(uint64_t c) { return (uint32_t)(c >> 8) & 0xFFFFFFu; }
+GG_HD uint64_t ck_bytes(uint64_t c) { return c >> 32; }
+
+// Decodes from start; ck(k, c) is called at the first symbol start at or
+// after s_nom + 64k for every k (c = ck_pack of it; a symbol start before
+// s_nom has no checkpoint) and stops the decode when it returns false.
+// n and bytes receive the tokens emitted and the bytes they stand for,
+// stop the bit position where decoding stopped.
+template <class Store, class Emit, class Ck>
+GG_HD uint32_t decode_span(const Bits& in, uint64_t start, uint64_t s_nom, uint64_t range_end, LaneTables<Store>& t,
+                           Emit&& emit, Ck&& ck, uint32_t& n, uint64_t& bytes, uint64_t& stop) {
+  Cursor cur{in.w};
+  cur.seek(start);
+  n = 0;
+  bytes = 0;
+  uint32_t k = 0;
+  uint64_t next_ck = s_nom;
+  for (;;) {
+    if (cur.pos >= range_end) {
+      stop = cur.pos;
+      return kSpanRange;
+    }
+    if (cur.pos >= next_ck) {  // (a symbol is shorter than kCkBits: one checkpoint at most)
+      if (!ck(k, ck_pack((uint32_t)(cur.pos - next_ck), n, bytes))) {
+        stop = cur.pos;
+        return kSpanSynced;
+      }
+      ++k;
+      next_ck += kCkBits;
+    }
+    const int sy = t.lit(cur);
+    if (sy < 0) break;
+    if (sy < 256) {
+      if (!emit((uint32_t)sy)) break;
+      ++n;
+      bytes += 1;
+      continue;
+    }
+    if (sy == 256) {
+      stop = cur.pos;
+      return kSpanEob;
+    }
+    const uint32_t li = (uint32_t)sy - 257u;
+    if (li >= 29) break;
+    const uint32_t len = len_base(li) + cur.get(len_extra(li));
+    const int d = t.dist(cur);
+    if (d < 0 || d >= 30) break;
+    const uint32_t dist = dist_base((uint32_t)d) + cur.get(dist_extra((uint32_t)d));
+    if (!emit(tok_match(len, dist))) break;
+    ++n;
+    bytes += len;
+  }
+  stop = cur.pos;
+  return kSpanBad;
+}
+
+// Sub-span layout of a block body [body0, span_end): nsub lanes of L bits
+// (at least kMinSpanBits each); the last lane runs to span_end.
+constexpr uint64_t kMinSpanBits = 256;
+GG_HD void span_layout(uint64_t body0, uint64_t span_end, uint32_t max_lanes, uint64_t& L, uint32_t& nsub) {
+  const uint64_t bits = span_end > body0 ? span_end - body0 : 0;
+  L = (bits + max_lanes - 1) / max_lanes;
+  if (L < kMinSpanBits) L = kMinSpanBits;
+  nsub = (uint32_t)((bits + L - 1) / L);
+  if (nsub == 0) nsub = 1;
+}
+
+// Per lane of a segment's decode: two token areas (the first decode, the
+// second) of span_cap(L) tokens each -- a decode of [S, R + 48) emits at
+// most one token per bit -- and span_cks(L) checkpoints (u64).
+GG_HD uint64_t span_cap(uint64_t L) { return (L + kCkBits + 3) / 4 * 4; }
+GG_HD uint64_t span_cks(uint64_t L) { return (L / kCkBits + 4) & ~1ull; }  // (even: areas stay 16-byte aligned)
+GG_HD uint64_t span_words(uint64_t L) { return 2 * span_cap(L) + 2 * span_cks(L); }  // (u32 words, even)
+// Scratch words the device decode of a segment of seg_bits bits needs (L
+// as span_layout makes it for the segment's longest possible body).
+GG_HD uint64_t decode_scratch(uint64_t seg_bits) {
+  uint64_t L;
+  uint32_t nsub;
+  span_layout(0, seg_bits, 64, L, nsub);
+  return 64 * span_words(L);
 }
 
 }  // namespace inflate

@@ -129,8 +129,8 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
       if (start[c] != ~0ull && start[c] > starts[f].back()) starts[f].push_back(start[c]);
   }
   std::vector<uint32_t> lane_file, status, bfin;
-  std::vector<uint64_t> lane_start, lane_end, tok_off, tok_cap, n_tok, out_len, last_end;
-  uint32_t *d_lfile = nullptr, *d_tok = nullptr;
+  std::vector<uint64_t> lane_start, lane_end, tok_off, tok_cap, scr_off, n_tok, out_len, last_end;
+  uint32_t *d_lfile = nullptr, *d_tok = nullptr, *d_scr = nullptr;
   uint64_t *d_toff = nullptr, *d_res = nullptr;
   for (int pass = 0;; ++pass) {
     if (pass >= kMaxRelaunch) return hand_back("block starts did not chain", 0);  // (ok = false)
@@ -139,31 +139,37 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     lane_end.clear();
     tok_off.clear();
     tok_cap.clear();
-    uint64_t toks = 0;
+    scr_off.clear();
+    uint64_t toks = 0, scr = 0;
     for (uint32_t f = 0; f < nf; ++f)
       for (size_t i = 0; i < starts[f].size(); ++i) {
         const uint64_t s0 = starts[f][i];
         const uint64_t e = i + 1 < starts[f].size() ? starts[f][i + 1] : ~0ull;
         // every symbol takes >= 1 bit: one token per bit bounds every lane
         // (literal-heavy DNA blocks reach ~0.5 tokens per bit)
-        const uint64_t cap = ((e == ~0ull ? fbits[f] : e) - s0) + 64;
+        const uint64_t bits = (e == ~0ull ? fbits[f] : e) - s0;
+        const uint64_t cap = bits + 64;
         lane_file.push_back(f);
         lane_start.push_back(s0);
         lane_end.push_back(e);
         tok_off.push_back(toks);
         tok_cap.push_back(cap);
+        scr_off.push_back(scr);
         toks += (cap + 3) / 4 * 4;
+        scr += inflate::decode_scratch(bits);
       }
     const uint32_t nl = (uint32_t)lane_file.size();
     if (nl == 0) break;
     uint32_t *d_status, *d_bfin;
-    uint64_t *d_lstart, *d_lend, *d_tcap;
+    uint64_t *d_lstart, *d_lend, *d_tcap, *d_soff;
     GG_HIP(m, scratch_t(m, "gz_lfile", nl, &d_lfile));
     GG_HIP(m, scratch_t(m, "gz_lstart", nl, &d_lstart));
     GG_HIP(m, scratch_t(m, "gz_lend", nl, &d_lend));
     GG_HIP(m, scratch_t(m, "gz_toff", nl, &d_toff));
     GG_HIP(m, scratch_t(m, "gz_tcap", nl, &d_tcap));
+    GG_HIP(m, scratch_t(m, "gz_soff", nl, &d_soff));
     GG_HIP(m, scratch_t(m, "gz_tok", std::max<uint64_t>(toks, 4), &d_tok));
+    GG_HIP(m, scratch_t(m, "gz_scr", std::max<uint64_t>(scr, 4), &d_scr));
     // results contiguous: n_tok, out_len, last_end (u64), then status, bfinal (u32)
     GG_HIP(m, scratch_t(m, "gz_res", (size_t)nl * 4, &d_res));
     d_status = (uint32_t*)(d_res + 3 * (size_t)nl);
@@ -173,6 +179,7 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     GG_HIP(m, hipMemcpyAsync(d_lend, lane_end.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     GG_HIP(m, hipMemcpyAsync(d_toff, tok_off.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     GG_HIP(m, hipMemcpyAsync(d_tcap, tok_cap.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync(d_soff, scr_off.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     InflateDecode d;
     d.in = (const uint32_t*)d_in;
     d.file_word = d_fword;
@@ -184,6 +191,8 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     d.tok = d_tok;
     d.tok_off = d_toff;
     d.tok_cap = d_tcap;
+    d.scr = d_scr;
+    d.scr_off = d_soff;
     d.n_tok = d_res;
     d.out_len = d_res + nl;
     d.last_end = d_res + 2 * (size_t)nl;
@@ -246,7 +255,7 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   foff.assign(nf + 1, 0);
   for (uint32_t f = 0; f < nf; ++f) foff[f + 1] = foff[f] + (flen[f] + 15) / 16 * 16;
   const uint64_t text_len = foff[nf];
-  if (text_len >= (1ull << 31)) return hand_back("batch text over 2 GiB", 0);  // (31-bit resolve pointers)
+  if (text_len >= (1ull << 30)) return hand_back("batch text over 1 GiB", 0);  // (30-bit expand pointers)
   for (size_t l = 0; l < lane_out.size(); ++l) lane_out[l] += foff[lane_file[l]];
   uint32_t *d_val, *d_flags, *d_crc;
   uint64_t *d_lout, *d_ftext, *d_flen;
@@ -277,7 +286,14 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   p.n_lanes = (uint32_t)lane_out.size();
   p.val = d_val;
   p.flags = d_flags;
-  GG_HIP(m, launch_inflate_place(p, text_len, *d_text, nf, d_ftext, d_flen, d_crc, st));
+  std::vector<uint32_t> seg_first(nf + 1, 0);
+  for (uint32_t f = 0; f < nf; ++f) seg_first[f + 1] = seg_first[f] + (uint32_t)((flen[f] + kInflateCrcSeg - 1) / kInflateCrcSeg);
+  const uint32_t nseg = seg_first[nf];
+  uint32_t *d_sfirst, *d_scrc;
+  GG_HIP(m, scratch_t(m, "gz_sfirst", nf + 1, &d_sfirst));
+  GG_HIP(m, scratch_t(m, "gz_scrc", std::max(nseg, 1u), &d_scrc));
+  GG_HIP(m, hipMemcpyAsync(d_sfirst, seg_first.data(), (nf + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  GG_HIP(m, launch_inflate_place(p, text_len, *d_text, nf, d_ftext, d_flen, d_sfirst, nseg, d_scrc, d_crc, st));
   // plain files (not gzip) go into their place as they are
   for (uint32_t f = 0; f < nf; ++f)
     if (!files[f].gz && files[f].data_len)

@@ -281,12 +281,12 @@ gg_status pairs_with_ani(gg_ctx* c, const std::vector<gg_pair>& res, gg_pair** p
 constexpr uint32_t kBatchGenomes = 32;          // genomes per K1 batch
 constexpr uint64_t kBatchWords = 64ull << 20;   // or 1 Gbases of packed words, whichever first
 constexpr uint64_t kBatchText = 1ull << 30;     // raw (device-parsed) batches: 1 GiB of FASTA text
-// device-inflate batches: up to 4096 files, 384 MiB of gzip data or 1.5 GiB
+// device-inflate batches: up to 4096 files, 384 MiB of gzip data or 960 MiB
 // of text (the inflate's parallel units are the streams' blocks, ~30 per
 // 3 Mbp genome: a batch needs hundreds of files to fill the GPU)
 constexpr uint32_t kBatchGenomesGz = 4096;
 constexpr uint64_t kBatchGzBytes = 384ull << 20;
-constexpr uint64_t kBatchGzText = 3ull << 29;
+constexpr uint64_t kBatchGzText = 960ull << 20;  // (inflate_batch: text < 1 GiB)
 
 // memcpy on up to T threads (staging copies of a batch into pinned memory:
 // one thread moves ~10 GB/s, a batch of FASTA text is up to 1 GiB)

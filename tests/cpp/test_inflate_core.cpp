@@ -80,6 +80,157 @@ static void expand(const std::vector<uint32_t>& toks, std::vector<uint8_t>& out)
   }
 }
 
+// The device decode of one segment [s0, end) (end ~0: the file's last),
+// restated serially: per block the header, then the body's sub-spans
+// decoded speculatively, chained by checkpoints in rounds (a lane not right
+// from its start decodes again from the true start until it meets its
+// first decode) and concatenated (inflate.hip inflate_decode_kernel).
+// rounds counts second-decode rounds, redo_bits the bits they decoded.
+struct SpecStats {
+  size_t rounds = 0, redo_bits = 0, spans = 0, span_bits = 0;
+};
+static uint32_t spec_segment(const Bits& in, uint64_t s0, uint64_t end, uint64_t limit, LaneTables<ArrayStore>& tab,
+                             std::vector<uint32_t>& out, uint64_t& out_len, uint64_t& last_end, uint32_t& fin,
+                             SpecStats& ss) {
+  const bool final_seg = end == ~0ull;
+  uint64_t pos = s0;
+  out_len = 0;
+  fin = 0;
+  for (;;) {
+    if (pos == end) break;
+    if (pos > end || pos >= limit) {
+      last_end = pos;
+      return kDecOverrun;
+    }
+    uint64_t q = pos;
+    uint32_t bf = 0, stl = 0;
+    const int bt = read_block_header(in, q, tab, bf, stl);
+    if (bt < 0) {
+      last_end = q;
+      return kDecBad;
+    }
+    if (bt == 0) {
+      if (q + 8ull * stl > limit) return kDecBad;
+      for (uint32_t i = 0; i < stl; ++i) out.push_back(((const uint8_t*)in.w)[q / 8 + i]);
+      out_len += stl;
+      pos = q + 8ull * stl;
+    } else {
+      const uint64_t span_end = final_seg ? limit : end;
+      uint64_t L;
+      uint32_t nsub;
+      span_layout(q, span_end, 64, L, nsub);
+      struct Lane {
+        uint64_t S, R, first = 0, Ea = 0, Eb = 0, ba = 0, bb = 0;
+        uint32_t na = 0, nb = 0, sa = 0, sb = 0, nck = 0;
+        int synced = -1;
+        bool redone = false;
+        std::vector<uint32_t> A, B;
+        std::vector<uint64_t> ck;
+        uint64_t E() const { return redone && synced < 0 ? Eb : Ea; }
+        uint32_t st() const { return redone && synced < 0 ? sb : sa; }
+      };
+      std::vector<Lane> ln(nsub);
+      for (uint32_t j = 0; j < nsub; ++j) {
+        Lane& x = ln[j];
+        x.S = q + j * L;
+        x.R = j + 1 == nsub ? span_end : x.S + L;
+        x.ck.assign(span_cks(L), 0);
+        x.sa = decode_span(in, x.S, x.S, x.R, tab,
+                           [&](uint32_t t) {
+                             if (x.A.size() >= span_cap(L)) return false;
+                             x.A.push_back(t);
+                             return true;
+                           },
+                           [&](uint32_t k, uint64_t c) {
+                             if (k < x.ck.size()) x.ck[k] = c, x.nck = k + 1;
+                             return true;
+                           },
+                           x.na, x.ba, x.Ea);
+        x.first = x.nck ? x.S + ck_off(x.ck[0]) : ~0ull;
+        ss.spans += 1;
+        ss.span_bits += x.R - x.S;
+      }
+      uint32_t c_end = 0;
+      bool overrun = false;
+      for (;;) {
+        std::vector<bool> ok(nsub);
+        uint32_t c = nsub, t = nsub;
+        for (uint32_t j = 0; j < nsub; ++j) {
+          ok[j] = j == 0 || (ln[j - 1].st() == kSpanRange && ln[j].first == ln[j - 1].E());
+          if (!ok[j] && c == nsub) c = j;
+          if (ln[j].st() != kSpanRange && t == nsub) t = j;
+        }
+        if (t < c) {
+          c_end = t;
+          break;
+        }
+        if (c >= nsub) {
+          overrun = true;
+          c_end = nsub - 1;
+          break;
+        }
+        ++ss.rounds;
+        std::vector<uint64_t> from(nsub, ~0ull);
+        for (uint32_t j = c; j < nsub; ++j)
+          if (!ok[j] && ln[j - 1].st() == kSpanRange) from[j] = ln[j - 1].E();
+        for (uint32_t j = c; j < nsub; ++j) {
+          if (from[j] == ~0ull) continue;
+          Lane& x = ln[j];
+          x.B.clear();
+          x.redone = true;
+          x.synced = -1;
+          x.first = from[j];
+          x.sb = decode_span(in, from[j], x.S, x.R, tab,
+                             [&](uint32_t tk) {
+                               if (x.B.size() >= span_cap(L)) return false;
+                               x.B.push_back(tk);
+                               return true;
+                             },
+                             [&](uint32_t k, uint64_t cc) {
+                               if (k < x.nck && ck_off(cc) == ck_off(x.ck[k])) {
+                                 x.synced = (int)k;
+                                 return false;
+                               }
+                               return true;
+                             },
+                             x.nb, x.bb, x.Eb);
+          ss.redo_bits += x.Eb - from[j];
+        }
+      }
+      if (overrun) {
+        last_end = ln[c_end].E();
+        return kDecOverrun;
+      }
+      if (ln[c_end].st() == kSpanBad) {
+        last_end = ln[c_end].E();
+        return kDecBad;
+      }
+      for (uint32_t j = 0; j <= c_end; ++j) {
+        const Lane& x = ln[j];
+        if (!x.redone) {
+          out.insert(out.end(), x.A.begin() + ck_tok(x.ck[0]), x.A.begin() + x.na);
+          out_len += x.ba - ck_bytes(x.ck[0]);
+        } else {
+          out.insert(out.end(), x.B.begin(), x.B.begin() + x.nb);
+          out_len += x.bb;
+          if (x.synced >= 0) {
+            out.insert(out.end(), x.A.begin() + ck_tok(x.ck[x.synced]), x.A.begin() + x.na);
+            out_len += x.ba - ck_bytes(x.ck[x.synced]);
+          }
+        }
+      }
+      pos = ln[c_end].E();
+    }
+    if (bf) {
+      fin = 1;
+      last_end = pos;
+      return final_seg ? kDecOk : kDecFinalEarly;
+    }
+  }
+  last_end = pos;
+  return kDecOk;
+}
+
 int main(int argc, char** argv) {
   int failures = 0;
   uint32_t chunk = 4096;
@@ -163,6 +314,23 @@ int main(int argc, char** argv) {
       if (!again) break;
     }
     if (starts.empty()) continue;
+    // (c) the device decode of each lane's segment: the same tokens
+    SpecStats ss;
+    for (size_t b = 0; b < starts.size(); ++b) {
+      const uint64_t end = b + 1 < starts.size() ? starts[b + 1] : ~0ull;
+      std::vector<uint32_t> t3;
+      uint64_t ol, le;
+      uint32_t fin;
+      const uint32_t r = spec_segment(in, starts[b], end, limit_bits, tab, t3, ol, le, fin, ss);
+      if (r != kDecOk || t3 != part[b] || ol != part_len[b]) {
+        fprintf(stderr, "%s: lane %zu: sub-span decode differs (status %u, %zu vs %zu tokens)\n", argv[a], b, r,
+                t3.size(), part[b].size());
+        ++failures;
+        starts.clear();
+        break;
+      }
+    }
+    if (starts.empty()) continue;
     // place: every byte a literal (bit 31) or a pointer to an earlier byte
     std::vector<uint32_t> val;
     for (size_t b = 0; b < part.size(); ++b)
@@ -193,8 +361,9 @@ int main(int argc, char** argv) {
       continue;
     }
     printf("{\"file\": \"%s\", \"bytes\": %zu, \"gz_bytes\": %zu, \"starts_found\": %zu, \"starts_dropped\": %zu, "
-           "\"lanes\": %zu, \"tokens\": %zu, \"max_chain\": %zu}\n",
-           argv[a], want.size(), gz.size(), found, dropped, starts.size(), toks.size(), max_chain);
+           "\"lanes\": %zu, \"tokens\": %zu, \"max_chain\": %zu, \"redo_rounds\": %zu, \"spans\": %zu, \"span_bits\": %zu, \"redo_bits\": %zu}\n",
+           argv[a], want.size(), gz.size(), found, dropped, starts.size(), toks.size(), max_chain, ss.rounds, ss.spans,
+           ss.span_bits, ss.redo_bits);
   }
   if (failures) {
     fprintf(stderr, "%d failure(s)\n", failures);
