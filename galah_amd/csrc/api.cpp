@@ -1217,6 +1217,12 @@ void gg_destroy(gg_ctx* ctx) {
   if (ctx->copy_done) (void)hipEventDestroy(ctx->copy_done);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  for (auto& sl : ctx->gz_slot) {
+    if (sl.st) (void)hipStreamSynchronize(sl.st);
+    if (sl.st) (void)hipStreamDestroy(sl.st);
+    if (sl.host) (void)hipHostFree(sl.host);
+    if (sl.dev) (void)hipFree(sl.dev);
+  }
   delete ctx;
 }
 

@@ -97,6 +97,17 @@ struct gg_ctx {
   // grow-only pinned host staging buffer (streamed ingest)
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
+  // device-inflate staging slots (multi.cpp GzPipe): batch N is inflated
+  // from one while N + 1 is staged into the other by a helper thread, which
+  // touches only its slot (grow-only pinned and device buffers, its stream)
+  struct GzSlot {
+    uint8_t* host = nullptr;
+    size_t host_cap = 0;
+    uint8_t* dev = nullptr;
+    size_t dev_cap = 0;
+    hipStream_t st = nullptr;
+  };
+  GzSlot gz_slot[2];
   // grow-only pinned host buffers keyed by purpose (small read-backs: one
   // DMA instead of a staged copy of pageable memory, ~35 us each)
   std::map<std::string, std::pair<void*, size_t>> host_scratch;
@@ -201,9 +212,12 @@ gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d
 // in_bytes) holds files[f]'s bytes; *d_text receives the batch's FASTA text,
 // file f at foff[f] (16-byte aligned, gaps '\n').  *ok = false (status GG_OK)
 // when the device path does not take the batch: the caller decodes it on the
-// host.  Synchronises m->stream.
+// host.  d_in: the batch already queued to the device on m->stream (at least
+// in_bytes + kInflatePad bytes; nullptr: inflate_batch uploads h_in).
+// Synchronises m->stream.
+constexpr uint64_t kInflatePad = 4096;  // device bytes past a batch's last file (readers run past its end)
 gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const std::vector<InflateFile>& files,
-                        uint8_t** d_text, std::vector<uint64_t>& foff, bool* ok);
+                        uint8_t** d_text, std::vector<uint64_t>& foff, bool* ok, uint8_t* d_in = nullptr);
 
 template <typename T>
 T* copy_out(const std::vector<T>& v) {

@@ -273,6 +273,7 @@ struct InflatePlace {
   const uint64_t* n_tok;
   const uint32_t* lane_file;
   const uint64_t* lane_out;    // [n_lanes] text position of the lane's first byte
+  const uint64_t* lane_pad;    // [n_lanes] its file's last lane: end of the '\n' padding after it (else 0)
   const uint64_t* file_text;   // [n_files] text position of the file's first byte
   uint32_t n_lanes;
   uint32_t* val;               // [text_len] literal (0x80000000 | byte) or the position copied

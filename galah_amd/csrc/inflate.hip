@@ -34,51 +34,153 @@ namespace {
 
 using namespace inflate;
 
-constexpr int kSearchWaves = 4;       // chunks per search workgroup (one wave each)
-constexpr uint32_t kSearchStep = 1024;  // positions filtered before the candidates are checked
+// A lane's code-length code store (inflate_core.hpp ClCode) in LDS.
+struct ClLds {
+  int32_t b[kClBits + 1];
+  uint8_t s[kClSyms + 1];
+  uint8_t o[kClBits + 1];
+  __device__ int32_t& base(int l) { return b[l]; }
+  __device__ uint8_t& sym(int i) { return s[i]; }
+  __device__ uint8_t& off(int l) { return o[l]; }
+};
 
-// One wave per chunk: positions in steps of kSearchStep, 64 at a time
-// through the register-only filter (block_header_quick); the survivors, in
-// order, in LDS; then checked fully one per lane (block_header_ok).  The
-// first that passes is the chunk's start.
+constexpr int kSearchWaves = 4;         // chunks per search workgroup (one wave each)
+constexpr uint32_t kSearchStep = 4096;  // positions per step: 64 consecutive per lane
+constexpr uint32_t kSearchCands = 256;  // candidates listed before they are checked
+constexpr uint32_t kWinWords = kSearchStep / 32 + 8;  // a step's bits plus the 160 after its first lane's last
+
+// block_header_quick (inflate_core.hpp) at bit I (< 32) of the 128-bit
+// window A (A[0] bit 0 = the first position of the group), with no branch:
+// the code-length code's Kraft sum by 7 lookups of 3 fields in kraft3.
+template <int I>
+__device__ __forceinline__ bool quick_at(const uint32_t (&A)[4], const uint8_t* kraft3) {
+  const uint32_t x0 = __builtin_amdgcn_alignbit(A[1], A[0], I);
+  const uint32_t x1 = __builtin_amdgcn_alignbit(A[2], A[1], I);
+  const uint32_t x2 = __builtin_amdgcn_alignbit(A[3], A[2], I);
+  const bool head = (((x0 >> 1) & 3u) == 2u) & (((x0 >> 3) & 31u) <= 29u) & (((x0 >> 8) & 31u) <= 29u);
+  const uint32_t hclen = ((x0 >> 13) & 15u) + 4u;
+  uint64_t f = (uint64_t)__builtin_amdgcn_alignbit(x1, x0, 17) | ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, 17) << 32);
+  f &= (1ull << (3 * hclen)) - 1ull;  // (3 hclen <= 57)
+  uint32_t kr = 0;
+#pragma unroll
+  for (int g = 0; g < 7; ++g) kr += kraft3[(uint32_t)(f >> (9 * g)) & 511u];
+  return head & (kr == 128u);
+}
+template <int I>
+__device__ __forceinline__ void quick_run(const uint32_t (&A)[4], const uint8_t* kraft3, uint32_t& m) {
+  if constexpr (I < 32) {
+    m |= (uint32_t)quick_at<I>(A, kraft3) << I;
+    quick_run<I + 1>(A, kraft3, m);
+  }
+}
+
+// One wave per chunk, in steps of kSearchStep positions: the step's words
+// staged in LDS, each lane filters its 64 consecutive positions from a
+// 160-bit register window (quick_run, ~0.1% pass) and the survivors are
+// appended in order to the chunk's list in LDS.  The full checks
+// (block_header_ok, one candidate per lane) run when the list is full or
+// the chunk is done, so a step waits on no header walk; the first
+// candidate that passes is the chunk's start.
 __global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(InflateSearch a) {
-  __shared__ uint32_t cand[kSearchWaves][kSearchStep];
+  __shared__ uint64_t cand[kSearchWaves][kSearchCands];
+  __shared__ uint32_t win[kSearchWaves][kWinWords];
+  __shared__ ClLds cls[kSearchWaves][64];
+  __shared__ uint8_t kraft3[512];  // sum over 3 code-length fields of 128 >> len (0 for len 0)
+  for (uint32_t i = threadIdx.x; i < 512; i += 64 * kSearchWaves) {
+    uint32_t k = 0;
+    for (int j = 0; j < 3; ++j) {
+      const uint32_t l = (i >> (3 * j)) & 7u;
+      k += l ? 128u >> l : 0u;
+    }
+    kraft3[i] = (uint8_t)k;
+  }
+  __syncthreads();
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t c = blockIdx.x * kSearchWaves + wv;
   const uint32_t lane = threadIdx.x & 63u;
   if (c >= a.n_chunks) return;
-  uint32_t* cw = cand[wv];
+  uint64_t* cw = cand[wv];
+  uint32_t* ww = win[wv];
+  ClLds& cl = cls[wv][lane];
   const uint32_t f = a.chunk_file[c];
-  const Bits in{a.in + a.file_word[f]};
+  const uint32_t* stream = a.in + a.file_word[f];
   const uint64_t b0 = a.chunk_bit0[c];
   const uint64_t b1 = min(b0 + (uint64_t)a.chunk_bits, a.file_bits[f]);
-  const uint64_t lt = (1ull << lane) - 1ull;
+  // words a position before b1 can touch in the filter (its 128 bits; the
+  // file's trailer or the batch's padding follows its deflate data)
+  const uint64_t wend = (a.file_bits[f] + 31) / 32 + 5;
+  const Bits in{stream};
   uint64_t found = ~0ull;
-  for (uint64_t s0 = b0; s0 < b1 && found == ~0ull; s0 += kSearchStep) {  // (uniform per wave)
-    uint32_t nc = 0;
-    for (uint32_t r = 0; r < kSearchStep; r += 64) {
-      const uint64_t p = s0 + r + lane;
-      const bool pass = p < b1 && block_header_quick(in, p);
-      const uint64_t m = __ballot(pass);
-      if (pass) cw[nc + (uint32_t)__popcll(m & lt)] = (uint32_t)(p - s0);
-      nc += (uint32_t)__popcll(m);
+  uint32_t nc = 0;  // candidates listed, not yet checked (uniform)
+  for (uint64_t s0 = b0; found == ~0ull;) {  // (uniform per wave)
+    if (s0 < b1) {
+      const uint64_t s1 = min(s0 + kSearchStep, b1);
+      const uint64_t w0 = s0 >> 5;
+      for (uint32_t i = lane; i < kWinWords; i += 64) ww[i] = w0 + i < wend ? stream[w0 + i] : 0u;
+      __builtin_amdgcn_wave_barrier();
+      // this lane's positions s0 + 64 lane + [0, 64)
+      const uint32_t q0 = (uint32_t)(s0 & 31u) + 64u * lane;
+      uint32_t A[5];
+      {
+        uint32_t W[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k) W[k] = ww[(q0 >> 5) + k];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) A[k] = __builtin_amdgcn_alignbit(W[k + 1], W[k], q0 & 31u);
+      }
+      uint32_t m0 = 0, m1 = 0;
+      {
+        const uint32_t a0[4] = {A[0], A[1], A[2], A[3]};
+        quick_run<0>(a0, kraft3, m0);
+      }
+      {
+        const uint32_t a1[4] = {A[1], A[2], A[3], A[4]};
+        quick_run<0>(a1, kraft3, m1);
+      }
+      uint64_t m = (uint64_t)m0 | ((uint64_t)m1 << 32);
+      const uint64_t p0 = s0 + 64ull * lane;
+      if (p0 >= s1) m = 0;
+      else if (s1 - p0 < 64) m &= (1ull << (s1 - p0)) - 1ull;
+      // candidates in position order: lane-major
+      const uint32_t cnt = (uint32_t)__popcll(m);
+      uint32_t incl = cnt;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o);
+        if (lane >= (uint32_t)o) incl += y;
+      }
+      const uint32_t total = __shfl(incl, 63);
+      uint32_t k = nc + incl - cnt;
+      while (m && k < kSearchCands) {
+        cw[k++] = p0 + (uint32_t)__ffsll((unsigned long long)m) - 1u;
+        m &= m - 1;
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (nc + total > kSearchCands) {  // the list is full: the next step starts after its last candidate
+        nc = kSearchCands;
+        s0 = cw[kSearchCands - 1] + 1;
+      } else {
+        nc += total;
+        s0 = s1;
+      }
+      if (nc < kSearchCands - 64 && s0 < b1) continue;  // (room for more: keep filtering)
     }
-    __builtin_amdgcn_wave_barrier();
+    // the full checks of the listed candidates, in order
     for (uint32_t k0 = 0; k0 < nc; k0 += 64) {
       bool ok = false;
-      uint64_t p = 0;
       if (k0 + lane < nc) {
-        p = s0 + cw[k0 + lane];
-        uint64_t q = p;
-        ok = block_header_ok(in, q);
+        uint64_t q = cw[k0 + lane];
+        ok = block_header_ok(in, q, cl);
       }
-      const uint64_t m = __ballot(ok);
-      if (m) {
-        found = s0 + cw[k0 + (uint32_t)__ffsll((unsigned long long)m) - 1u];
+      const uint64_t bm = __ballot(ok);
+      if (bm) {
+        found = cw[k0 + (uint32_t)__ffsll((unsigned long long)bm) - 1u];
         break;
       }
     }
     __builtin_amdgcn_wave_barrier();
+    nc = 0;
+    if (s0 >= b1) break;
   }
   if (lane == 0) a.start[c] = found;
 }
@@ -86,10 +188,14 @@ __global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(Infla
 struct LdsStore {
   int32_t* lb;
   int32_t* db;
+  uint32_t* lc;
+  uint32_t* dc;
   uint16_t* ls;
   uint8_t* ds;
   __device__ int32_t& lbase(int l) { return lb[l]; }
   __device__ int32_t& dbase(int l) { return db[l]; }
+  __device__ uint32_t& lcnt(int l) { return lc[l]; }
+  __device__ uint32_t& dcnt(int l) { return dc[l]; }
   __device__ uint16_t& lsym(int i) { return ls[i]; }
   __device__ uint8_t& dsym(int i) { return ds[i]; }
 };
@@ -121,6 +227,20 @@ struct TokSink {
   }
 };
 
+// n tokens from a lane's scratch to the segment's tokens, 8 loads in flight
+// (a plain loop waited on each load in turn).
+__device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint32_t n) {
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = src[i + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) dst[i + k] = v[k];
+  }
+  for (; i < n; ++i) dst[i] = src[i];
+}
+
 // One wave per segment (a found block start up to the next one).  Per block:
 // lane 0 reads the header into the wave's LDS tables; the body is split into
 // up to 64 sub-spans decoded at once, each lane from the start of its span
@@ -132,6 +252,8 @@ struct TokSink {
 // to the segment's tokens.
 __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecode a) {
   __shared__ int32_t lb[kMaxBits + 1], db[kMaxBits + 1];
+  __shared__ uint32_t lcn[kMaxBits + 1], dcn[kMaxBits + 1];
+  __shared__ ClLds hcl;  // (lane 0's, while it reads a header)
   __shared__ uint32_t slim[2][kMaxBits + 1];
   __shared__ uint16_t ls[kLitSyms];
   __shared__ uint8_t ds[kDistSyms];
@@ -144,7 +266,7 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
   const uint32_t seg = blockIdx.x;
   if (seg >= a.n_lanes) return;
   LaneTables<LdsStore> tab;
-  tab.s = LdsStore{lb, db, ls, ds};
+  tab.s = LdsStore{lb, db, lcn, dcn, ls, ds};
   const uint32_t f = a.lane_file[seg];
   const Bits in{a.in + a.file_word[f]};
   const uint64_t limit = a.file_bits[f];
@@ -168,7 +290,7 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
     if (j == 0) {
       uint64_t q = pos;
       uint32_t bf = 0, stl = 0;
-      const int bt = read_block_header(in, q, tab, bf, stl);
+      const int bt = read_block_header(in, q, tab, hcl, bf, stl);
       s_bt = bt;
       s_bfinal = bf;
       s_body0 = q;
@@ -335,8 +457,8 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
         break;
       }
       uint32_t* dst = out + n_out + (incl - valid);
-      for (uint32_t i = 0; i < n1; ++i) dst[i] = p1[i];
-      for (uint32_t i = 0; i < n2; ++i) dst[n1 + i] = p2[i];
+      copy_tokens(dst, p1, n1);
+      copy_tokens(dst + n1, p2, n2);
       n_out += total;
       out_bytes += tb;
       pos = e_end;
@@ -357,33 +479,39 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
   }
 }
 
-// One workgroup per segment, its output written in order in steps of up to
-// 256 tokens / kExpandBytes bytes: every byte of a step staged in LDS as a
-// literal (0x80000000 | byte), a position before the segment (a pointer the
-// resolve pass follows: the segment before is not expanded yet), the value of
-// an earlier step's byte (read back from val: a literal or such a pointer),
-// or kIntra | the step byte it copies; kIntra pointers are then followed
-// inside the step by pointer jumping, and the step goes to val in one
-// coalesced pass.  So pointers left in val reach only into earlier segments
-// and the resolve chains are short.
-constexpr int kExpandThreads = 256;
+// One workgroup per segment, its output built in order in steps of up to
+// 1024 tokens / kExpandBytes bytes.  The segment's last 32 KB of output stay
+// in an LDS ring (u16 per byte: a literal, or a back-reference to before
+// the segment as its distance from the segment's start), so every
+// back-reference inside the segment is an LDS read: a step's bytes are
+// staged as literals, pointers to before the segment (the segment before is
+// not expanded yet: the resolve pass follows them), ring values, or kIntra |
+// the step byte they copy; kIntra pointers are followed inside the step by
+// pointer jumping, and the step goes to val (coalesced) and to the ring.
+// So pointers left in val reach only into earlier segments and the resolve
+// chains are short.
+constexpr int kExpandThreads = 1024;
 constexpr uint32_t kExpandBytes = 8192;
-constexpr uint32_t kIntra = 0x40000000u;  // (batch text < 2^30 bytes: pointers leave bit 30 clear)
+constexpr uint32_t kRing = 32768;          // the DEFLATE window
+constexpr uint32_t kIntra = 0x40000000u;   // (batch text < 2^30 bytes: pointers leave bit 30 clear)
+constexpr uint16_t kRingPtr = 0x8000u;     // ring entry: pointer to o0 - 1 - (entry & 0x7FFF)
 __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflatePlace a) {
   __shared__ uint32_t v[kExpandBytes];
+  __shared__ uint16_t ring[kRing];
   __shared__ uint32_t s_take, s_bytes;
   __shared__ uint32_t wsum[kExpandThreads / 64];
   const uint32_t seg = blockIdx.x;
   const uint32_t tid = threadIdx.x, ln = tid & 63u, wave = tid >> 6;
   const uint32_t* tok = a.tok + a.tok_off[seg];
   const uint64_t n = a.n_tok[seg];
-  const uint64_t o0 = a.lane_out[seg];                     // the segment's first text position
-  const uint64_t f0 = a.file_text[a.lane_file[seg]];      // its file's
+  const uint64_t o0 = a.lane_out[seg];                 // the segment's first text position
+  const uint64_t f0 = a.file_text[a.lane_file[seg]];  // its file's
   uint64_t base = o0;
   bool bad = false;
+  uint32_t tk_next = tid < n ? tok[tid] : 0u;  // (the next step's token, loaded a step ahead)
   for (uint64_t t0 = 0; t0 < n;) {
     const uint64_t ti = t0 + tid;
-    const uint32_t tk = ti < n ? tok[ti] : 0u;
+    const uint32_t tk = tk_next;
     const uint32_t len = ti < n ? tok_len(tk) : 0u;
     uint32_t inc = len;
 #pragma unroll
@@ -420,9 +548,14 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
           for (uint32_t k = 0; k < len; ++k) {
             const uint64_t s = src + k;
             uint32_t x;
-            if (s >= base) x = kIntra | (uint32_t)(s - base);
-            else if (s < o0) x = (uint32_t)s;
-            else x = __hip_atomic_load(&a.val[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (s >= base) {
+              x = kIntra | (uint32_t)(s - base);
+            } else if (s < o0) {
+              x = (uint32_t)s;
+            } else {
+              const uint32_t r = ring[(uint32_t)s & (kRing - 1)];
+              x = r & kRingPtr ? (uint32_t)(o0 - 1 - (r & 0x7FFFu)) : 0x80000000u | r;
+            }
             v[before + k] = x;
           }
         }
@@ -430,6 +563,10 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
     }
     __syncthreads();
     const uint32_t nb = s_bytes, nt = s_take;
+    {
+      const uint64_t tn = t0 + nt + tid;  // the next step's token (in flight during this step's LDS work)
+      tk_next = tn < n ? tok[tn] : 0u;
+    }
     for (;;) {  // kIntra pointers followed inside the step (each points to an earlier byte)
       bool more = false;
       for (uint32_t i = tid; i < nb; i += kExpandThreads) {
@@ -442,40 +579,60 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
       }
       if (!__syncthreads_or(more)) break;
     }
-    for (uint32_t i = tid; i < nb; i += kExpandThreads) a.val[base + i] = v[i];
-    __threadfence();
+    for (uint32_t i = tid; i < nb; i += kExpandThreads) {
+      const uint32_t x = v[i];
+      a.val[base + i] = x;
+      ring[(uint32_t)(base + i) & (kRing - 1)] =
+          x >> 31 ? (uint16_t)(x & 0xFFu) : (uint16_t)(kRingPtr | (uint32_t)(o0 - 1 - x));
+    }
     __syncthreads();
     base += nb;
     t0 += nt;
   }
+  // a file's last segment: the padding up to the next file ('\n' parses as nothing)
+  for (uint64_t i = base + tid; i < a.lane_pad[seg]; i += kExpandThreads) a.val[i] = 0x80000000u | '\n';
   if (bad) atomicOr(a.flags, 1u);
 }
 
-// Pointers followed to their literals; 16 output bytes per thread, written
-// as one store; every resolved byte is written back as a literal.
-__global__ __launch_bounds__(256) void inflate_resolve_kernel(uint32_t* __restrict__ val, uint8_t* __restrict__ text,
-                                                              uint64_t n, uint32_t* __restrict__ flags) {
+// Pointers (into earlier segments) followed to their literals: 16 output
+// bytes per thread from one 64-byte load of val, every pointer of the 16
+// followed at once (independent loads), hop after hop until none is left
+// (one or two hops: a pointer's target is a literal or, if it lies in the
+// first 32 KB of its own segment, a pointer one segment further back).
+__global__ __launch_bounds__(256) void inflate_resolve_kernel(const uint32_t* __restrict__ val,
+                                                              uint8_t* __restrict__ text, uint64_t n,
+                                                              uint32_t* __restrict__ flags) {
   for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g * 16 < n; g += (uint64_t)gridDim.x * 256) {
+    uint32_t x[16];
+    if (g * 16 + 16 <= n) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 w = *(const uint4*)(val + g * 16 + 4 * q);
+        x[4 * q] = w.x;
+        x[4 * q + 1] = w.y;
+        x[4 * q + 2] = w.z;
+        x[4 * q + 3] = w.w;
+      }
+    } else {
+#pragma unroll
+      for (int b = 0; b < 16; ++b) x[b] = g * 16 + b < n ? val[g * 16 + b] : 0x80000000u | '\n';
+    }
+    for (uint32_t hop = 0;; ++hop) {
+      bool any = false;
+#pragma unroll
+      for (int b = 0; b < 16; ++b) any |= !(x[b] >> 31);
+      if (!any) break;
+      if (hop > 64) {  // (cannot happen: every pointer goes back a segment)
+        atomicOr(flags, 2u);
+        break;
+      }
+#pragma unroll
+      for (int b = 0; b < 16; ++b)
+        if (!(x[b] >> 31)) x[b] = val[x[b]];
+    }
     uint32_t out[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int b = 0; b < 16; ++b) {
-      const uint64_t i = g * 16 + b;
-      uint32_t byte = '\n';  // (positions between files: the parser's padding)
-      if (i < n) {
-        uint32_t v = val[i];
-        uint32_t hops = 0;
-        while (!(v >> 31)) {
-          v = __atomic_load_n(&val[v], __ATOMIC_RELAXED);
-          if (++hops > (1u << 22)) {  // (cannot happen: every pointer goes back)
-            atomicOr(flags, 2u);
-            break;
-          }
-        }
-        if (hops) __atomic_store_n(&val[i], v, __ATOMIC_RELAXED);
-        byte = v & 0xFFu;
-      }
-      out[b >> 2] |= byte << (8 * (b & 3));
-    }
+    for (int b = 0; b < 16; ++b) out[b >> 2] |= (x[b] & 0xFFu) << (8 * (b & 3));
     if (g * 16 + 16 <= n) *(uint4*)(text + g * 16) = make_uint4(out[0], out[1], out[2], out[3]);
     else
       for (int b = 0; b < 16 && g * 16 + b < n; ++b) text[g * 16 + b] = (uint8_t)(out[b >> 2] >> (8 * (b & 3)));
@@ -563,14 +720,20 @@ __global__ __launch_bounds__(kCrcThreads) void inflate_crc_seg_kernel(const uint
   seg_crc[g] = ~c;
 }
 
-__global__ __launch_bounds__(64) void inflate_crc_fold_kernel(const uint8_t* __restrict__ text,
-                                                              const uint64_t* __restrict__ file_text,
-                                                              const uint64_t* __restrict__ file_len,
-                                                              const uint32_t* __restrict__ seg_first,
-                                                              const uint32_t* __restrict__ seg_crc, uint32_t n_files,
-                                                              uint32_t* __restrict__ crc_out) {
+// One workgroup per file: each thread folds a contiguous run of the file's
+// segments, then the runs are folded pairwise in a tree.
+constexpr int kFoldThreads = 256;
+__global__ __launch_bounds__(kFoldThreads) void inflate_crc_fold_kernel(const uint8_t* __restrict__ text,
+                                                                        const uint64_t* __restrict__ file_text,
+                                                                        const uint64_t* __restrict__ file_len,
+                                                                        const uint32_t* __restrict__ seg_first,
+                                                                        const uint32_t* __restrict__ seg_crc,
+                                                                        uint32_t n_files, uint32_t* __restrict__ crc_out) {
   __shared__ uint32_t x2k[64];
-  if (threadIdx.x == 0) {  // x^(2^k) mod P
+  __shared__ uint32_t pc[kFoldThreads];
+  __shared__ uint64_t pl[kFoldThreads];
+  const uint32_t tid = threadIdx.x;
+  if (tid == 0) {  // x^(2^k) mod P
     uint32_t p = 1u << 30;  // x^1
     for (int k = 0; k < 64; ++k) {
       x2k[k] = p;
@@ -578,18 +741,34 @@ __global__ __launch_bounds__(64) void inflate_crc_fold_kernel(const uint8_t* __r
     }
   }
   __syncthreads();
-  const uint32_t f = blockIdx.x * 64 + threadIdx.x;
-  if (f >= n_files) return;
+  const uint32_t f = blockIdx.x;
   const uint64_t len = file_len[f];
+  const uint32_t g0 = seg_first[f], ns = seg_first[f + 1] - g0;
+  const uint32_t per = (ns + kFoldThreads - 1) / kFoldThreads;
+  const uint32_t a0 = min(ns, tid * per), a1 = min(ns, a0 + per);
   const uint32_t xseg = crc_x8n(kCrcSeg, x2k);
-  uint32_t crc = 0;  // of the bytes so far (standard CRC-32; 0 for none)
-  for (uint32_t g = seg_first[f]; g < seg_first[f + 1]; ++g) {
-    const uint64_t off = (uint64_t)(g - seg_first[f]) * kCrcSeg;
-    const uint64_t bl = min<uint64_t>(kCrcSeg, len - off);
-    crc = crc_mul(bl == kCrcSeg ? xseg : crc_x8n(bl, x2k), crc) ^ seg_crc[g];
+  uint32_t crc = 0;  // of this thread's run (standard CRC-32; 0 for none)
+  uint64_t bytes = 0;
+  for (uint32_t k = a0; k < a1; ++k) {
+    const uint64_t bl = min<uint64_t>(kCrcSeg, len - (uint64_t)k * kCrcSeg);
+    crc = crc_mul(bl == kCrcSeg ? xseg : crc_x8n(bl, x2k), crc) ^ seg_crc[g0 + k];
+    bytes += bl;
   }
-  crc_out[f] = crc;
-  crc_out[n_files + f] = len ? text[file_text[f]] : 0u;  // (the caller checks the format: FASTA starts with '>')
+  pc[tid] = crc;
+  pl[tid] = bytes;
+  __syncthreads();
+  for (uint32_t w = 1; w < kFoldThreads; w <<= 1) {  // crc(A || B) = x^(8|B|) crc(A) ^ crc(B)
+    if ((tid & (2 * w - 1)) == 0) {
+      const uint64_t lb = pl[tid + w];
+      pc[tid] = (lb ? crc_mul(crc_x8n(lb, x2k), pc[tid]) : pc[tid]) ^ pc[tid + w];
+      pl[tid] += lb;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    crc_out[f] = pc[0];
+    crc_out[n_files + f] = len ? text[file_text[f]] : 0u;  // (the caller checks the format: FASTA starts with '>')
+  }
 }
 
 }  // namespace
@@ -625,7 +804,7 @@ hipError_t launch_inflate_place(const InflatePlace& a, uint64_t text_len, uint8_
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (n_files)
-    hipLaunchKernelGGL(inflate_crc_fold_kernel, dim3((n_files + 63) / 64), dim3(64), 0, st, text, file_text, file_len,
+    hipLaunchKernelGGL(inflate_crc_fold_kernel, dim3(n_files), dim3(kFoldThreads), 0, st, text, file_text, file_len,
                        seg_first, seg_crc, n_files, crc);
   return hipGetLastError();
 }

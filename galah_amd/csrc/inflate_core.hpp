@@ -33,6 +33,7 @@ namespace inflate {
 // The DEFLATE stream of one gzip member, as 32-bit little-endian words with
 // at least two words of padding after its last byte; bit positions count
 // from the member's first deflate byte, LSB first (RFC 1951 3.1.1).
+// (The header functions below take any reader with Bits' peek / get.)
 struct Bits {
   const uint32_t* w;
   // the 32 stream bits starting at pos, the first in bit 0
@@ -168,59 +169,92 @@ GG_HD uint32_t dist_extra(uint32_t d) { return d < 4 ? 0u : (d - 2) >> 1; }
 
 constexpr uint8_t kClOrder[kClSyms] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15};
 
-// The code-length code of a dynamic header: its 19 lengths (packed 3 bits
-// each into cl_lens), its canonical code and the symbols sorted.
+// The code-length code of a dynamic header.  Its limits live in registers
+// (indexed by constants only); the bases, the symbols sorted by (length,
+// value) and a scratch row of offsets are indexed by data, so they live in
+// a store (host: arrays; device: a few bytes of the lane's LDS):
+//   int32_t& base(int l); uint8_t& sym(int i); uint8_t& off(int l)
+constexpr int kClBits = 7;  // longest code-length code
 struct ClCode {
-  Canon c{};
-  uint8_t sym[kClSyms];
+  uint32_t limit[kClBits + 1];  // left-justified 7-bit codes below limit[l] have length <= l
+};
+struct ClArrays {
+  int32_t b[kClBits + 1];
+  uint8_t s[kClSyms + 1];
+  uint8_t o[kClBits + 1];
+  int32_t& base(int l) { return b[l]; }
+  uint8_t& sym(int i) { return s[i]; }
+  uint8_t& off(int l) { return o[l]; }
 };
 
-// Reads HCLEN + 4 code-length-code lengths at pos; false if the code is not
-// complete (zlib refuses an incomplete code-length code).
-GG_HD bool read_cl_code(const Bits& in, uint64_t& pos, uint32_t hclen, ClCode& cl) {
-  uint32_t lens[kClSyms];
+// The length of code-length symbol s, from the header's HCLEN + 4 fields
+// (3 bits each, in kClOrder) packed into f.
+constexpr uint8_t kClField[kClSyms] = {3, 17, 15, 13, 11, 9, 7, 5, 4, 6, 8, 10, 12, 14, 16, 18, 0, 1, 2};
+GG_HD uint32_t cl_len(uint64_t f, uint32_t hclen, int s) {
+  return kClField[s] < hclen ? (uint32_t)(f >> (3 * kClField[s])) & 7u : 0u;
+}
+
+// The code-length code at pos (pos + 17 of the header; hclen = HCLEN + 4);
+// false if it is not complete (zlib refuses an incomplete code-length code).
+// pos is moved past its fields.
+template <class ClS, class B>
+GG_HD bool read_cl_code(const B& in, uint64_t& pos, uint32_t hclen, ClCode& cl, ClS& st) {
+  const uint64_t f = (uint64_t)in.peek(pos) | ((uint64_t)in.peek(pos + 32) << 32);
+  pos += 3 * hclen;
+  uint32_t count[kClBits + 1];
 #pragma unroll
-  for (int i = 0; i < kClSyms; ++i) lens[i] = 0;
-  for (uint32_t i = 0; i < hclen; ++i) lens[kClOrder[i]] = in.get(pos, 3);
-  uint32_t count[kMaxBits + 1];
+  for (int l = 0; l <= kClBits; ++l) count[l] = 0;
 #pragma unroll
-  for (int l = 0; l <= kMaxBits; ++l) count[l] = 0;
+  for (int s = 0; s < kClSyms; ++s) {
+    const uint32_t l = cl_len(f, hclen, s);
 #pragma unroll
-  for (int i = 0; i < kClSyms; ++i) count[lens[i]] += 1;
-  count[0] = 0;
-  int max_len;
-  if (canon_from_counts(count, cl.c, max_len) != 0) return false;  // incomplete or over-subscribed
-  uint32_t offs[8];
-  uint32_t o = 0;
-#pragma unroll
-  for (int l = 0; l < 8; ++l) {
-    offs[l] = o;
-    if (l) o += count[l];
+    for (int m = 1; m <= kClBits; ++m) count[m] += l == (uint32_t)m ? 1u : 0u;
   }
+  int left = 1;
+  uint32_t first = 0, offs = 0;
 #pragma unroll
-  for (int s = 0; s < kClSyms; ++s)
-    if (lens[s]) cl.sym[offs[lens[s]]++] = (uint8_t)s;
+  for (int l = 1; l <= kClBits; ++l) {
+    left = (left << 1) - (int)count[l];
+    cl.limit[l] = (first + count[l]) << (kClBits - l);
+    st.base(l) = (int32_t)offs - (int32_t)first;
+    st.off(l) = (uint8_t)offs;
+    offs += count[l];
+    first = (first + count[l]) << 1;
+  }
+  cl.limit[0] = 0;
+  if (left != 0) return false;  // incomplete or over-subscribed
+#pragma unroll
+  for (int s = 0; s < kClSyms; ++s) {
+    const uint32_t l = cl_len(f, hclen, s);
+    if (l) {
+      const uint8_t o = st.off((int)l);
+      st.sym(o) = (uint8_t)s;
+      st.off((int)l) = (uint8_t)(o + 1);
+    }
+  }
   return true;
 }
 
-GG_HD int decode_sym(const Bits& in, uint64_t& pos, const Canon& c, const uint8_t* sym8, const uint16_t* sym16) {
-  const uint32_t x = rev15(in.peek(pos));
-  const int L = code_len(c, x);
-  if (L > kMaxBits) return -1;
+template <class ClS, class B>
+GG_HD int decode_cl_sym(const B& in, uint64_t& pos, const ClCode& cl, ClS& st) {
+  const uint32_t x = rev15(in.peek(pos)) >> (kMaxBits - kClBits);  // left-justified 7 bits
+  int L = 1;
+#pragma unroll
+  for (int l = 1; l < kClBits; ++l) L += x >= cl.limit[l] ? 1 : 0;
+  if (x >= cl.limit[kClBits]) return -1;
   pos += (uint32_t)L;
-  const int idx = c.base[L] + (int)(x >> (kMaxBits - L));
-  return sym8 ? sym8[idx] : sym16[idx];
+  return st.sym(st.base(L) + (int)(x >> (kClBits - L)));
 }
 
 // Walks the lit/len + distance code lengths of a dynamic header (after the
 // code-length code), calling f(symbol index, length) for each nonzero
 // length (f returns false to stop: the walk then fails); false on a
 // malformed sequence.
-template <class F>
-GG_HD bool walk_lengths(const Bits& in, uint64_t& pos, const ClCode& cl, uint32_t n, F&& f) {
+template <class ClS, class F, class B>
+GG_HD bool walk_lengths(const B& in, uint64_t& pos, const ClCode& cl, ClS& st, uint32_t n, F&& f) {
   uint32_t i = 0, prev = 0;
   while (i < n) {
-    const int s = decode_sym(in, pos, cl.c, cl.sym, nullptr);
+    const int s = decode_cl_sym(in, pos, cl, st);
     if (s < 0) return false;
     if (s < 16) {
       if (s && !f(i, (uint32_t)s)) return false;
@@ -248,14 +282,12 @@ GG_HD bool walk_lengths(const Bits& in, uint64_t& pos, const ClCode& cl, uint32_
   return true;
 }
 
-// Is there a valid dynamic-block header at pos?  (The search's test: a
-// complete code-length code, length sequence in range, an end-of-block
-// code, lit/len and distance codes zlib accepts.)  On success pos is moved
-// past the header.
 // The search's first filter, from registers only: BTYPE 10 (dynamic), HLIT
 // and HDIST in range, and a complete code-length code (its Kraft sum over
-// the 3-bit lengths, sum 2^(7 - len) = 128).  Passes ~1% of positions.
-GG_HD bool block_header_quick(const Bits& in, uint64_t pos) {
+// the 3-bit lengths, sum 2^(7 - len) = 128).  Passes ~0.1% of the
+// positions of a zlib stream.
+template <class B>
+GG_HD bool block_header_quick(const B& in, uint64_t pos) {
   const uint32_t h = in.peek(pos);
   if (((h >> 1) & 3u) != 2u) return false;  // BTYPE 10: dynamic Huffman
   if (((h >> 3) & 31u) > 29u || ((h >> 8) & 31u) > 29u) return false;  // HLIT <= 286, HDIST <= 30
@@ -270,48 +302,52 @@ GG_HD bool block_header_quick(const Bits& in, uint64_t pos) {
   return kraft == 128u;
 }
 
-GG_HD bool block_header_ok(const Bits& in, uint64_t& pos) {
+// Is there a valid dynamic-block header at pos?  (The search's test: a
+// complete code-length code, length sequence in range, an end-of-block
+// code, lit/len and distance codes zlib accepts -- complete, or a single
+// code of length 1, or, for distances, none.)  The codes are judged by
+// their Kraft sums as the lengths are walked (in units of 2^-15; an
+// over-subscribed code stops the walk: most positions that pass the quick
+// filter fail within a few dozen lengths), with no table built.  On
+// success pos is moved past the header.
+template <class ClS, class B>
+GG_HD bool block_header_ok(const B& in, uint64_t& pos, ClS& st) {
   if (!block_header_quick(in, pos)) return false;
   const uint32_t h = in.peek(pos);
   const uint32_t hlit = ((h >> 3) & 31u) + 257u, hdist = ((h >> 8) & 31u) + 1u, hclen = ((h >> 13) & 15u) + 4u;
   uint64_t p = pos + 17;
   ClCode cl;
-  if (!read_cl_code(in, p, hclen, cl)) return false;
-  uint32_t lc[kMaxBits + 1], dc[kMaxBits + 1];
-#pragma unroll
-  for (int l = 0; l <= kMaxBits; ++l) lc[l] = dc[l] = 0;
+  if (!read_cl_code(in, p, hclen, cl, st)) return false;
   bool eob = false;
-  // Kraft sums in units of 2^-15: an over-subscribed code stops the walk
-  // (most positions that pass the code-length code fail within a few lengths)
-  uint32_t kl = 0, kd = 0;
-  if (!walk_lengths(in, p, cl, hlit + hdist, [&](uint32_t i, uint32_t len) {
+  uint32_t kl = 0, kd = 0, nd = 0, ml = 0, md = 0;
+  if (!walk_lengths(in, p, cl, st, hlit + hdist, [&](uint32_t i, uint32_t len) {
         if (i < hlit) {
-          lc[len] += 1;
-          if (i == 256) eob = true;
+          eob |= i == 256;
           kl += 1u << (kMaxBits - len);
+          ml = len > ml ? len : ml;
           return kl <= (1u << kMaxBits);
         }
-        dc[len] += 1;
         kd += 1u << (kMaxBits - len);
+        ++nd;
+        md = len > md ? len : md;
         return kd <= (1u << kMaxBits);
       }))
     return false;
   if (!eob) return false;
-  Canon c{};
-  int ml = 0;
-  int r = canon_from_counts(lc, c, ml);
-  if (!code_ok(r, ml, false)) return false;
-  r = canon_from_counts(dc, c, ml);
-  if (!code_ok(r, ml, true)) return false;
+  // (code_ok: complete, or incomplete with its longest code of length 1)
+  if (kl != (1u << kMaxBits) && ml != 1) return false;
+  if (nd && kd != (1u << kMaxBits) && md != 1) return false;
   pos = p;
   return true;
 }
 
 // One lane's tables for its current block.  The limits are indexed by
-// constants only (code_len unrolled: registers on the device); the bases and
-// the symbols sorted by (length, value) are indexed by data, so they live in
-// the Store (host: arrays; device: the lane's LDS):
-//   int32_t& lbase(int), dbase(int); uint16_t& lsym(int); uint8_t& dsym(int)
+// constants only (code_len unrolled: registers on the device); the bases,
+// the symbols sorted by (length, value) and the per-length counts a header
+// read keeps are indexed by data, so they live in the Store (host: arrays;
+// device: LDS):
+//   int32_t& lbase(int), dbase(int); uint32_t& lcnt(int), dcnt(int);
+//   uint16_t& lsym(int); uint8_t& dsym(int)
 template <class Store>
 struct LaneTables {
   uint32_t llim[kMaxBits + 1], dlim[kMaxBits + 1];
@@ -350,13 +386,17 @@ struct LaneTables {
   }
 };
 
-// Host store: plain arrays.
+// Host store: plain arrays.  (lcnt / dcnt: counts per length, then the
+// next slot per length, while a header is read.)
 struct ArrayStore {
   int32_t lb[kMaxBits + 1], db[kMaxBits + 1];
+  uint32_t lc[kMaxBits + 1], dc[kMaxBits + 1];
   uint16_t ls[kLitSyms];
   uint8_t ds[kDistSyms];
   int32_t& lbase(int l) { return lb[l]; }
   int32_t& dbase(int l) { return db[l]; }
+  uint32_t& lcnt(int l) { return lc[l]; }
+  uint32_t& dcnt(int l) { return dc[l]; }
   uint16_t& lsym(int i) { return ls[i]; }
   uint8_t& dsym(int i) { return ds[i]; }
 };
@@ -365,8 +405,8 @@ struct ArrayStore {
 // btype (0 stored, 1 fixed, 2 dynamic) or -1 on a malformed header; bfinal
 // receives the BFINAL bit.  For a stored block pos ends at its first data
 // byte and stored_len receives LEN.
-template <class Store>
-GG_HD int read_block_header(const Bits& in, uint64_t& pos, LaneTables<Store>& t, uint32_t& bfinal,
+template <class Store, class ClS>
+GG_HD int read_block_header(const Bits& in, uint64_t& pos, LaneTables<Store>& t, ClS& cls, uint32_t& bfinal,
                             uint32_t& stored_len) {
   const uint32_t h = in.peek(pos);
   bfinal = h & 1u;
@@ -380,7 +420,7 @@ GG_HD int read_block_header(const Bits& in, uint64_t& pos, LaneTables<Store>& t,
     stored_len = len;
     return 0;
   }
-  uint32_t lc[kMaxBits + 1], dc[kMaxBits + 1];
+  uint32_t lc[kMaxBits + 1], dc[kMaxBits + 1];  // (indexed by constants only)
 #pragma unroll
   for (int l = 0; l <= kMaxBits; ++l) lc[l] = dc[l] = 0;
   int ml = 0;
@@ -410,21 +450,28 @@ GG_HD int read_block_header(const Bits& in, uint64_t& pos, LaneTables<Store>& t,
   if (hlit > 286 || hdist > 30) return -1;
   uint64_t p = pos + 17;
   ClCode cl;
-  if (!read_cl_code(in, p, hclen, cl)) return -1;
+  if (!read_cl_code(in, p, hclen, cl, cls)) return -1;
   const uint64_t lens_at = p;
   bool eob = false;
-  // pass 1: counts per length
-  if (!walk_lengths(in, p, cl, hlit + hdist, [&](uint32_t i, uint32_t len) {
+  // pass 1: counts per length (in the store: indexed by data)
+#pragma unroll
+  for (int l = 0; l <= kMaxBits; ++l) t.s.lcnt(l) = t.s.dcnt(l) = 0;
+  if (!walk_lengths(in, p, cl, cls, hlit + hdist, [&](uint32_t i, uint32_t len) {
         if (i < hlit) {
-          lc[len] += 1;
-          if (i == 256) eob = true;
+          t.s.lcnt((int)len) += 1;
+          eob |= i == 256;
         } else {
-          dc[len] += 1;
+          t.s.dcnt((int)len) += 1;
         }
         return true;
       }))
     return -1;
   if (!eob) return -1;
+#pragma unroll
+  for (int l = 1; l <= kMaxBits; ++l) {
+    lc[l] = t.s.lcnt(l);
+    dc[l] = t.s.dcnt(l);
+  }
   int r = canon_from_counts(lc, c, ml);
   if (!code_ok(r, ml, false)) return -1;
   t.set_lit(c);
@@ -432,20 +479,19 @@ GG_HD int read_block_header(const Bits& in, uint64_t& pos, LaneTables<Store>& t,
   if (!code_ok(r, ml, true)) return -1;
   t.set_dist(c);
   // pass 2: symbols sorted by (length, value) (the lengths are walked again
-  // instead of being stored)
-  uint32_t lo[kMaxBits + 1], doff[kMaxBits + 1];
+  // instead of being stored); lcnt / dcnt become each length's next slot
   uint32_t a = 0, b = 0;
 #pragma unroll
   for (int l = 1; l <= kMaxBits; ++l) {
-    lo[l] = a;
-    doff[l] = b;
+    t.s.lcnt(l) = a;
+    t.s.dcnt(l) = b;
     a += lc[l];
     b += dc[l];
   }
   uint64_t q = lens_at;
-  walk_lengths(in, q, cl, hlit + hdist, [&](uint32_t i, uint32_t len) {
-    if (i < hlit) t.s.lsym((int)lo[len]++) = (uint16_t)i;
-    else t.s.dsym((int)doff[len]++) = (uint8_t)(i - hlit);
+  walk_lengths(in, q, cl, cls, hlit + hdist, [&](uint32_t i, uint32_t len) {
+    if (i < hlit) t.s.lsym((int)t.s.lcnt((int)len)++) = (uint16_t)i;
+    else t.s.dsym((int)t.s.dcnt((int)len)++) = (uint8_t)(i - hlit);
     return true;
   });
   pos = p;
@@ -471,9 +517,9 @@ enum DecodeStatus : uint32_t {
 // the BFINAL block), writing tokens through emit(t) (returns false when
 // full).  out_len receives the bytes the tokens stand for, last_end the bit
 // position after the last decoded block.
-template <class Store, class Emit>
+template <class Store, class ClS, class Emit>
 GG_HD uint32_t decode_blocks(const Bits& in, uint64_t pos, uint64_t end, uint64_t limit_bits, LaneTables<Store>& t,
-                             Emit&& emit, uint64_t& out_len, uint64_t& last_end, uint32_t& bfinal_seen) {
+                             ClS& cls, Emit&& emit, uint64_t& out_len, uint64_t& last_end, uint32_t& bfinal_seen) {
   out_len = 0;
   bfinal_seen = 0;
   last_end = pos;
@@ -487,7 +533,7 @@ GG_HD uint32_t decode_blocks(const Bits& in, uint64_t pos, uint64_t end, uint64_
       return kDecOverrun;
     }
     uint32_t bfinal = 0, stored = 0;
-    const int bt = read_block_header(in, pos, t, bfinal, stored);
+    const int bt = read_block_header(in, pos, t, cls, bfinal, stored);
     if (bt < 0) {
       last_end = pos;
       return kDecBad;

@@ -11,6 +11,7 @@
 // (libdeflate, which also reports a corrupt file).  So the device path
 // changes no result, only where the bytes are inflated.
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -61,23 +62,32 @@ gg_status hand_back(const char* why, uint32_t f) {
   if (inflate_debug()) fprintf(stderr, "[inflate] batch handed back to the host: %s (file %u of the batch)\n", why, f);
   return GG_OK;
 }
-constexpr uint32_t kChunkBytes = 4096;  // search granularity: a zlib -6 block of FASTA is ~25-30 KB
+constexpr uint32_t kChunkBytes = 16384;  // search granularity: a zlib -6 block of FASTA is ~25-30 KB
 constexpr int kMaxRelaunch = 8;         // decode passes that may drop wrong starts before giving up
 }  // namespace
 
 // files[f]: the deflate data of a gzip file (gz = true; data_off is 4-byte
 // aligned in h_in, isize/crc from its trailer) or plain text (gz = false).
 gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const std::vector<InflateFile>& files,
-                        uint8_t** d_text, std::vector<uint64_t>& foff, bool* ok) {
+                        uint8_t** d_text, std::vector<uint64_t>& foff, bool* ok, uint8_t* d_in) {
   *ok = false;
   hipStream_t st = m->stream;
+  // GALAHGPU_INFLATE_DEBUG=1: wall time of each stage (host + device), on stderr
+  const auto t_start = std::chrono::steady_clock::now();
+  auto stamp = [&](const char* what) {
+    if (inflate_debug())
+      fprintf(stderr, "[inflate] %-22s %8.3f ms\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
+  };
   const uint32_t nf = (uint32_t)files.size();
-  // the batch on the device (+ padding the cursors read past a file's end)
-  uint8_t* d_in;
-  const uint64_t in_alloc = (in_bytes + 15) / 16 * 16 + 64;
-  GG_HIP(m, scratch_t(m, "gz_in", in_alloc, &d_in));
-  GG_HIP(m, hipMemsetAsync(d_in + in_bytes, 0, in_alloc - in_bytes, st));
-  if (in_bytes) GG_HIP(m, hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, st));
+  // the batch on the device (+ padding that readers past the last file's
+  // end touch: a cursor's 3 words ahead, a header walk of a corrupt stream,
+  // at most 316 code lengths of <= 14 bits)
+  if (!d_in) {
+    GG_HIP(m, scratch_t(m, "gz_in", in_bytes + kInflatePad, &d_in));
+    if (in_bytes) GG_HIP(m, hipMemcpyAsync(d_in, h_in, in_bytes, hipMemcpyHostToDevice, st));
+  }
+  GG_HIP(m, hipMemsetAsync(d_in + in_bytes, 0, kInflatePad, st));
   std::vector<uint64_t> fword(nf), fbits(nf);
   std::vector<uint32_t> chunk_file;
   std::vector<uint64_t> chunk_bit0;
@@ -120,6 +130,7 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     GG_HIP(m, hipMemcpyAsync(start.data(), d_start, nc * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   }
   GG_HIP(m, hipStreamSynchronize(st));
+  stamp("copy + search");
   // lanes per file: the stream's first bit and every block start found
   std::vector<std::vector<uint64_t>> starts(nf);
   for (uint32_t f = 0; f < nf; ++f) {
@@ -128,145 +139,155 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     for (uint32_t c = first_chunk[f]; c < first_chunk[f + 1]; ++c)
       if (start[c] != ~0ull && start[c] > starts[f].back()) starts[f].push_back(start[c]);
   }
-  std::vector<uint32_t> lane_file, status, bfin;
-  std::vector<uint64_t> lane_start, lane_end, tok_off, tok_cap, scr_off, n_tok, out_len, last_end;
-  uint32_t *d_lfile = nullptr, *d_tok = nullptr, *d_scr = nullptr;
-  uint64_t *d_toff = nullptr, *d_res = nullptr;
+  // one lane (a wave of the decode kernel) per start: [start, end) up to the
+  // next start (~0: the file's last lane), its tokens in a region of the
+  // token buffer sized one per bit, its scratch likewise
+  struct Lane {
+    uint32_t file;
+    uint64_t start, end, tok_off, cap, scr_off;
+    uint64_t n_tok = 0, out_len = 0, last_end = 0;
+    uint32_t status = 0, bfin = 0;
+    bool redo = true, alive = true;
+  };
+  std::vector<Lane> lanes;
+  uint64_t toks = 0, scr = 0;
+  for (uint32_t f = 0; f < nf; ++f)
+    for (size_t i = 0; i < starts[f].size(); ++i) {
+      const uint64_t s0 = starts[f][i];
+      const uint64_t e = i + 1 < starts[f].size() ? starts[f][i + 1] : ~0ull;
+      // every symbol takes >= 1 bit: one token per bit bounds every lane
+      // (literal-heavy DNA blocks reach ~0.5 tokens per bit)
+      const uint64_t bits = (e == ~0ull ? fbits[f] : e) - s0;
+      Lane ln{f, s0, e, toks, bits + 64, scr};
+      lanes.push_back(ln);
+      toks += (bits + 64 + 3) / 4 * 4;
+      scr += inflate::decode_scratch(bits);
+    }
+  uint32_t *d_tok = nullptr, *d_scr = nullptr;
+  GG_HIP(m, scratch_t(m, "gz_tok", std::max<uint64_t>(toks, 4), &d_tok));
+  GG_HIP(m, scratch_t(m, "gz_scr", std::max<uint64_t>(scr, 4), &d_scr));
   for (int pass = 0;; ++pass) {
-    if (pass >= kMaxRelaunch) return hand_back("block starts did not chain", 0);  // (ok = false)
-    lane_file.clear();
-    lane_start.clear();
-    lane_end.clear();
-    tok_off.clear();
-    tok_cap.clear();
-    scr_off.clear();
-    uint64_t toks = 0, scr = 0;
-    for (uint32_t f = 0; f < nf; ++f)
-      for (size_t i = 0; i < starts[f].size(); ++i) {
-        const uint64_t s0 = starts[f][i];
-        const uint64_t e = i + 1 < starts[f].size() ? starts[f][i + 1] : ~0ull;
-        // every symbol takes >= 1 bit: one token per bit bounds every lane
-        // (literal-heavy DNA blocks reach ~0.5 tokens per bit)
-        const uint64_t bits = (e == ~0ull ? fbits[f] : e) - s0;
-        const uint64_t cap = bits + 64;
-        lane_file.push_back(f);
-        lane_start.push_back(s0);
-        lane_end.push_back(e);
-        tok_off.push_back(toks);
-        tok_cap.push_back(cap);
-        scr_off.push_back(scr);
-        toks += (cap + 3) / 4 * 4;
-        scr += inflate::decode_scratch(bits);
-      }
-    const uint32_t nl = (uint32_t)lane_file.size();
+    std::vector<uint32_t> redo;
+    for (uint32_t l = 0; l < (uint32_t)lanes.size(); ++l)
+      if (lanes[l].alive && lanes[l].redo) redo.push_back(l);
+    const uint32_t nl = (uint32_t)redo.size();
     if (nl == 0) break;
-    uint32_t *d_status, *d_bfin;
-    uint64_t *d_lstart, *d_lend, *d_tcap, *d_soff;
+    if (pass >= kMaxRelaunch) return hand_back("block starts did not chain", 0);  // (ok = false)
+    // the lanes to decode: 6 arrays of nl u64 (file, start, end, tok_off, cap, scr_off)
+    std::vector<uint64_t> arg((size_t)nl * 6);
+    for (uint32_t k = 0; k < nl; ++k) {
+      const Lane& x = lanes[redo[k]];
+      arg[k] = x.file;
+      arg[nl + k] = x.start;
+      arg[2 * (size_t)nl + k] = x.end;
+      arg[3 * (size_t)nl + k] = x.tok_off;
+      arg[4 * (size_t)nl + k] = x.cap;
+      arg[5 * (size_t)nl + k] = x.scr_off;
+    }
+    uint64_t *d_arg, *d_res;
+    uint32_t* d_lfile;
+    GG_HIP(m, scratch_t(m, "gz_larg", arg.size(), &d_arg));
     GG_HIP(m, scratch_t(m, "gz_lfile", nl, &d_lfile));
-    GG_HIP(m, scratch_t(m, "gz_lstart", nl, &d_lstart));
-    GG_HIP(m, scratch_t(m, "gz_lend", nl, &d_lend));
-    GG_HIP(m, scratch_t(m, "gz_toff", nl, &d_toff));
-    GG_HIP(m, scratch_t(m, "gz_tcap", nl, &d_tcap));
-    GG_HIP(m, scratch_t(m, "gz_soff", nl, &d_soff));
-    GG_HIP(m, scratch_t(m, "gz_tok", std::max<uint64_t>(toks, 4), &d_tok));
-    GG_HIP(m, scratch_t(m, "gz_scr", std::max<uint64_t>(scr, 4), &d_scr));
     // results contiguous: n_tok, out_len, last_end (u64), then status, bfinal (u32)
     GG_HIP(m, scratch_t(m, "gz_res", (size_t)nl * 4, &d_res));
-    d_status = (uint32_t*)(d_res + 3 * (size_t)nl);
-    d_bfin = d_status + nl;
-    GG_HIP(m, hipMemcpyAsync(d_lfile, lane_file.data(), nl * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync(d_lstart, lane_start.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync(d_lend, lane_end.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync(d_toff, tok_off.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync(d_tcap, tok_cap.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync(d_soff, scr_off.data(), nl * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    std::vector<uint32_t> lf(nl);
+    for (uint32_t k = 0; k < nl; ++k) lf[k] = lanes[redo[k]].file;
+    GG_HIP(m, hipMemcpyAsync(d_arg, arg.data(), arg.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync(d_lfile, lf.data(), nl * sizeof(uint32_t), hipMemcpyHostToDevice, st));
     InflateDecode d;
     d.in = (const uint32_t*)d_in;
     d.file_word = d_fword;
     d.file_bits = d_fbits;
     d.lane_file = d_lfile;
-    d.lane_start = d_lstart;
-    d.lane_end = d_lend;
+    d.lane_start = d_arg + nl;
+    d.lane_end = d_arg + 2 * (size_t)nl;
     d.n_lanes = nl;
     d.tok = d_tok;
-    d.tok_off = d_toff;
-    d.tok_cap = d_tcap;
+    d.tok_off = d_arg + 3 * (size_t)nl;
+    d.tok_cap = d_arg + 4 * (size_t)nl;
     d.scr = d_scr;
-    d.scr_off = d_soff;
+    d.scr_off = d_arg + 5 * (size_t)nl;
     d.n_tok = d_res;
     d.out_len = d_res + nl;
     d.last_end = d_res + 2 * (size_t)nl;
-    d.status = d_status;
-    d.bfinal = d_bfin;
+    d.status = (uint32_t*)(d_res + 3 * (size_t)nl);
+    d.bfinal = d.status + nl;
     GG_HIP(m, launch_inflate_decode(d, st));
     std::vector<uint64_t> res((size_t)nl * 4);
     GG_HIP(m, hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
-    n_tok.assign(res.begin(), res.begin() + nl);
-    out_len.assign(res.begin() + nl, res.begin() + 2 * nl);
-    last_end.assign(res.begin() + 2 * nl, res.begin() + 3 * nl);
+    stamp("decode pass");
     const uint32_t* r32 = (const uint32_t*)(res.data() + 3 * (size_t)nl);
-    status.assign(r32, r32 + nl);
-    bfin.assign(r32 + nl, r32 + 2 * nl);
-    // a lane that passed the next start without landing on it: that start is
-    // not a block boundary -- dropped, and the batch decoded again
-    bool again = false;
-    uint32_t l = 0;
-    for (uint32_t f = 0; f < nf; ++f) {
-      std::vector<uint64_t> keep;
-      bool drop_next = false;
-      for (size_t i = 0; i < starts[f].size(); ++i, ++l) {
-        if (drop_next) {
-          drop_next = false;
-          again = true;
-          continue;
-        }
-        keep.push_back(starts[f][i]);
-        if (status[l] == inflate::kDecOverrun && i + 1 < starts[f].size()) drop_next = true;
-        else if (status[l] != inflate::kDecOk)  // malformed / full / a second member: host path
-          return hand_back(status[l] == inflate::kDecFull ? "token capacity"
-                           : status[l] == inflate::kDecFinalEarly ? "stream ended early (several members?)"
-                                                                  : "malformed stream", f);
-      }
-      starts[f].swap(keep);
+    for (uint32_t k = 0; k < nl; ++k) {
+      Lane& x = lanes[redo[k]];
+      x.n_tok = res[k];
+      x.out_len = res[nl + k];
+      x.last_end = res[2 * (size_t)nl + k];
+      x.status = r32[k];
+      x.bfin = r32[nl + k];
+      x.redo = false;
     }
-    if (!again) break;
+    // a lane that passed the next start without landing on it: that start is
+    // not a block boundary -- the lane takes the next lane's range and token
+    // region (they follow its own) and is decoded again, alone
+    for (uint32_t l = 0; l < (uint32_t)lanes.size(); ++l) {
+      Lane& x = lanes[l];
+      if (!x.alive || x.redo) continue;
+      uint32_t nx = l + 1;
+      while (nx < lanes.size() && !lanes[nx].alive) ++nx;
+      const bool has_next = nx < lanes.size() && lanes[nx].file == x.file;
+      if (x.status == inflate::kDecOverrun && has_next) {
+        Lane& y = lanes[nx];
+        x.end = y.end;
+        x.cap = y.tok_off + y.cap - x.tok_off;
+        x.redo = true;
+        y.alive = false;
+      } else if (x.status != inflate::kDecOk) {  // malformed / full / a second member: host path
+        return hand_back(x.status == inflate::kDecFull ? "token capacity"
+                         : x.status == inflate::kDecFinalEarly ? "stream ended early (several members?)"
+                                                               : "malformed stream", x.file);
+      }
+    }
   }
+  std::vector<Lane> live;
+  for (const Lane& x : lanes)
+    if (x.alive) live.push_back(x);
   // every file: its last lane decoded the final block, ending at the trailer
   // (one member), and the output length agrees with ISIZE
-  std::vector<uint64_t> flen(nf, 0), lane_out(lane_file.size());
-  {
-    uint32_t l = 0;
-    for (uint32_t f = 0; f < nf; ++f) {
-      if (!files[f].gz) {
-        flen[f] = files[f].data_len;
-        continue;
-      }
-      for (size_t i = 0; i < starts[f].size(); ++i, ++l) {
-        lane_out[l] = flen[f];
-        flen[f] += out_len[l];
-        if (i + 1 == starts[f].size()) {
-          if (!bfin[l] || (last_end[l] + 7) / 8 != files[f].data_len) return hand_back("not one member", f);
-        }
-      }
+  std::vector<uint64_t> flen(nf, 0), lane_out(live.size());
+  for (size_t l = 0; l < live.size(); ++l) {
+    const uint32_t f = live[l].file;
+    lane_out[l] = flen[f];
+    flen[f] += live[l].out_len;
+    if (l + 1 == live.size() || live[l + 1].file != f) {
+      if (!live[l].bfin || (live[l].last_end + 7) / 8 != files[f].data_len) return hand_back("not one member", f);
       if ((uint32_t)flen[f] != files[f].isize) return hand_back("ISIZE", f);
     }
   }
+  for (uint32_t f = 0; f < nf; ++f)
+    if (!files[f].gz) flen[f] = files[f].data_len;
   foff.assign(nf + 1, 0);
   for (uint32_t f = 0; f < nf; ++f) foff[f + 1] = foff[f] + (flen[f] + 15) / 16 * 16;
   const uint64_t text_len = foff[nf];
   if (text_len >= (1ull << 30)) return hand_back("batch text over 1 GiB", 0);  // (30-bit expand pointers)
-  for (size_t l = 0; l < lane_out.size(); ++l) lane_out[l] += foff[lane_file[l]];
-  uint32_t *d_val, *d_flags, *d_crc;
+  for (size_t l = 0; l < lane_out.size(); ++l) lane_out[l] += foff[live[l].file];
+  uint32_t *d_val, *d_flags, *d_crc, *d_lfile;
   uint64_t *d_lout, *d_ftext, *d_flen;
   GG_HIP(m, scratch_t(m, "gz_val", std::max<uint64_t>(text_len, 1), &d_val));
   GG_HIP(m, scratch_t(m, "stage_text", std::max<uint64_t>(text_len, 16) + 16, d_text));
-  GG_HIP(m, scratch_t(m, "gz_lout", std::max<size_t>(lane_out.size(), 1), &d_lout));
+  // per live lane: text position, token offset, token count, end of the
+  // padding after it (its file's last lane: the next file's start; else 0)
+  // (u64), then its file (u32)
+  const size_t NL = std::max<size_t>(live.size(), 1);
+  GG_HIP(m, scratch_t(m, "gz_lout", 4 * NL + (NL + 1) / 2, &d_lout));
+  d_lfile = (uint32_t*)(d_lout + 4 * NL);
   GG_HIP(m, scratch_t(m, "gz_ftext", 2 * (size_t)nf + 1, &d_ftext));
   d_flen = d_ftext + nf;
   GG_HIP(m, scratch_t(m, "gz_flags", 2 * (size_t)nf + 1, &d_flags));
   d_crc = d_flags + 1;
-  GG_HIP(m, hipMemsetD32Async((hipDeviceptr_t)d_val, 0x80000000u | '\n', text_len, st));
+  for (uint32_t f = 0; f < nf; ++f)  // (plain files: their text is copied in after the resolve)
+    if (!files[f].gz && foff[f + 1] > foff[f])
+      GG_HIP(m, hipMemsetD32Async((hipDeviceptr_t)(d_val + foff[f]), 0x80000000u | '\n', foff[f + 1] - foff[f], st));
   GG_HIP(m, hipMemsetAsync(d_flags, 0, sizeof(uint32_t), st));
   std::vector<uint64_t> ftext(2 * (size_t)nf);
   for (uint32_t f = 0; f < nf; ++f) {
@@ -274,16 +295,24 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     ftext[nf + f] = flen[f];
   }
   GG_HIP(m, hipMemcpyAsync(d_ftext, ftext.data(), ftext.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-  if (!lane_out.empty())
-    GG_HIP(m, hipMemcpyAsync(d_lout, lane_out.data(), lane_out.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  std::vector<uint64_t> lv(4 * NL + (NL + 1) / 2, 0);
+  for (size_t l = 0; l < live.size(); ++l) {
+    lv[l] = lane_out[l];
+    lv[NL + l] = live[l].tok_off;
+    lv[2 * NL + l] = live[l].n_tok;
+    if (l + 1 == live.size() || live[l + 1].file != live[l].file) lv[3 * NL + l] = foff[live[l].file + 1];
+    ((uint32_t*)(lv.data() + 4 * NL))[l] = live[l].file;
+  }
+  GG_HIP(m, hipMemcpyAsync(d_lout, lv.data(), lv.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   InflatePlace p;
   p.tok = d_tok;
-  p.tok_off = d_toff;
-  p.n_tok = d_res;
+  p.tok_off = d_lout + NL;
+  p.n_tok = d_lout + 2 * NL;
+  p.lane_pad = d_lout + 3 * NL;
   p.lane_file = d_lfile;
   p.lane_out = d_lout;
   p.file_text = d_ftext;
-  p.n_lanes = (uint32_t)lane_out.size();
+  p.n_lanes = (uint32_t)live.size();
   p.val = d_val;
   p.flags = d_flags;
   std::vector<uint32_t> seg_first(nf + 1, 0);
@@ -303,6 +332,7 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   std::vector<uint32_t> chk(2 * (size_t)nf + 1);
   GG_HIP(m, hipMemcpyAsync(chk.data(), d_flags, chk.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   GG_HIP(m, hipStreamSynchronize(st));
+  stamp("expand + resolve + crc");
   if (chk[0]) return hand_back(chk[0] & 1 ? "distance before the file start" : "pointer chain", 0);
   for (uint32_t f = 0; f < nf; ++f)
     if (files[f].gz && (chk[1 + f] != files[f].crc || chk[1 + nf + f] != '>'))  // (FASTQ, malformed: the host path)

@@ -27,6 +27,7 @@
 // exactly one device on identical sketch rows.
 #include <algorithm>
 #include <chrono>
+#include <future>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -336,6 +337,14 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   hipStream_t st = m->stream;
   const uint32_t nf = (uint32_t)foff.size() - 1;
   const uint64_t bb = parse_block_bytes();
+  static const bool dbg = [] {
+    const char* e = getenv("GALAHGPU_INFLATE_DEBUG");
+    return e && *e == '1';
+  }();
+  const auto t0 = Clock::now();
+  auto stamp = [&](const char* what) {
+    if (dbg) fprintf(stderr, "[parse] %-12s %8.3f ms\n", what, ms_since(t0));
+  };
   std::vector<uint32_t> bfile;
   std::vector<uint64_t> bstart, bend;
   for (uint32_t f = 0; f < nf; ++f)
@@ -382,6 +391,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
     GG_HIP(m, parse_batch_pass(1, p, st));
     GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_nl, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
+    stamp("pass 1");
     uint64_t acc = 0;
     for (uint32_t b = 0; b < nb; ++b) {
       const uint64_t x = h[b];
@@ -394,6 +404,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
     GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_bases, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipMemcpyAsync(h2.data(), p.blk_last, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
+    stamp("pass 2");
     for (uint32_t b = 0; b < nb; ++b) fbases[bfile[b]] += h[b];
     for (uint32_t f = 0; f < nf; ++f) gofs[f + 1] = gofs[f] + (fbases[f] + 15) / 16 * 16;  // genomes on words
     {
@@ -420,6 +431,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
       GG_HIP(m, parse_batch_pass(3, p, st));
       GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_runs, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
       GG_HIP(m, hipStreamSynchronize(st));
+      stamp("pass 3");
       for (uint32_t b = 0; b < nb; ++b) {
         const uint64_t x = h[b];
         h[b] = n_starts;
@@ -446,6 +458,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
     GG_HIP(m, parse_batch_pass(5, p, st));
     if (n_starts) GG_HIP(m, hipMemcpyAsync(hs.data(), starts, n_starts * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
+    stamp("pass 4-5");
   }
   // runs: consecutive starts of one genome; a genome's last run ends at its
   // last base; keep runs of >= k bases
@@ -457,89 +470,211 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
     const uint64_t e = (r + 1 < n_starts && hs[r + 1] < gend) ? hs[r + 1] : gend;
     if (e - a >= (uint64_t)m->k) runs.push_back(gg_run{f, (uint32_t)(e - a), a});
   }
+  stamp("runs");
   return GG_OK;
 }
 
-// Grows m's pinned staging buffer to hold `need` bytes, keeping its first
-// `keep` bytes (at most ~2x need, up to `hint`).
-gg_status grow_pinned(gg_ctx* m, size_t need, size_t keep, size_t hint) {
-  if (need <= m->pinned_bytes) return GG_OK;
-  std::vector<uint8_t> kept((const uint8_t*)m->pinned, (const uint8_t*)m->pinned + keep);
-  void* stage;
-  GG_HIP(m, pinned(m, std::max(need, std::min<size_t>(2 * need, hint)), &stage));
-  if (keep) memcpy(stage, kept.data(), keep);
-  return GG_OK;
-}
-
-// One device-inflate batch of the streamed file list (GALAHGPU_INFLATE=
-// device): files [b0, b1) of the stream are staged as read (gzip files
-// compressed, each positioned so its deflate data starts on a 4-byte
-// boundary), inflated on m's device (inflate_host.cpp) and parsed there.
-// The batch is cut early at kBatchGzBytes of gzip data or kBatchGzText of
-// text (the rest goes back through cursor); row_of receives one row per
-// file taken.  A batch the device inflate does not take is decoded on the
-// host threads instead (counted in GG_FALLBACK_INFLATE_HOST).
-gg_status inflate_files_batch(gg_ctx* m, PackStream& stream, uint32_t b0, uint32_t b1, std::mutex& cursor_mu,
-                              uint32_t& cursor, bool& stop, bool& file_error, int copy_threads, uint32_t** d_words,
-                              uint64_t* nw, std::vector<gg_run>& runs, std::vector<uint32_t>& row_of,
-                              const std::vector<uint32_t>& miss_at, const char* const* names) {
-  struct Held {
-    uint64_t pos, len;
-    bool gz;
-  };
+// Device-inflate batches of the streamed file list (GALAHGPU_INFLATE=
+// device), pipelined per member: while the member inflates, parses and
+// sketches batch N on its stream, a helper thread stages batch N + 1 into
+// the member's other slot -- files read by the PackStream workers, copied
+// into the slot's pinned buffer (gzip files compressed, each positioned so
+// its deflate data starts on a 4-byte boundary) and queued to the slot's
+// device buffer on the slot's stream as they are staged.  A batch is cut
+// early at kBatchGzBytes of gzip data or kBatchGzText of text (the rest
+// goes back through the cursor).  A batch the device inflate does not take
+// is decoded on the host threads instead (GG_FALLBACK_INFLATE_HOST).
+struct GzHeld {
+  uint64_t pos, len;
+  bool gz;
+};
+struct GzStaged {
+  uint32_t b0 = 0, b1 = 0;  // the files taken
   std::vector<InflateFile> files;
-  std::vector<Held> held;
-  uint64_t at = 0, gz_bytes = 0, text_est = 0;
-  bool host_only = false;
-  for (uint32_t i = b0; i < b1; ++i) {
-    const std::vector<uint8_t>* tx;
-    bool gz = false;
-    std::string err;
-    const gg_status gs = stream.get_raw(i, &tx, &err, &gz);
-    if (gs != GG_OK) {
-      std::lock_guard<std::mutex> lk(cursor_mu);
-      if (!stop) file_error = true;
-      return fail(m, gs, err);
+  std::vector<GzHeld> held;
+  std::vector<uint32_t> row_of;
+  uint64_t at = 0;          // bytes staged
+  bool host_only = false;   // a gzip header the device path does not read
+  gg_status st = GG_OK;     // a file that did not read (err), or a HIP failure
+  bool file_err = false;
+  std::string err;
+  double ms = 0;
+};
+
+class GzPipe {
+ public:
+  GzPipe(gg_ctx* m, PackStream& stream, uint32_t nm, std::mutex& cursor_mu, uint32_t& cursor, bool& stop,
+         int copy_threads, const std::vector<uint32_t>& miss_at)
+      : m_(m), stream_(stream), nm_(nm), mu_(cursor_mu), cursor_(cursor), stop_(stop), threads_(copy_threads),
+        miss_at_(miss_at) {}
+  ~GzPipe() {
+    if (next_.valid()) next_.wait();
+  }
+  // The next staged batch (nullptr: no more); starts staging the one after.
+  GzStaged* next() {
+    bool have;
+    if (next_.valid()) {
+      have = next_.get();
+    } else {
+      have = stage(slot_, staged_[slot_]);
     }
-    InflateFile f;
-    size_t doff = 0, dlen = tx->size();
-    uint32_t isz = 0, crc = 0;
-    const bool member = gz && gzip_member(tx->data(), tx->size(), &doff, &dlen, &isz, &crc);
-    if (gz && !member) host_only = true;  // (a gzip header this path does not read: the host decodes)
-    const uint64_t p = (at + doff + 3) / 4 * 4 - doff;
-    gg_status ps = grow_pinned(m, p + tx->size() + 16, at, 2 * kBatchGzBytes);
-    if (ps != GG_OK) return ps;
-    parallel_copy((uint8_t*)m->pinned + p, tx->data(), tx->size(), copy_threads);
-    f.gz = member;
-    f.data_off = p + doff;
-    f.data_len = dlen;
-    f.isize = isz;
-    f.crc = crc;
-    files.push_back(f);
-    held.push_back(Held{p, tx->size(), gz});
-    at = p + tx->size();
-    gz_bytes += gz ? tx->size() : 0;
-    text_est += member ? isz : tx->size();
-    row_of.push_back(miss_at[i]);
-    stream.release(i);
-    if ((gz_bytes >= kBatchGzBytes || text_est >= kBatchGzText) && i + 1 < b1) {  // cut the batch here
-      std::lock_guard<std::mutex> lk(cursor_mu);
-      if (cursor == b1) {
-        cursor = i + 1;
-        b1 = i + 1;
+    if (!have) return nullptr;
+    cur_ = slot_;
+    slot_ ^= 1;
+    if (staged_[cur_].st == GG_OK)
+      next_ = std::async(std::launch::async, [this] {
+        (void)hipSetDevice(m_->device);
+        return stage(slot_, staged_[slot_]);
+      });
+    return &staged_[cur_];
+  }
+  const uint8_t* host() const { return m_->gz_slot[cur_].host; }
+  uint8_t* dev() const { return m_->gz_slot[cur_].dev; }
+  hipStream_t up_stream() const { return m_->gz_slot[cur_].st; }
+
+ private:
+  static constexpr uint64_t kUpPiece = 16ull << 20;  // device copies of >= 16 MiB as the batch is staged
+
+  // Claims and stages one batch into slot si; false when no files are left.
+  bool stage(int si, GzStaged& g) {
+    g = GzStaged{};
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (stop_ || cursor_ >= nm_) return false;
+      g.b0 = cursor_;
+      g.b1 = std::min(nm_, g.b0 + kBatchGenomesGz);
+      cursor_ = g.b1;
+    }
+    const auto t0 = Clock::now();
+    gg_ctx::GzSlot& sl = m_->gz_slot[si];
+    auto hip = [&](hipError_t e, const char* what) {
+      if (e != hipSuccess && g.st == GG_OK) {
+        g.st = e == hipErrorOutOfMemory ? GG_ERR_OUT_OF_MEMORY : GG_ERR_HIP;
+        g.err = std::string(what) + ": " + hipGetErrorString(e);
+      }
+      return e == hipSuccess;
+    };
+    if (!sl.st && !hip(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking), "hipStreamCreate")) return true;
+    uint64_t up = 0;  // bytes [0, up) are queued to sl.dev
+    uint64_t gz_bytes = 0, text_est = 0;
+    for (uint32_t i = g.b0; i < g.b1; ++i) {
+      const std::vector<uint8_t>* tx;
+      bool gz = false;
+      const gg_status gs = stream_.get_raw(i, &tx, &g.err, &gz);
+      if (gs != GG_OK) {
+        g.st = gs;
+        g.file_err = true;
+        g.b1 = i;
+        return true;
+      }
+      InflateFile f;
+      size_t doff = 0, dlen = tx->size();
+      uint32_t isz = 0, crc = 0;
+      const bool member = gz && gzip_member(tx->data(), tx->size(), &doff, &dlen, &isz, &crc);
+      if (gz && !member) g.host_only = true;
+      const uint64_t p = (g.at + doff + 3) / 4 * 4 - doff;
+      const uint64_t need = p + tx->size() + 16;
+      if (need > sl.host_cap || need + kInflatePad > sl.dev_cap) {  // grow the slot (a batch of large files)
+        if (!hip(hipStreamSynchronize(sl.st), "hipStreamSynchronize")) return true;
+        const uint64_t cap = std::max<uint64_t>(need + kInflatePad, 2 * kBatchGzBytes);
+        if (need > sl.host_cap) {
+          uint8_t* h = nullptr;
+          if (!hip(hipHostMalloc((void**)&h, cap, hipHostMallocDefault), "hipHostMalloc")) return true;
+          if (g.at) memcpy(h, sl.host, g.at);
+          if (sl.host) (void)hipHostFree(sl.host);
+          sl.host = h;
+          sl.host_cap = cap;
+        }
+        if (need + kInflatePad > sl.dev_cap) {
+          if (sl.dev) (void)hipFree(sl.dev);
+          sl.dev = nullptr;
+          sl.dev_cap = 0;
+          if (!hip(hipMalloc((void**)&sl.dev, cap), "hipMalloc")) return true;
+          sl.dev_cap = cap;
+          up = 0;  // (queued again from the host copy)
+        }
+      }
+      parallel_copy(sl.host + p, tx->data(), tx->size(), threads_);
+      f.gz = member;
+      f.data_off = p + doff;
+      f.data_len = dlen;
+      f.isize = isz;
+      f.crc = crc;
+      g.files.push_back(f);
+      g.held.push_back(GzHeld{p, tx->size(), gz});
+      g.at = p + tx->size();
+      if (g.at - up >= kUpPiece) {
+        if (!hip(hipMemcpyAsync(sl.dev + up, sl.host + up, g.at - up, hipMemcpyHostToDevice, sl.st), "hipMemcpyAsync"))
+          return true;
+        up = g.at;
+      }
+      gz_bytes += gz ? tx->size() : 0;
+      text_est += member ? isz : tx->size();
+      g.row_of.push_back(miss_at_[i]);
+      stream_.release(i);
+      if ((gz_bytes >= kBatchGzBytes || text_est >= kBatchGzText) && i + 1 < g.b1) {  // cut the batch here
+        std::lock_guard<std::mutex> lk(mu_);
+        if (cursor_ == g.b1) {
+          cursor_ = i + 1;
+          g.b1 = i + 1;
+        }
       }
     }
+    if (g.at > up &&
+        !hip(hipMemcpyAsync(sl.dev + up, sl.host + up, g.at - up, hipMemcpyHostToDevice, sl.st), "hipMemcpyAsync"))
+      return true;
+    g.ms = ms_since(t0);
+    return true;
   }
+
+  gg_ctx* m_;
+  PackStream& stream_;
+  uint32_t nm_;
+  std::mutex& mu_;
+  uint32_t& cursor_;
+  bool& stop_;
+  int threads_;
+  const std::vector<uint32_t>& miss_at_;
+  GzStaged staged_[2];
+  int slot_ = 0, cur_ = 0;
+  std::future<bool> next_;
+};
+
+// Inflates (or, when the device path does not take it, decodes on the host
+// threads) and parses one staged batch on m's stream: 2-bit words into
+// *d_words, runs into runs.
+gg_status inflate_staged_batch(gg_ctx* m, GzPipe& pipe, GzStaged& g, int copy_threads, std::mutex& cursor_mu,
+                               bool& stop, bool& file_error, uint32_t** d_words, uint64_t* nw,
+                               std::vector<gg_run>& runs, const char* const* names) {
+  static const bool dbg = [] {
+    const char* e = getenv("GALAHGPU_INFLATE_DEBUG");
+    return e && *e == '1';
+  }();
+  const auto t0 = Clock::now();
+  if (g.st != GG_OK) {
+    if (g.file_err) {
+      std::lock_guard<std::mutex> lk(cursor_mu);
+      if (!stop) file_error = true;
+    }
+    return fail(m, g.st, g.err);
+  }
+  // the stream waits for the batch's copies (queued on the slot's stream)
+  hipEvent_t up_done = m->copy_done;
+  if (!up_done) GG_HIP(m, hipEventCreateWithFlags(&m->copy_done, hipEventDisableTiming));
+  up_done = m->copy_done;
+  GG_HIP(m, hipEventRecord(up_done, pipe.up_stream()));
+  GG_HIP(m, hipStreamWaitEvent(m->stream, up_done, 0));
+  if (dbg) fprintf(stderr, "[inflate] batch of %zu files staged in %.3f ms\n", g.files.size(), g.ms);
   uint8_t* d_text = nullptr;
   std::vector<uint64_t> foff;
   bool ok = false;
-  if (!host_only) {
-    const gg_status is = inflate_batch(m, (const uint8_t*)m->pinned, at, files, &d_text, foff, &ok);
+  if (!g.host_only) {
+    const gg_status is = inflate_batch(m, pipe.host(), g.at, g.files, &d_text, foff, &ok, pipe.dev());
     if (is != GG_OK) return is;
   }
   if (!ok) {  // the host decodes this batch (and reports a corrupt file)
     ++m->fallbacks[GG_FALLBACK_INFLATE_HOST];
-    const size_t nf = files.size();
+    const size_t nf = g.files.size();
     std::vector<std::vector<uint8_t>> texts(nf);
     std::vector<gg_status> sts(nf, GG_OK);
     std::vector<std::string> errs(nf);
@@ -547,12 +682,12 @@ gg_status inflate_files_batch(gg_ctx* m, PackStream& stream, uint32_t b0, uint32
     const int T = std::max(1, std::min<int>(copy_threads, (int)nf));
     auto work = [&](int t) {
       for (size_t f = (size_t)t; f < nf; f += (size_t)T) {
-        const uint8_t* b = (const uint8_t*)m->pinned + held[f].pos;
-        if (held[f].gz) {
-          const std::vector<uint8_t> gzb(b, b + held[f].len);
-          sts[f] = host_text_from_gzip(gzb, names[b0 + f], texts[f], errs[f]);
+        const uint8_t* b = pipe.host() + g.held[f].pos;
+        if (g.held[f].gz) {
+          const std::vector<uint8_t> gzb(b, b + g.held[f].len);
+          sts[f] = host_text_from_gzip(gzb, names[g.b0 + f], texts[f], errs[f]);
         } else {
-          texts[f].assign(b, b + held[f].len);
+          texts[f].assign(b, b + g.held[f].len);
         }
       }
     };
@@ -573,7 +708,9 @@ gg_status inflate_files_batch(gg_ctx* m, PackStream& stream, uint32_t b0, uint32
     if (foff[nf]) GG_HIP(m, hipMemcpyAsync(d_text, all.data(), foff[nf], hipMemcpyHostToDevice, m->stream));
     GG_HIP(m, hipStreamSynchronize(m->stream));
   }
-  return parse_raw_batch(m, d_text, foff, d_words, nw, runs);
+  const gg_status ps = parse_raw_batch(m, d_text, foff, d_words, nw, runs);
+  if (dbg) fprintf(stderr, "[inflate] batch inflated and parsed in %.3f ms\n", ms_since(t0));
+  return ps;
 }
 
 // Sketches of paths[0..n) into every member's full array (rows[i]); spans
@@ -663,13 +800,21 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
     std::vector<uint32_t> row_of;
     std::vector<uint64_t> out_rows;
     std::vector<uint32_t> out_lens;
+    std::unique_ptr<GzPipe> pipe;
+    if (gz_dev) pipe.reset(new GzPipe(m, stream, nm, cursor_mu, cursor, stop, copy_threads, miss_at));
     for (;;) {
       uint32_t b0, b1;
-      {
+      GzStaged* staged = nullptr;
+      if (gz_dev) {
+        staged = pipe->next();
+        if (!staged) break;
+        b0 = staged->b0;
+        b1 = staged->b1;
+      } else {
         std::lock_guard<std::mutex> lk(cursor_mu);
         if (stop || cursor >= nm) break;
         b0 = cursor;
-        b1 = std::min(nm, b0 + (gz_dev ? kBatchGenomesGz : kBatchGenomes));
+        b1 = std::min(nm, b0 + kBatchGenomes);
         cursor = b1;
       }
       // assemble the batch in the pinned staging buffer
@@ -679,9 +824,10 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
       uint32_t g = 0;
       uint32_t* d_words = nullptr;
       if (gz_dev) {  // gzip -> device inflate -> device parser
-        const gg_status gs = inflate_files_batch(m, stream, b0, b1, cursor_mu, cursor, stop, file_error, copy_threads,
-                                                 &d_words, &nw, runs, row_of, miss_at, miss.data());
+        const gg_status gs = inflate_staged_batch(m, *pipe, *staged, copy_threads, cursor_mu, stop, file_error,
+                                                  &d_words, &nw, runs, miss.data());
         if (gs != GG_OK) return gs;
+        row_of = staged->row_of;
       } else if (raw) {  // FASTA text -> device parser
         std::vector<uint64_t> foff(1, 0);
         for (uint32_t i = b0; i < b1; ++i) {
@@ -722,7 +868,6 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
         const gg_status ps = parse_raw_batch(m, d_text, foff, &d_words, &nw, runs);
         if (ps != GG_OK) return ps;
       }
-      if (gz_dev) b1 = b0 + (uint32_t)row_of.size();  // (the batch may have been cut)
       for (uint32_t i = b0; !raw && i < b1; ++i, ++g) {
         const std::vector<uint32_t>* w;
         const std::vector<gg_run>* rr;

@@ -90,7 +90,7 @@ struct SpecStats {
   size_t rounds = 0, redo_bits = 0, spans = 0, span_bits = 0;
 };
 static uint32_t spec_segment(const Bits& in, uint64_t s0, uint64_t end, uint64_t limit, LaneTables<ArrayStore>& tab,
-                             std::vector<uint32_t>& out, uint64_t& out_len, uint64_t& last_end, uint32_t& fin,
+                             ClArrays& cla, std::vector<uint32_t>& out, uint64_t& out_len, uint64_t& last_end, uint32_t& fin,
                              SpecStats& ss) {
   const bool final_seg = end == ~0ull;
   uint64_t pos = s0;
@@ -104,7 +104,7 @@ static uint32_t spec_segment(const Bits& in, uint64_t s0, uint64_t end, uint64_t
     }
     uint64_t q = pos;
     uint32_t bf = 0, stl = 0;
-    const int bt = read_block_header(in, q, tab, bf, stl);
+    const int bt = read_block_header(in, q, tab, cla, bf, stl);
     if (bt < 0) {
       last_end = q;
       return kDecBad;
@@ -248,16 +248,17 @@ int main(int argc, char** argv) {
     }
     const long off = gzip_data_offset(gz);
     const size_t nbytes = gz.size() - (size_t)off;
-    std::vector<uint32_t> words((nbytes + 3) / 4 + 4, 0);
+    std::vector<uint32_t> words((nbytes + 3) / 4 + 1024, 0);  // (a header walk may read ~4.5 kbit past the end)
     memcpy(words.data(), gz.data() + off, nbytes);
     const Bits in{words.data()};
     const uint64_t limit_bits = (uint64_t)nbytes * 8;
     LaneTables<ArrayStore> tab;
+    ClArrays cla;
     // (a) serially
     std::vector<uint32_t> toks;
     uint64_t out_len = 0, last_end = 0;
     uint32_t bf = 0;
-    const uint32_t st = decode_blocks(in, 0, ~0ull, limit_bits, tab,
+    const uint32_t st = decode_blocks(in, 0, ~0ull, limit_bits, tab, cla,
                                       [&](uint32_t t) {
                                         toks.push_back(t);
                                         return true;
@@ -275,7 +276,7 @@ int main(int argc, char** argv) {
     for (uint64_t c = chunk; c < nbytes; c += chunk) {
       for (uint64_t p = c * 8; p < std::min<uint64_t>((c + chunk) * 8, limit_bits); ++p) {
         uint64_t q = p;
-        if (block_header_ok(in, q)) {
+        if (block_header_ok(in, q, cla)) {
           starts.push_back(p);
           break;
         }
@@ -293,7 +294,7 @@ int main(int argc, char** argv) {
         const uint64_t end = b + 1 < starts.size() ? starts[b + 1] : ~0ull;
         uint64_t ol, le;
         uint32_t fin;
-        const uint32_t r = decode_blocks(in, starts[b], end, limit_bits, tab,
+        const uint32_t r = decode_blocks(in, starts[b], end, limit_bits, tab, cla,
                                          [&](uint32_t t) {
                                            part[b].push_back(t);
                                            return true;
@@ -321,7 +322,7 @@ int main(int argc, char** argv) {
       std::vector<uint32_t> t3;
       uint64_t ol, le;
       uint32_t fin;
-      const uint32_t r = spec_segment(in, starts[b], end, limit_bits, tab, t3, ol, le, fin, ss);
+      const uint32_t r = spec_segment(in, starts[b], end, limit_bits, tab, cla, t3, ol, le, fin, ss);
       if (r != kDecOk || t3 != part[b] || ol != part_len[b]) {
         fprintf(stderr, "%s: lane %zu: sub-span decode differs (status %u, %zu vs %zu tokens)\n", argv[a], b, r,
                 t3.size(), part[b].size());
