@@ -261,6 +261,7 @@ struct InflateDecode {
   const uint64_t* tok_cap;
   uint32_t* scr;               // speculative sub-span tokens of lane l at scr_off[l] (inflate::decode_scratch)
   const uint64_t* scr_off;
+  uint64_t* prof = nullptr;    // (debug) cycles in header / first decode / resync rounds / copy, blocks, tokens
   uint32_t* status;            // [n_lanes] inflate::DecodeStatus
   uint64_t* n_tok;             // [n_lanes]
   uint64_t* out_len;           // [n_lanes] bytes the lane's tokens stand for

@@ -49,34 +49,42 @@ constexpr uint32_t kSearchStep = 4096;  // positions per step: 64 consecutive pe
 constexpr uint32_t kSearchCands = 256;  // candidates listed before they are checked
 constexpr uint32_t kWinWords = kSearchStep / 32 + 8;  // a step's bits plus the 160 after its first lane's last
 
-// block_header_quick (inflate_core.hpp) at bit I (< 32) of the 128-bit
-// window A (A[0] bit 0 = the first position of the group), with no branch:
-// the code-length code's Kraft sum by 7 lookups of 3 fields in kraft3.
-template <int I>
-__device__ __forceinline__ bool quick_at(const uint32_t (&A)[4], const uint8_t* kraft3) {
-  const uint32_t x0 = __builtin_amdgcn_alignbit(A[1], A[0], I);
-  const uint32_t x1 = __builtin_amdgcn_alignbit(A[2], A[1], I);
-  const uint32_t x2 = __builtin_amdgcn_alignbit(A[3], A[2], I);
-  const bool head = (((x0 >> 1) & 3u) == 2u) & (((x0 >> 3) & 31u) <= 29u) & (((x0 >> 8) & 31u) <= 29u);
-  const uint32_t hclen = ((x0 >> 13) & 15u) + 4u;
-  uint64_t f = (uint64_t)__builtin_amdgcn_alignbit(x1, x0, 17) | ((uint64_t)__builtin_amdgcn_alignbit(x2, x1, 17) << 32);
-  f &= (1ull << (3 * hclen)) - 1ull;  // (3 hclen <= 57)
-  uint32_t kr = 0;
+// block_header_quick (inflate_core.hpp) for the 64 positions of a lane at
+// once.  A[0..4]: the 160 stream bits from the lane's first position.  The
+// header fields are tested as 64-bit masks over the positions (bit i of
+// S(k) = stream bit i + k): BTYPE 10, HLIT and HDIST not 30 or 31; the ~22%
+// of positions left get the code-length code's Kraft sum, by 7 lookups of 3
+// fields in kraft3.
+__device__ __forceinline__ uint64_t quick64(const uint32_t (&A)[5], const uint8_t* kraft3) {
+  const uint64_t lo = (uint64_t)A[0] | ((uint64_t)A[1] << 32), hi = (uint64_t)A[2] | ((uint64_t)A[3] << 32);
+  auto S = [&](int k) { return (lo >> k) | (hi << (64 - k)); };  // (1 <= k <= 12)
+  uint64_t m = ~S(1) & S(2);
+  m &= ~(S(4) & S(5) & S(6) & S(7));
+  m &= ~(S(9) & S(10) & S(11) & S(12));
+  uint64_t out = 0;
+  while (m) {
+    const uint32_t i = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    m &= m - 1;
+    // bits i + 13 .. i + 13 + 63 (HCLEN, then the code-length fields)
+    const uint32_t o = i + 13, w = o >> 5, sh = o & 31u;
+    const uint32_t a0 = w == 0 ? A[0] : w == 1 ? A[1] : A[2];
+    const uint32_t a1 = w == 0 ? A[1] : w == 1 ? A[2] : A[3];
+    const uint32_t a2 = w == 0 ? A[2] : w == 1 ? A[3] : A[4];
+    const uint32_t y0 = __builtin_amdgcn_alignbit(a1, a0, sh), y1 = __builtin_amdgcn_alignbit(a2, a1, sh);
+    const uint32_t hclen = (y0 & 15u) + 4u;
+    uint64_t f = ((uint64_t)y0 >> 4) | ((uint64_t)y1 << 28);  // (60 bits valid)
+    f &= (1ull << (3 * hclen)) - 1ull;  // (3 hclen <= 57)
+    uint32_t kr = 0;
 #pragma unroll
-  for (int g = 0; g < 7; ++g) kr += kraft3[(uint32_t)(f >> (9 * g)) & 511u];
-  return head & (kr == 128u);
-}
-template <int I>
-__device__ __forceinline__ void quick_run(const uint32_t (&A)[4], const uint8_t* kraft3, uint32_t& m) {
-  if constexpr (I < 32) {
-    m |= (uint32_t)quick_at<I>(A, kraft3) << I;
-    quick_run<I + 1>(A, kraft3, m);
+    for (int g = 0; g < 7; ++g) kr += kraft3[(uint32_t)(f >> (9 * g)) & 511u];
+    if (kr == 128u) out |= 1ull << i;
   }
+  return out;
 }
 
 // One wave per chunk, in steps of kSearchStep positions: the step's words
 // staged in LDS, each lane filters its 64 consecutive positions from a
-// 160-bit register window (quick_run, ~0.1% pass) and the survivors are
+// 160-bit register window (quick64, ~0.1% pass) and the survivors are
 // appended in order to the chunk's list in LDS.  The full checks
 // (block_header_ok, one candidate per lane) run when the list is full or
 // the chunk is done, so a step waits on no header walk; the first
@@ -128,16 +136,7 @@ __global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(Infla
 #pragma unroll
         for (int k = 0; k < 5; ++k) A[k] = __builtin_amdgcn_alignbit(W[k + 1], W[k], q0 & 31u);
       }
-      uint32_t m0 = 0, m1 = 0;
-      {
-        const uint32_t a0[4] = {A[0], A[1], A[2], A[3]};
-        quick_run<0>(a0, kraft3, m0);
-      }
-      {
-        const uint32_t a1[4] = {A[1], A[2], A[3], A[4]};
-        quick_run<0>(a1, kraft3, m1);
-      }
-      uint64_t m = (uint64_t)m0 | ((uint64_t)m1 << 32);
+      uint64_t m = quick64(A, kraft3);
       const uint64_t p0 = s0 + 64ull * lane;
       if (p0 >= s1) m = 0;
       else if (s1 - p0 < 64) m &= (1ull << (s1 - p0)) - 1ull;
@@ -192,6 +191,10 @@ struct LdsStore {
   uint32_t* dc;
   uint16_t* ls;
   uint8_t* ds;
+  uint32_t* lf;
+  uint32_t* df;
+  __device__ uint32_t& lfast(int i) { return lf[i]; }
+  __device__ uint32_t& dfast(int i) { return df[i]; }
   __device__ int32_t& lbase(int l) { return lb[l]; }
   __device__ int32_t& dbase(int l) { return db[l]; }
   __device__ uint32_t& lcnt(int l) { return lc[l]; }
@@ -227,6 +230,119 @@ struct TokSink {
   }
 };
 
+// A block's header read by the whole wave.  Lane 0 parses the fields and
+// walks the code lengths (SeqBits) into LDS (lens); then every lane counts
+// them per length by ballots, builds the canonical limits in its registers
+// (tab.llim / dlim) and the bases, and the symbols sorted by (length, value)
+// are placed in the LDS tables by ballot ranks.  Returns btype (0 stored,
+// 1 fixed, 2 dynamic) or -1 for a header zlib refuses (inflate_core.hpp
+// read_block_header, the same checks).
+struct HeaderLds {
+  uint8_t lens[kLitSyms + kDistSyms];
+  uint64_t body0;
+  uint32_t stored, bfinal, hlit, hdist;
+  int32_t bt;
+};
+__device__ int wave_header(const Bits& in, uint64_t pos, LaneTables<LdsStore>& tab, ClLds& hcl, HeaderLds& H,
+                           uint32_t lane) {
+  for (uint32_t i = lane; i < (uint32_t)(kLitSyms + kDistSyms); i += 64) H.lens[i] = 0;
+  __syncthreads();
+  if (lane == 0) {
+    const uint32_t h = in.peek(pos);
+    int bt = (int)((h >> 1) & 3u);
+    H.bfinal = h & 1u;
+    H.stored = 0;
+    if (bt == 0) {
+      uint64_t q = (pos + 3 + 7) & ~7ull;
+      const uint32_t v = in.peek(q);
+      if (((v & 0xFFFFu) ^ (v >> 16)) != 0xFFFFu) bt = -1;
+      H.stored = v & 0xFFFFu;
+      H.body0 = q + 32;
+    } else if (bt == 1) {  // fixed codes (RFC 1951 3.2.6)
+      for (uint32_t i = 0; i < 288; ++i) H.lens[i] = i < 144 ? 8 : i < 256 ? 9 : i < 280 ? 7 : 8;
+      for (uint32_t i = 0; i < 32; ++i) H.lens[288 + i] = 5;
+      H.hlit = 288;
+      H.hdist = 32;
+      H.body0 = pos + 3;
+    } else if (bt == 2) {
+      const uint32_t hlit = ((h >> 3) & 31u) + 257u, hdist = ((h >> 8) & 31u) + 1u, hclen = ((h >> 13) & 15u) + 4u;
+      H.hlit = hlit;
+      H.hdist = hdist;
+      SeqBits sb{Cursor{in.w}};
+      sb.c.seek(pos);
+      uint64_t p = pos + 17;
+      ClCode cl;
+      if (hlit > 286 || hdist > 30 || !read_cl_code(sb, p, hclen, cl, hcl) ||
+          !walk_lengths(sb, p, cl, hcl, hlit + hdist, [&](uint32_t i, uint32_t len) {
+            H.lens[i] = (uint8_t)len;
+            return true;
+          }))
+        bt = -1;
+      H.body0 = p;
+    } else {
+      bt = -1;
+      H.body0 = pos;
+    }
+    H.bt = bt;
+  }
+  __syncthreads();
+  const int bt = H.bt;
+  if (bt <= 0) return bt;
+  const uint32_t hlit = H.hlit, hdist = H.hdist;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t lc[kMaxBits + 1], dc[kMaxBits + 1];
+#pragma unroll
+  for (int l = 0; l <= kMaxBits; ++l) lc[l] = dc[l] = 0;
+  const uint32_t dlen = lane < hdist ? H.lens[hlit + lane] : 0u;
+  for (uint32_t c0 = 0; c0 < hlit; c0 += 64) {
+    const uint32_t len = c0 + lane < hlit ? H.lens[c0 + lane] : 0u;
+#pragma unroll
+    for (int l = 1; l <= kMaxBits; ++l) lc[l] += (uint32_t)__popcll(__ballot(len == (uint32_t)l));
+  }
+#pragma unroll
+  for (int l = 1; l <= kMaxBits; ++l) dc[l] = (uint32_t)__popcll(__ballot(dlen == (uint32_t)l));
+  if (H.lens[256] == 0) return -1;  // no end-of-block code
+  Canon c{};
+  int ml = 0;
+  int r = canon_from_counts(lc, c, ml);
+  if (!code_ok(r, ml, false)) return -1;
+  tab.set_lit(c);
+  r = canon_from_counts(dc, c, ml);
+  if (!code_ok(r, ml, true)) return -1;
+  tab.set_dist(c);
+  // symbols sorted by (length, value): slot = first of its length + its rank
+  uint32_t off[kMaxBits + 1];
+  uint32_t a = 0;
+#pragma unroll
+  for (int l = 1; l <= kMaxBits; ++l) {
+    off[l] = a;
+    a += lc[l];
+  }
+  for (uint32_t c0 = 0; c0 < hlit; c0 += 64) {
+    const uint32_t len = c0 + lane < hlit ? H.lens[c0 + lane] : 0u;
+#pragma unroll
+    for (int l = 1; l <= kMaxBits; ++l) {
+      const uint64_t m = __ballot(len == (uint32_t)l);
+      if (len == (uint32_t)l) tab.s.lsym((int)(off[l] + (uint32_t)__popcll(m & lt))) = (uint16_t)(c0 + lane);
+      off[l] += (uint32_t)__popcll(m);
+    }
+  }
+  a = 0;
+#pragma unroll
+  for (int l = 1; l <= kMaxBits; ++l) {
+    const uint64_t m = __ballot(dlen == (uint32_t)l);
+    if (dlen == (uint32_t)l) tab.s.dsym((int)(a + (uint32_t)__popcll(m & lt))) = (uint8_t)lane;
+    a += (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  for (uint32_t i = lane; i < kFastSize; i += 64) {  // the one-lookup tables of the short codes
+    tab.s.lfast((int)i) = tab.fast_entry(i, false);
+    tab.s.dfast((int)i) = tab.fast_entry(i, true);
+  }
+  __syncthreads();
+  return bt;
+}
+
 // n tokens from a lane's scratch to the segment's tokens, 8 loads in flight
 // (a plain loop waited on each load in turn).
 __device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint32_t n) {
@@ -254,19 +370,17 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
   __shared__ int32_t lb[kMaxBits + 1], db[kMaxBits + 1];
   __shared__ uint32_t lcn[kMaxBits + 1], dcn[kMaxBits + 1];
   __shared__ ClLds hcl;  // (lane 0's, while it reads a header)
-  __shared__ uint32_t slim[2][kMaxBits + 1];
+  __shared__ HeaderLds H;
   __shared__ uint16_t ls[kLitSyms];
   __shared__ uint8_t ds[kDistSyms];
+  __shared__ uint32_t lf[kFastSize], df[kFastSize];
   __shared__ uint64_t sE[kSpanLanes];
   __shared__ uint32_t sSt[kSpanLanes];
-  __shared__ uint64_t s_body0, s_stored;
-  __shared__ int32_t s_bt;
-  __shared__ uint32_t s_bfinal;
   const uint32_t j = threadIdx.x;
   const uint32_t seg = blockIdx.x;
   if (seg >= a.n_lanes) return;
   LaneTables<LdsStore> tab;
-  tab.s = LdsStore{lb, db, lcn, dcn, ls, ds};
+  tab.s = LdsStore{lb, db, lcn, dcn, ls, ds, lf, df};
   const uint32_t f = a.lane_file[seg];
   const Bits in{a.in + a.file_word[f]};
   const uint64_t limit = a.file_bits[f];
@@ -287,31 +401,25 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
       status = kDecOverrun;
       break;
     }
-    if (j == 0) {
-      uint64_t q = pos;
-      uint32_t bf = 0, stl = 0;
-      const int bt = read_block_header(in, q, tab, hcl, bf, stl);
-      s_bt = bt;
-      s_bfinal = bf;
-      s_body0 = q;
-      s_stored = stl;
-#pragma unroll
-      for (int l = 0; l <= kMaxBits; ++l) {
-        slim[0][l] = tab.llim[l];
-        slim[1][l] = tab.dlim[l];
+    uint64_t tp = a.prof ? clock64() : 0;  // (GALAHGPU_INFLATE_DEBUG: cycles per phase)
+    auto phase = [&](int k) {
+      if (a.prof) {
+        const uint64_t t = clock64();
+        if (j == 0) atomicAdd((unsigned long long*)&a.prof[k], (unsigned long long)(t - tp));
+        tp = t;
       }
-    }
-    __syncthreads();
-    const int bt = s_bt;
-    const uint32_t bfinal = s_bfinal;
-    const uint64_t body0 = s_body0;
+    };
+    const int bt = wave_header(in, pos, tab, hcl, H, j);
+    phase(0);
+    const uint32_t bfinal = H.bfinal;
+    const uint64_t body0 = H.body0;
     if (bt < 0) {
       status = kDecBad;
       pos = body0;
       break;
     }
     if (bt == 0) {  // stored: its bytes as literal tokens
-      const uint64_t stl = s_stored;
+      const uint64_t stl = H.stored;
       if (body0 + 8 * stl > limit) {
         status = kDecBad;
         break;
@@ -326,11 +434,6 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
       out_bytes += stl;
       pos = body0 + 8 * stl;
     } else {
-#pragma unroll
-      for (int l = 0; l <= kMaxBits; ++l) {
-        tab.llim[l] = slim[0][l];
-        tab.dlim[l] = slim[1][l];
-      }
       const uint64_t span_end = final_seg ? limit : end;
       uint64_t L;
       uint32_t nsub;
@@ -358,6 +461,7 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
                          na, ba, Ea);
         sink.flush();
       }
+      phase(1);
       uint64_t first = act && nck ? S + ck_off(ck[0]) : ~0ull;
       bool redone = false;
       int synced = -1;
@@ -419,6 +523,7 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
         pos = e_end;
         break;
       }
+      phase(2);
       // this span's tokens: [p1, p1 + n1) then [p2, p2 + n2)
       const uint32_t* p1 = A;
       const uint32_t* p2 = A;
@@ -459,6 +564,11 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
       uint32_t* dst = out + n_out + (incl - valid);
       copy_tokens(dst, p1, n1);
       copy_tokens(dst + n1, p2, n2);
+      phase(3);
+      if (a.prof && j == 0) {
+        atomicAdd((unsigned long long*)&a.prof[4], 1ull);
+        atomicAdd((unsigned long long*)&a.prof[5], (unsigned long long)total);
+      }
       n_out += total;
       out_bytes += tb;
       pos = e_end;

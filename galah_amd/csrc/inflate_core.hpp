@@ -50,20 +50,29 @@ struct Bits {
   }
 };
 
-// The same stream read forward through three cached words: the symbol loop
-// peeks 32 bits per symbol from registers and loads one word per 32 bits
-// consumed, ahead of its use (a Bits::peek per symbol waited on two loads).
+// The same stream read forward through cached words: the symbol loop peeks
+// 32 bits per symbol from registers (words a, b), and the words after them
+// arrive two at a time, loaded two words before they are needed, so the
+// decode waits on memory only when it outruns a load issued ~64 bits earlier
+// (loading each word as the window reached it stalled every ~32 bits).
 struct Cursor {
   const uint32_t* w;
   uint64_t pos;
-  uint64_t wi;  // word of pos
-  uint32_t a, b, c;  // words wi, wi + 1, wi + 2
+  uint64_t wi;       // word of pos
+  uint32_t a, b;     // words wi, wi + 1
+  uint32_t g0, g1;   // the next words to enter the window (g0 first; `left` of them)
+  uint32_t n0, n1;   // the two after those (in flight)
+  uint32_t left;
   GG_HD void seek(uint64_t p) {
     pos = p;
     wi = p >> 5;
     a = w[wi];
     b = w[wi + 1];
-    c = w[wi + 2];
+    g0 = w[wi + 2];
+    g1 = w[wi + 3];
+    n0 = w[wi + 4];
+    n1 = w[wi + 5];
+    left = 2;
   }
   GG_HD uint32_t peek() const {
     const uint32_t sh = (uint32_t)pos & 31u;
@@ -76,15 +85,53 @@ struct Cursor {
   GG_HD void skip(uint32_t n) {  // n <= 32
     pos += n;
     if ((pos >> 5) != wi) {
-      a = b;
-      b = c;
       ++wi;
-      c = w[wi + 2];
+      a = b;
+      b = g0;
+      g0 = g1;
+      if (--left == 0) {  // the next two words (loaded two words ago); load the two after them
+        g0 = n0;
+        g1 = n1;
+        n0 = w[wi + 4];
+        n1 = w[wi + 5];
+        left = 2;
+      }
     }
   }
   GG_HD uint32_t get(uint32_t n) {  // n <= 31
     const uint32_t v = peek() & ((1u << n) - 1u);
     skip(n);
+    return v;
+  }
+};
+
+// The stream read forward through a Cursor behind Bits' interface (the
+// device's header walks): positions asked for go forward, a peek within the
+// three cached words loads nothing (a walk through Bits waited on two loads
+// per code length); a position behind the cached words starts it over.
+struct SeqBits {
+  mutable Cursor c;
+  GG_HD uint32_t peek(uint64_t pos) const {
+    int64_t d = (int64_t)(pos - (c.wi << 5));  // pos in the cached words a, b, c
+    if (d < 0 || d >= 160) {
+      c.seek(pos);
+      d = (int64_t)(pos & 31u);
+    }
+    while (d >= 64) {  // the window one word on
+      c.skip(32u - ((uint32_t)c.pos & 31u));
+      d -= 32;
+    }
+    const uint32_t sh = (uint32_t)d & 31u;
+    const uint32_t lo = d < 32 ? c.a : c.b, hi = d < 32 ? c.b : c.g0;  // (g0: word wi + 2)
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, sh);
+#else
+    return sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+#endif
+  }
+  GG_HD uint32_t get(uint64_t& pos, uint32_t n) const {
+    const uint32_t v = peek(pos) & ((1u << n) - 1u);
+    pos += n;
     return v;
   }
 };
@@ -154,16 +201,15 @@ GG_HD bool code_ok(int r, int max_len, bool allow_empty) {
 }
 
 // RFC 1951 3.2.5 length and distance tables
-GG_HD uint32_t len_base(uint32_t i) {  // lit/len symbol 257 + i
-  constexpr uint16_t b[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                              31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-  return b[i];
+GG_HD uint32_t len_base(uint32_t i) {  // lit/len symbol 257 + i (3, 4, .., 10, 11, 13, .., 227, 258)
+  if (i < 8) return 3 + i;
+  if (i == 28) return 258;
+  return ((4u + (i & 3u)) << ((i >> 2) - 1u)) + 3u;
 }
 GG_HD uint32_t len_extra(uint32_t i) { return i < 8 || i == 28 ? 0u : (i - 4) >> 2; }
-GG_HD uint32_t dist_base(uint32_t d) {
-  constexpr uint16_t b[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
-                              193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-  return b[d];
+GG_HD uint32_t dist_base(uint32_t d) {  // (1, 2, 3, 4, 5, 7, .., 24577)
+  if (d < 4) return d + 1;
+  return ((2u + (d & 1u)) << ((d >> 1) - 1u)) + 1u;
 }
 GG_HD uint32_t dist_extra(uint32_t d) { return d < 4 ? 0u : (d - 2) >> 1; }
 
@@ -348,6 +394,30 @@ GG_HD bool block_header_ok(const B& in, uint64_t& pos, ClS& st) {
 // device: LDS):
 //   int32_t& lbase(int), dbase(int); uint32_t& lcnt(int), dcnt(int);
 //   uint16_t& lsym(int); uint8_t& dsym(int)
+// Decode entries: the value in bits 0..15 (a literal byte, a length base or
+// a distance base), its extra bits in 16..19, the code length in 20..23
+// (fast tables only; 0 = not in the table), the kind in 24..25.
+constexpr int kFastBits = 10;
+constexpr uint32_t kFastSize = 1u << kFastBits;
+constexpr int kFastLenShift = 20;
+constexpr uint32_t kFastLenMask = 15u << kFastLenShift;
+enum EntryKind : uint32_t { kEntryLit = 0, kEntryLen = 1, kEntryEob = 2, kEntryInvalid = 3 };
+constexpr uint32_t kEntryBad = kEntryInvalid << 24;
+GG_HD uint32_t entry_kind(uint32_t e) { return e >> 24; }
+GG_HD uint32_t entry_value(uint32_t e) { return e & 0xFFFFu; }
+GG_HD uint32_t entry_extra(uint32_t e) { return (e >> 16) & 15u; }
+GG_HD uint32_t lit_value(int sy) {  // lit/len symbol -> entry (without its code length)
+  if (sy < 256) return (uint32_t)sy;
+  if (sy == 256) return kEntryEob << 24;
+  const uint32_t li = (uint32_t)sy - 257u;
+  if (li >= 29) return kEntryBad;
+  return (kEntryLen << 24) | (len_extra(li) << 16) | len_base(li);
+}
+GG_HD uint32_t dist_value(int d) {  // distance symbol -> entry
+  if (d >= 30) return kEntryBad;
+  return (kEntryLen << 24) | (dist_extra((uint32_t)d) << 16) | dist_base((uint32_t)d);
+}
+
 template <class Store>
 struct LaneTables {
   uint32_t llim[kMaxBits + 1], dlim[kMaxBits + 1];
@@ -364,6 +434,46 @@ struct LaneTables {
     for (int l = 0; l <= kMaxBits; ++l) {
       dlim[l] = c.limit[l];
       s.dbase(l) = c.base[l];
+    }
+  }
+  // A symbol as a table entry (fast_entry): codes of <= kFastBits bits in
+  // one lookup of the next kFastBits stream bits, longer ones by the limits.
+  // The entry is consumed from the cursor.
+  GG_HD uint32_t lit_entry(Cursor& cur) {
+    const uint32_t e = s.lfast(cur.peek() & (kFastSize - 1));
+    if (e & kFastLenMask) {
+      cur.skip((e >> kFastLenShift) & 15u);
+      return e;
+    }
+    const int sy = lit(cur);
+    return sy < 0 ? kEntryBad : lit_value(sy);
+  }
+  GG_HD uint32_t dist_entry(Cursor& cur) {
+    const uint32_t e = s.dfast(cur.peek() & (kFastSize - 1));
+    if (e & kFastLenMask) {
+      cur.skip((e >> kFastLenShift) & 15u);
+      return e;
+    }
+    const int d = dist(cur);
+    return d < 0 ? kEntryBad : dist_value(d);
+  }
+  // The fast entry of the kFastBits stream bits i (LSB first) for the lit/len
+  // (dist = false) or distance code: 0 when the code there is longer.
+  GG_HD uint32_t fast_entry(uint32_t i, bool dist_code) const {
+    const uint32_t x = rev15(i);  // (bits past the kFastBits read as 0)
+    int L = 1;  // the smallest l with x < limit[l] (15: none below 15)
+#pragma unroll
+    for (int l = 1; l < kMaxBits; ++l) L += x >= (dist_code ? dlim[l] : llim[l]) ? 1 : 0;
+    if (L > kFastBits) return 0;
+    Store& st = const_cast<Store&>(s);
+    const uint32_t v = dist_code ? dist_value(st.dsym(st.dbase(L) + (int)(x >> (kMaxBits - L))))
+                                 : lit_value(st.lsym(st.lbase(L) + (int)(x >> (kMaxBits - L))));
+    return v | ((uint32_t)L << kFastLenShift);
+  }
+  GG_HD void build_fast() {  // (serially; the device builds them with its wave)
+    for (uint32_t i = 0; i < kFastSize; ++i) {
+      s.lfast((int)i) = fast_entry(i, false);
+      s.dfast((int)i) = fast_entry(i, true);
     }
   }
   GG_HD int lit(Cursor& cur) {
@@ -393,6 +503,9 @@ struct ArrayStore {
   uint32_t lc[kMaxBits + 1], dc[kMaxBits + 1];
   uint16_t ls[kLitSyms];
   uint8_t ds[kDistSyms];
+  uint32_t lf[kFastSize], df[kFastSize];
+  uint32_t& lfast(int i) { return lf[i]; }
+  uint32_t& dfast(int i) { return df[i]; }
   int32_t& lbase(int l) { return lb[l]; }
   int32_t& dbase(int l) { return db[l]; }
   uint32_t& lcnt(int l) { return lc[l]; }
@@ -443,6 +556,7 @@ GG_HD int read_block_header(const Bits& in, uint64_t& pos, LaneTables<Store>& t,
       else t.s.lsym((int)o8++) = (uint16_t)sy;
     }
     for (uint32_t d = 0; d < (uint32_t)kDistSyms; ++d) t.s.dsym((int)d) = (uint8_t)d;
+    t.build_fast();
     return 1;
   }
   if (btype != 2) return -1;
@@ -494,6 +608,7 @@ GG_HD int read_block_header(const Bits& in, uint64_t& pos, LaneTables<Store>& t,
     else t.s.dsym((int)t.s.dcnt((int)len)++) = (uint8_t)(i - hlit);
     return true;
   });
+  t.build_fast();
   pos = p;
   return 2;
 }
@@ -550,29 +665,25 @@ GG_HD uint32_t decode_blocks(const Bits& in, uint64_t pos, uint64_t end, uint64_
           last_end = cur.pos;
           return kDecBad;
         }
-        const int sy = t.lit(cur);
-        if (sy < 0) {
-          last_end = cur.pos;
-          return kDecBad;
-        }
-        if (sy < 256) {
-          if (!emit((uint32_t)sy)) return kDecFull;
+        const uint32_t e = t.lit_entry(cur);
+        const uint32_t kind = entry_kind(e);
+        if (kind == kEntryLit) {
+          if (!emit(entry_value(e))) return kDecFull;
           out_len += 1;
           continue;
         }
-        if (sy == 256) break;
-        const uint32_t li = (uint32_t)sy - 257u;
-        if (li >= 29) {
+        if (kind == kEntryEob) break;
+        if (kind != kEntryLen) {
           last_end = cur.pos;
           return kDecBad;
         }
-        const uint32_t len = len_base(li) + cur.get(len_extra(li));
-        const int d = t.dist(cur);
-        if (d < 0 || d >= 30) {
+        const uint32_t len = entry_value(e) + cur.get(entry_extra(e));
+        const uint32_t de = t.dist_entry(cur);
+        if (entry_kind(de) != kEntryLen) {
           last_end = cur.pos;
           return kDecBad;
         }
-        const uint32_t dist = dist_base((uint32_t)d) + cur.get(dist_extra((uint32_t)d));
+        const uint32_t dist = entry_value(de) + cur.get(entry_extra(de));
         if (!emit(tok_match(len, dist))) return kDecFull;
         out_len += len;
       }
@@ -637,37 +748,40 @@ GG_HD uint32_t decode_span(const Bits& in, uint64_t start, uint64_t s_nom, uint6
   bytes = 0;
   uint32_t k = 0;
   uint64_t next_ck = s_nom;
+  uint64_t next_stop = next_ck < range_end ? next_ck : range_end;  // (one compare per symbol)
   for (;;) {
-    if (cur.pos >= range_end) {
-      stop = cur.pos;
-      return kSpanRange;
-    }
-    if (cur.pos >= next_ck) {  // (a symbol is shorter than kCkBits: one checkpoint at most)
-      if (!ck(k, ck_pack((uint32_t)(cur.pos - next_ck), n, bytes))) {
+    if (cur.pos >= next_stop) {
+      if (cur.pos >= range_end) {
         stop = cur.pos;
-        return kSpanSynced;
+        return kSpanRange;
       }
-      ++k;
-      next_ck += kCkBits;
+      if (cur.pos >= next_ck) {  // (a symbol is shorter than kCkBits: one checkpoint at most)
+        if (!ck(k, ck_pack((uint32_t)(cur.pos - next_ck), n, bytes))) {
+          stop = cur.pos;
+          return kSpanSynced;
+        }
+        ++k;
+        next_ck += kCkBits;
+      }
+      next_stop = next_ck < range_end ? next_ck : range_end;
     }
-    const int sy = t.lit(cur);
-    if (sy < 0) break;
-    if (sy < 256) {
-      if (!emit((uint32_t)sy)) break;
+    const uint32_t e = t.lit_entry(cur);
+    const uint32_t kind = entry_kind(e);
+    if (kind == kEntryLit) {
+      if (!emit(entry_value(e))) break;
       ++n;
       bytes += 1;
       continue;
     }
-    if (sy == 256) {
+    if (kind == kEntryEob) {
       stop = cur.pos;
       return kSpanEob;
     }
-    const uint32_t li = (uint32_t)sy - 257u;
-    if (li >= 29) break;
-    const uint32_t len = len_base(li) + cur.get(len_extra(li));
-    const int d = t.dist(cur);
-    if (d < 0 || d >= 30) break;
-    const uint32_t dist = dist_base((uint32_t)d) + cur.get(dist_extra((uint32_t)d));
+    if (kind != kEntryLen) break;
+    const uint32_t len = entry_value(e) + cur.get(entry_extra(e));
+    const uint32_t de = t.dist_entry(cur);
+    if (entry_kind(de) != kEntryLen) break;
+    const uint32_t dist = entry_value(de) + cur.get(entry_extra(de));
     if (!emit(tok_match(len, dist))) break;
     ++n;
     bytes += len;

@@ -139,6 +139,11 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     for (uint32_t c = first_chunk[f]; c < first_chunk[f + 1]; ++c)
       if (start[c] != ~0ull && start[c] > starts[f].back()) starts[f].push_back(start[c]);
   }
+  if (inflate_debug()) {
+    size_t ns = 0;
+    for (const auto& v : starts) ns += v.size();
+    fprintf(stderr, "[inflate] %u files, %u chunks, %zu starts\n", nf, nc, ns);
+  }
   // one lane (a wave of the decode kernel) per start: [start, end) up to the
   // next start (~0: the file's last lane), its tokens in a region of the
   // token buffer sized one per bit, its scratch likewise
@@ -212,7 +217,22 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     d.last_end = d_res + 2 * (size_t)nl;
     d.status = (uint32_t*)(d_res + 3 * (size_t)nl);
     d.bfinal = d.status + nl;
+    uint64_t* d_prof = nullptr;
+    if (inflate_debug()) {
+      GG_HIP(m, scratch_t(m, "gz_prof", 8, &d_prof));
+      GG_HIP(m, hipMemsetAsync(d_prof, 0, 8 * sizeof(uint64_t), st));
+      d.prof = d_prof;
+    }
     GG_HIP(m, launch_inflate_decode(d, st));
+    if (d_prof) {
+      uint64_t pr[8];
+      GG_HIP(m, hipStreamSynchronize(st));
+      GG_HIP(m, hipMemcpy(pr, d_prof, sizeof pr, hipMemcpyDeviceToHost));
+      const double nb = (double)std::max<uint64_t>(pr[4], 1);
+      fprintf(stderr, "[inflate] decode: %u lanes, %llu blocks, %.0f tokens/block; cycles per block: header %.0f, "
+              "first decode %.0f, resync %.0f, copy %.0f\n", nl, (unsigned long long)pr[4], pr[5] / nb, pr[0] / nb,
+              pr[1] / nb, pr[2] / nb, pr[3] / nb);
+    }
     std::vector<uint64_t> res((size_t)nl * 4);
     GG_HIP(m, hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));

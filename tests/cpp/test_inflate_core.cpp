@@ -276,7 +276,16 @@ int main(int argc, char** argv) {
     for (uint64_t c = chunk; c < nbytes; c += chunk) {
       for (uint64_t p = c * 8; p < std::min<uint64_t>((c + chunk) * 8, limit_bits); ++p) {
         uint64_t q = p;
-        if (block_header_ok(in, q, cla)) {
+        SeqBits sb{Cursor{in.w}};
+        sb.c.seek(p);
+        uint64_t q2 = p;
+        const bool ok2 = block_header_ok(sb, q2, cla);  // (the device's cursor reader)
+        const bool ok1 = block_header_ok(in, q, cla);
+        if (ok1 != ok2 || (ok1 && q != q2)) {
+          fprintf(stderr, "%s: header check through SeqBits differs at bit %llu\n", argv[a], (unsigned long long)p);
+          ++failures;
+        }
+        if (ok1) {
           starts.push_back(p);
           break;
         }
