@@ -223,13 +223,13 @@ struct ParseLaunch {
   uint64_t* blk_bases;   // pass 2 out
   uint64_t* blk_last;    // pass 2 out
   const uint64_t* pre_last;
-  uint64_t* blk_runs;    // pass 3 out
+  uint64_t* blk_runs;    // pass 2 out: run starts as if no base came before the block
+  uint64_t* blk_first;   // pass 2 out: 1 when the block's first non-dropped byte is a base
   const uint64_t* base_off;
   const uint64_t* run_off;
-  uint8_t* codes;        // pass 4 out (packed positions)
-  uint64_t* starts;      // pass 4 out (run start positions)
+  uint64_t* starts;      // pass 3 out (run start positions)
   uint64_t n_words;
-  uint32_t* words;       // pass 5 out
+  uint32_t* words;       // pass 3 out (cleared before)
 };
 hipError_t parse_batch_pass(int pass, const ParseLaunch& p, hipStream_t st);
 uint32_t parse_block_bytes();

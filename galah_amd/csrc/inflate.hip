@@ -46,7 +46,8 @@ struct ClLds {
 
 constexpr int kSearchWaves = 4;         // chunks per search workgroup (one wave each)
 constexpr uint32_t kSearchStep = 4096;  // positions per step: 64 consecutive per lane
-constexpr uint32_t kSearchCands = 256;  // candidates listed before they are checked
+constexpr uint32_t kSearchCands = 256;  // candidates listed at most (more: the scan resumes after the last listed)
+constexpr uint32_t kCheckAt = 48;       // candidates that trigger a round of full checks (~1 per 1,100 positions)
 constexpr uint32_t kWinWords = kSearchStep / 32 + 8;  // a step's bits plus the 160 after its first lane's last
 
 // block_header_quick (inflate_core.hpp) for the 64 positions of a lane at
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(Infla
         nc += total;
         s0 = s1;
       }
-      if (nc < kSearchCands - 64 && s0 < b1) continue;  // (room for more: keep filtering)
+      if (nc < kCheckAt && s0 < b1) continue;  // (check in groups: a start found early ends the scan)
     }
     // the full checks of the listed candidates, in order
     for (uint32_t k0 = 0; k0 < nc; k0 += 64) {

@@ -103,6 +103,22 @@ struct Cursor {
     skip(n);
     return v;
   }
+  GG_HD uint64_t peek64() const {  // the 64 stream bits from pos
+    const uint32_t sh = (uint32_t)pos & 31u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t x0 = __builtin_amdgcn_alignbit(b, a, sh), x1 = __builtin_amdgcn_alignbit(g0, b, sh);
+#else
+    const uint32_t x0 = sh ? (a >> sh) | (b << (32 - sh)) : a, x1 = sh ? (b >> sh) | (g0 << (32 - sh)) : b;
+#endif
+    return (uint64_t)x0 | ((uint64_t)x1 << 32);
+  }
+  GG_HD void skip_long(uint32_t n) {  // n <= 64
+    if (n > 32) {
+      skip(32);
+      n -= 32;
+    }
+    skip(n);
+  }
 };
 
 // The stream read forward through a Cursor behind Bits' interface (the
@@ -765,23 +781,75 @@ GG_HD uint32_t decode_span(const Bits& in, uint64_t start, uint64_t s_nom, uint6
       }
       next_stop = next_ck < range_end ? next_ck : range_end;
     }
-    const uint32_t e = t.lit_entry(cur);
+    // one token from 64 peeked bits: the lit/len code and, for a length,
+    // its extra bits, the distance code and its extra bits (<= 10 + 5 + 10
+    // + 13 bits through the one-lookup tables); longer codes take the
+    // limits (lit_entry / dist_entry)
+    const uint64_t bb = cur.peek64();
+    uint32_t e = t.s.lfast((int)(bb & (kFastSize - 1)));
+    uint32_t used = (e >> kFastLenShift) & 15u;
+    if (used == 0) {  // a long lit/len code
+      e = t.lit_entry(cur);
+      if (entry_kind(e) != kEntryLen) {
+        if (entry_kind(e) == kEntryLit) {
+          if (!emit(entry_value(e))) break;
+          ++n;
+          bytes += 1;
+          continue;
+        }
+        if (entry_kind(e) == kEntryEob) {
+          stop = cur.pos;
+          return kSpanEob;
+        }
+        break;
+      }
+      const uint32_t len = entry_value(e) + cur.get(entry_extra(e));
+      const uint32_t de = t.dist_entry(cur);
+      if (entry_kind(de) != kEntryLen) break;
+      const uint32_t dist = entry_value(de) + cur.get(entry_extra(de));
+      if (!emit(tok_match(len, dist))) break;
+      ++n;
+      bytes += len;
+      continue;
+    }
     const uint32_t kind = entry_kind(e);
     if (kind == kEntryLit) {
+      cur.skip(used);
       if (!emit(entry_value(e))) break;
       ++n;
       bytes += 1;
       continue;
     }
-    if (kind == kEntryEob) {
-      stop = cur.pos;
-      return kSpanEob;
+    if (kind != kEntryLen) {
+      if (kind == kEntryEob) {
+        cur.skip(used);
+        stop = cur.pos;
+        return kSpanEob;
+      }
+      cur.skip(used);
+      break;
     }
-    if (kind != kEntryLen) break;
-    const uint32_t len = entry_value(e) + cur.get(entry_extra(e));
-    const uint32_t de = t.dist_entry(cur);
-    if (entry_kind(de) != kEntryLen) break;
-    const uint32_t dist = entry_value(de) + cur.get(entry_extra(de));
+    const uint32_t lx = entry_extra(e);
+    const uint32_t len = entry_value(e) + ((uint32_t)(bb >> used) & ((1u << lx) - 1u));
+    used += lx;
+    const uint32_t de = t.s.dfast((int)((bb >> used) & (kFastSize - 1)));
+    const uint32_t dl = (de >> kFastLenShift) & 15u;
+    uint32_t dist;
+    if (dl == 0) {  // a long distance code
+      cur.skip(used);
+      const uint32_t d2 = t.dist_entry(cur);
+      if (entry_kind(d2) != kEntryLen) break;
+      dist = entry_value(d2) + cur.get(entry_extra(d2));
+    } else {
+      if (entry_kind(de) != kEntryLen) {
+        cur.skip(used + dl);
+        break;
+      }
+      used += dl;
+      const uint32_t dx = entry_extra(de);
+      dist = entry_value(de) + ((uint32_t)(bb >> used) & ((1u << dx) - 1u));
+      cur.skip_long(used + dx);
+    }
     if (!emit(tok_match(len, dist))) break;
     ++n;
     bytes += len;

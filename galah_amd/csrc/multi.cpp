@@ -359,11 +359,11 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   p.raw = d_text;
   p.n_bytes = foff[nf];
   p.n_blocks = nb;
-  uint64_t* blk;  // 9 arrays of nb u64: start, end, nl, pre_nl, bases, last, pre_last, runs, base_off; + run_off
-  GG_HIP(m, scratch_t(m, "parse_blk", (size_t)std::max(nb, 1u) * 10 + nf + 1, &blk));
+  uint64_t* blk;  // 11 arrays of nb u64: start, end, nl, pre_nl, bases, last, pre_last, runs, base_off, run_off, first
+  GG_HIP(m, scratch_t(m, "parse_blk", (size_t)std::max(nb, 1u) * 11 + nf + 1, &blk));
   uint32_t* d_bfile;
   GG_HIP(m, scratch_t(m, "parse_bfile", std::max(nb, 1u), &d_bfile));
-  uint64_t* d_fstart = blk + (size_t)std::max(nb, 1u) * 10;
+  uint64_t* d_fstart = blk + (size_t)std::max(nb, 1u) * 11;
   const size_t NB = std::max(nb, 1u);
   p.blk_file = d_bfile;
   p.blk_start = blk;
@@ -376,8 +376,9 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   p.blk_runs = blk + 7 * NB;
   p.base_off = blk + 8 * NB;
   p.run_off = blk + 9 * NB;
+  p.blk_first = blk + 10 * NB;
   p.file_start = d_fstart;
-  std::vector<uint64_t> h(nb), h2(nb);
+  std::vector<uint64_t> h(nb), h2(nb), hr(nb), hf(nb);
   if (nb) {
     GG_HIP(m, hipMemcpyAsync(d_bfile, bfile.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, st));
     GG_HIP(m, hipMemcpyAsync((void*)p.blk_start, bstart.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
@@ -399,66 +400,60 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
       acc = std::max(acc, x);
     }
     GG_HIP(m, hipMemcpyAsync((void*)p.pre_nl, h.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    // pass 2 -> bases per block, last non-dropped byte before each block
+    // pass 2 -> bases, run starts (as if no base before), first byte a base?, last non-dropped byte
     GG_HIP(m, parse_batch_pass(2, p, st));
     GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_bases, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipMemcpyAsync(h2.data(), p.blk_last, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipMemcpyAsync(hr.data(), p.blk_runs, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipMemcpyAsync(hf.data(), p.blk_first, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
     stamp("pass 2");
     for (uint32_t b = 0; b < nb; ++b) fbases[bfile[b]] += h[b];
     for (uint32_t f = 0; f < nf; ++f) gofs[f + 1] = gofs[f] + (fbases[f] + 15) / 16 * 16;  // genomes on words
-    {
-      std::vector<uint64_t> boff(nb);
-      uint64_t cur = 0;
-      uint32_t cf = ~0u;
-      for (uint32_t b = 0; b < nb; ++b) {
-        if (bfile[b] != cf) {
-          cf = bfile[b];
-          cur = gofs[cf];
-        }
-        boff[b] = cur;
-        cur += h[b];
+    std::vector<uint64_t> boff(nb);
+    uint64_t cur = 0;
+    uint32_t cf = ~0u;
+    for (uint32_t b = 0; b < nb; ++b) {
+      if (bfile[b] != cf) {
+        cf = bfile[b];
+        cur = gofs[cf];
       }
-      GG_HIP(m, hipMemcpyAsync((void*)p.base_off, boff.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-      uint64_t last = 0;
-      for (uint32_t b = 0; b < nb; ++b) {
-        const uint64_t x = h2[b];
-        h2[b] = last;
-        if (x) last = x;
-      }
-      GG_HIP(m, hipMemcpyAsync((void*)p.pre_last, h2.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-      // pass 3 -> run starts per block
-      GG_HIP(m, parse_batch_pass(3, p, st));
-      GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_runs, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-      GG_HIP(m, hipStreamSynchronize(st));
-      stamp("pass 3");
-      for (uint32_t b = 0; b < nb; ++b) {
-        const uint64_t x = h[b];
-        h[b] = n_starts;
-        n_starts += x;
-      }
-      GG_HIP(m, hipMemcpyAsync((void*)p.run_off, h.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+      boff[b] = cur;
+      cur += h[b];
     }
+    GG_HIP(m, hipMemcpyAsync((void*)p.base_off, boff.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    // the last non-dropped byte before each block; a block whose first
+    // non-dropped byte is a base continues the run of a block before it (in
+    // its file) that ended in a base
+    uint64_t last = 0;
+    for (uint32_t b = 0; b < nb; ++b) {
+      const uint64_t x = h2[b];
+      h2[b] = last;
+      if (x) last = x;
+      const uint64_t fs = foff[bfile[b]];
+      const bool prev_base = h2[b] && ((h2[b] >> 2) - 1) >= fs && (h2[b] & 3u) == 0;
+      const uint64_t runs = hr[b] - (prev_base && hf[b] ? 1 : 0);
+      hr[b] = n_starts;
+      n_starts += runs;
+    }
+    GG_HIP(m, hipMemcpyAsync((void*)p.pre_last, h2.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync((void*)p.run_off, hr.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   }
   const uint64_t total = gofs[nf];
   *n_words = total / 16;
-  uint8_t* codes;
   uint64_t* starts;
-  GG_HIP(m, scratch_t(m, "parse_codes", std::max<uint64_t>(total, 16), &codes));
   GG_HIP(m, scratch_t(m, "parse_starts", std::max<uint64_t>(n_starts, 1), &starts));
   GG_HIP(m, scratch_t(m, "stage_words", std::max<uint64_t>(*n_words, 1), d_words));
-  p.codes = codes;
   p.starts = starts;
   p.n_words = *n_words;
   p.words = *d_words;
   std::vector<uint64_t> hs(n_starts);
   if (nb) {
-    GG_HIP(m, hipMemsetAsync(codes, 0, std::max<uint64_t>(total, 16), st));
-    GG_HIP(m, parse_batch_pass(4, p, st));
-    GG_HIP(m, parse_batch_pass(5, p, st));
+    if (*n_words) GG_HIP(m, hipMemsetAsync(*d_words, 0, *n_words * sizeof(uint32_t), st));
+    GG_HIP(m, parse_batch_pass(3, p, st));
     if (n_starts) GG_HIP(m, hipMemcpyAsync(hs.data(), starts, n_starts * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
-    stamp("pass 4-5");
+    stamp("pass 3");
   }
   // runs: consecutive starts of one genome; a genome's last run ends at its
   // last base; keep runs of >= k bases

@@ -17,14 +17,14 @@
 // never enumerated by K1).
 //
 // Work is split in blocks of kBlockBytes bytes that never straddle files.
-// Four passes, each one coalesced read of the block, with tiny per-block
+// Three passes, each one coalesced read of the block, with tiny per-block
 // scans on the host in between:
 //   1. last '\n' of every block;
-//   2. with the line-start prefix: bases per block and the block's last
-//      non-dropped byte (index, header-or-break-or-base);
-//   3. with that prefix: run starts per block;
-//   4. emit every base's code byte at its packed position and every run
-//      start; then 16 code bytes -> one word.
+//   2. with the line-start prefix: bases per block, run starts (as if no
+//      base came before the block), whether the first non-dropped byte is a
+//      base, and the block's last non-dropped byte;
+//   3. with those prefixes: every base's 2-bit code into its packed word
+//      (assembled in LDS) and every run start.
 #include "device_util.hpp"
 #include "gg_internal.hpp"
 
@@ -134,19 +134,20 @@ struct ChunkClass {
 __device__ __forceinline__ void classify(const BlockArgs& a, uint64_t fstart, uint64_t nl_before /* index+1 or 0 */,
                                          uint64_t b1, const uint32_t (&c)[kPerThread], uint64_t i0, ChunkClass& out) {
   // line start of the chunk's first byte, and whether that line is a header
-  uint64_t ls = nl_before > fstart ? nl_before : fstart;
+  const uint64_t ls = nl_before > fstart ? nl_before : fstart;  // (<= i0)
   bool hdr = ls < a.n && a.raw[ls] == '>';
+  int32_t lsr = ls == i0 ? 0 : -1;  // a line start inside the chunk, relative to i0
+  const uint32_t lim = b1 > i0 ? (uint32_t)min<uint64_t>(b1 - i0, kPerThread) : 0u;  // bytes of the block in the chunk
 #pragma unroll
   for (int j = 0; j < kPerThread; ++j) {
-    const uint64_t i = i0 + j;
     uint32_t k;
-    if (i >= b1) {
+    if ((uint32_t)j >= lim) {
       k = kCodeSkip;
     } else {
-      if (i == ls) hdr = c[j] == '>';  // (a new line began at i)
+      if (j == lsr) hdr = c[j] == '>';  // (a new line began at j)
       if (c[j] == '\n') {
         k = kCodeSkip;
-        ls = i + 1;
+        lsr = j + 1;
       } else {
         k = hdr ? (uint32_t)kCodeBreak : byte_class(c[j]);
       }
@@ -166,39 +167,6 @@ __device__ __forceinline__ uint64_t thread_nl_prefix(const uint32_t (&c)[kPerThr
   auto mx = [](int64_t x, int64_t y) { return x > y ? x : y; };
   const int64_t ex = block_exclusive<int64_t>(last, 0, mx, sh, nullptr);
   return (uint64_t)(ex > (int64_t)block_pre ? ex : (int64_t)block_pre);
-}
-
-// pass 2: bases per block, and the block's last non-dropped byte
-__global__ __launch_bounds__(kThreads) void parse_count_kernel(BlockArgs a, const uint64_t* __restrict__ blk_end,
-                                                              const uint64_t* __restrict__ pre_nl,
-                                                              uint64_t* __restrict__ blk_bases,
-                                                              uint64_t* __restrict__ blk_last) {
-  __shared__ int64_t shi[kThreads / 64];
-  __shared__ uint64_t shu[kThreads / 64];
-  const uint32_t b = blockIdx.x;
-  const uint64_t b1 = blk_end[b];
-  const uint64_t fstart = a.file_start[a.blk_file[b]];
-  uint32_t c[kPerThread];
-  uint64_t i0;
-  load_chunk(a, a.blk_start[b], b1, c, i0);
-  const uint64_t nlp = thread_nl_prefix(c, i0, b1, pre_nl[b], shi);
-  ChunkClass k;
-  classify(a, fstart, nlp, b1, c, i0, k);
-  uint64_t bases = 0, last = 0;
-#pragma unroll
-  for (int j = 0; j < kPerThread; ++j) {
-    if (k.cls[j] < 4) ++bases;
-    if (k.cls[j] != kCodeSkip) last = ((i0 + j + 1) << 2) | (k.cls[j] < 4 ? 0u : 1u);
-  }
-  uint64_t tb, tl;
-  auto add = [](uint64_t x, uint64_t y) { return x + y; };
-  (void)block_exclusive<uint64_t>(bases, 0, add, shu, &tb);
-  auto lat = [](uint64_t x, uint64_t y) { return later(x, y); };
-  (void)block_exclusive<uint64_t>(last, 0, lat, shu, &tl);
-  if (threadIdx.x == 0) {
-    blk_bases[b] = tb;
-    blk_last[b] = tl;
-  }
 }
 
 // run-start flags of one chunk given the last non-dropped byte before it
@@ -230,11 +198,16 @@ __device__ __forceinline__ uint64_t thread_last_prefix(const ChunkClass& k, uint
   return later(block_pre, ex);
 }
 
-// pass 3: run starts per block
-__global__ __launch_bounds__(kThreads) void parse_runs_kernel(BlockArgs a, const uint64_t* __restrict__ blk_end,
-                                                             const uint64_t* __restrict__ pre_nl,
-                                                             const uint64_t* __restrict__ pre_last,
-                                                             uint64_t* __restrict__ blk_runs) {
+// pass 2: per block its bases, its run starts counted as if no base came
+// before it (runs0), whether its first non-dropped byte is a base (the host
+// then takes one start off when the block before ends in a base), and its
+// last non-dropped byte
+__global__ __launch_bounds__(kThreads) void parse_count_kernel(BlockArgs a, const uint64_t* __restrict__ blk_end,
+                                                              const uint64_t* __restrict__ pre_nl,
+                                                              uint64_t* __restrict__ blk_bases,
+                                                              uint64_t* __restrict__ blk_runs0,
+                                                              uint64_t* __restrict__ blk_first,
+                                                              uint64_t* __restrict__ blk_last) {
   __shared__ int64_t shi[kThreads / 64];
   __shared__ uint64_t shu[kThreads / 64];
   const uint32_t b = blockIdx.x;
@@ -246,28 +219,54 @@ __global__ __launch_bounds__(kThreads) void parse_runs_kernel(BlockArgs a, const
   const uint64_t nlp = thread_nl_prefix(c, i0, b1, pre_nl[b], shi);
   ChunkClass k;
   classify(a, fstart, nlp, b1, c, i0, k);
-  const uint64_t prev = thread_last_prefix(k, i0, pre_last[b], shu);
+  // within the block: the last non-dropped byte before this thread's chunk
+  const uint64_t prev = thread_last_prefix(k, i0, 0, shu);
   bool st[kPerThread];
-  const uint64_t n = run_starts(k, prev, fstart, st, i0);
-  uint64_t tot;
+  uint64_t nr = run_starts(k, prev, 0, st, i0);  // (fstart 0: a byte before the chunk inside the block counts)
+  uint64_t bases = 0, last = 0, first = ~0ull;  // first: (index << 2 | kind) of the chunk's first non-dropped byte
+#pragma unroll
+  for (int j = kPerThread - 1; j >= 0; --j)
+    if (k.cls[j] != kCodeSkip) first = ((uint64_t)j << 2) | (k.cls[j] < 4 ? 0u : 1u);
+#pragma unroll
+  for (int j = 0; j < kPerThread; ++j) {
+    if (k.cls[j] < 4) ++bases;
+    if (k.cls[j] != kCodeSkip) last = ((i0 + j + 1) << 2) | (k.cls[j] < 4 ? 0u : 1u);
+  }
+  if (first != ~0ull) first += (uint64_t)threadIdx.x << 7;  // (block-relative index: thread * 32 + j)
+  uint64_t tb, tl, tr, tf;
   auto add = [](uint64_t x, uint64_t y) { return x + y; };
-  (void)block_exclusive<uint64_t>(n, 0, add, shu, &tot);
-  if (threadIdx.x == 0) blk_runs[b] = tot;
+  (void)block_exclusive<uint64_t>(bases, 0, add, shu, &tb);
+  auto lat = [](uint64_t x, uint64_t y) { return later(x, y); };
+  (void)block_exclusive<uint64_t>(last, 0, lat, shu, &tl);
+  (void)block_exclusive<uint64_t>(nr, 0, add, shu, &tr);
+  auto mn = [](uint64_t x, uint64_t y) { return x < y ? x : y; };
+  (void)block_exclusive<uint64_t>(first, ~0ull, mn, shu, &tf);
+  if (threadIdx.x == 0) {
+    blk_bases[b] = tb;
+    blk_last[b] = tl;
+    blk_runs0[b] = tr;
+    blk_first[b] = tf != ~0ull && (tf & 3u) == 0;
+  }
 }
 
-// pass 4: code bytes at their packed positions, run starts (packed position)
+// pass 3: 2-bit codes straight into the packed words (the block's words
+// assembled in LDS; the first and last, which a neighbouring block may
+// share, merged with atomicOr; words pre-cleared), and every run start
+// (packed position)
 __global__ __launch_bounds__(kThreads) void parse_emit_kernel(BlockArgs a, const uint64_t* __restrict__ blk_end,
                                                              const uint64_t* __restrict__ pre_nl,
                                                              const uint64_t* __restrict__ pre_last,
                                                              const uint64_t* __restrict__ base_off,
                                                              const uint64_t* __restrict__ run_off,
-                                                             uint8_t* __restrict__ codes,
+                                                             uint32_t* __restrict__ words,
                                                              uint64_t* __restrict__ starts) {
   __shared__ int64_t shi[kThreads / 64];
   __shared__ uint64_t shu[kThreads / 64];
+  __shared__ uint32_t wl[kBlockBytes / 16 + 2];
   const uint32_t b = blockIdx.x;
   const uint64_t b1 = blk_end[b];
   const uint64_t fstart = a.file_start[a.blk_file[b]];
+  for (uint32_t i = threadIdx.x; i < kBlockBytes / 16 + 2; i += kThreads) wl[i] = 0;
   uint32_t c[kPerThread];
   uint64_t i0;
   load_chunk(a, a.blk_start[b], b1, c, i0);
@@ -281,28 +280,26 @@ __global__ __launch_bounds__(kThreads) void parse_emit_kernel(BlockArgs a, const
 #pragma unroll
   for (int j = 0; j < kPerThread; ++j) nb += k.cls[j] < 4;
   auto add = [](uint64_t x, uint64_t y) { return x + y; };
-  uint64_t pos = base_off[b] + block_exclusive<uint64_t>(nb, 0, add, shu, nullptr);
+  uint64_t total;
+  const uint64_t p0 = base_off[b];
+  const uint64_t w0 = p0 >> 4;
+  uint64_t pos = p0 + block_exclusive<uint64_t>(nb, 0, add, shu, &total);
   uint64_t rr = run_off[b] + block_exclusive<uint64_t>(nr, 0, add, shu, nullptr);
+  __syncthreads();  // (wl cleared)
 #pragma unroll
   for (int j = 0; j < kPerThread; ++j) {
     if (k.cls[j] >= 4) continue;
     if (st[j]) starts[rr++] = pos;
-    codes[pos++] = (uint8_t)k.cls[j];
+    atomicOr(&wl[(uint32_t)((pos >> 4) - w0)], k.cls[j] << (30u - 2u * (uint32_t)(pos & 15u)));
+    ++pos;
   }
-}
-
-// 16 code bytes -> one word, first base in bits 31..30
-__global__ __launch_bounds__(256) void parse_pack_kernel(const uint8_t* __restrict__ codes, uint64_t n_words,
-                                                         uint32_t* __restrict__ words) {
-  for (uint64_t w = (uint64_t)blockIdx.x * 256 + threadIdx.x; w < n_words; w += (uint64_t)gridDim.x * 256) {
-    const uint4 v = *(const uint4*)(codes + 16 * w);
-    const uint32_t x[4] = {v.x, v.y, v.z, v.w};
-    uint32_t out = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) out |= ((x[q] >> (8 * j)) & 3u) << (30 - 2 * (4 * q + j));
-    words[w] = out;
+  __syncthreads();
+  if (total) {
+    const uint32_t nw = (uint32_t)(((p0 + total - 1) >> 4) - w0 + 1);
+    for (uint32_t i = threadIdx.x; i < nw; i += kThreads) {
+      if (i == 0 || i + 1 == nw) atomicOr(&words[w0 + i], wl[i]);
+      else words[w0 + i] = wl[i];
+    }
   }
 }
 
@@ -316,21 +313,13 @@ hipError_t parse_batch_pass(int pass, const ParseLaunch& p, hipStream_t st) {
       hipLaunchKernelGGL(parse_nl_kernel, grid, block, 0, st, a, p.blk_end, p.blk_nl);
       break;
     case 2:
-      hipLaunchKernelGGL(parse_count_kernel, grid, block, 0, st, a, p.blk_end, p.pre_nl, p.blk_bases, p.blk_last);
+      hipLaunchKernelGGL(parse_count_kernel, grid, block, 0, st, a, p.blk_end, p.pre_nl, p.blk_bases, p.blk_runs,
+                         p.blk_first, p.blk_last);
       break;
     case 3:
-      hipLaunchKernelGGL(parse_runs_kernel, grid, block, 0, st, a, p.blk_end, p.pre_nl, p.pre_last, p.blk_runs);
-      break;
-    case 4:
       hipLaunchKernelGGL(parse_emit_kernel, grid, block, 0, st, a, p.blk_end, p.pre_nl, p.pre_last, p.base_off,
-                         p.run_off, p.codes, p.starts);
+                         p.run_off, p.words, p.starts);
       break;
-    case 5: {
-      const uint64_t blocks = std::min<uint64_t>(65536, (p.n_words + 255) / 256);
-      if (p.n_words) hipLaunchKernelGGL(parse_pack_kernel, dim3((uint32_t)std::max<uint64_t>(1, blocks)), dim3(256), 0,
-                                        st, p.codes, p.n_words, p.words);
-      break;
-    }
     default:
       return hipErrorInvalidValue;
   }

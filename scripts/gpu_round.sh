@@ -40,6 +40,11 @@ for st in $STAGES; do
       rc=$?; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc ;;
     inflate_probe)  # device vs host gzip inflate on C2-like files (reasons for a hand-back on stderr)
       GALAHGPU_INFLATE_DEBUG=1 run inflate_probe 600 python3 -u scripts/inflate_probe.py ${PROBE_FILES:-200} 3 || exit $? ;;
+    pmc_inflate)  # instruction counters of the device inflate kernels (one pass: 8 SQ counters)
+      export PROBE_MODES=device
+      run pmc_inflate 120 timeout -s KILL 100 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU \
+        SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_BRANCH SQ_WAVE_CYCLES SQ_WAIT_INST_ANY --kernel-include-regex 'inflate_|parse_' \
+        --output-format csv -d "$OUT/pmc_inflate" -o p -- python3 -u scripts/inflate_probe.py 100 1 || exit $? ;;
     inflate_prof)  # kernel trace + stats of the device inflate probe
       PROBE_MODES=device run inflate_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o inflate -- \
         python3 -u scripts/inflate_probe.py ${PROBE_FILES:-200} 2 || exit $? ;;
