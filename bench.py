@@ -447,13 +447,16 @@ def files_leg(a, device, steps):
                     "pairs_found": int(found), "phase_ms": {p: round(v / len(times), 2) for p, v in ph.items()},
                     "inflate_host_batches": fb}, pairs
 
-        host, hp = timed("host")
-        out.update(host)
-        t = host["s_per_call_median"]
-        # the same files inflated on the GPU (inflate.hip): the host threads only read
+        # the default path for gzip files: inflated on the GPU (inflate.hip), the host threads only read
         dev, dp = timed("device")
-        dev["same_pairs_as_host"] = bool(np.array_equal(hp, dp))
-        out["device_inflate"] = dev
+        out.update(dev)
+        out["inflate"] = "device"
+        t = dev["s_per_call_median"]
+        # the same files gunzipped and packed on the host threads (GALAHGPU_INFLATE=host, round 3's path)
+        host, hp = timed("host")
+        out["host_inflate"] = host
+        out["same_pairs_as_host_inflate"] = bool(np.array_equal(hp, dp))
+        out["device_over_host_inflate"] = round(host["s_per_call_median"] / t, 3)
         probe = os.path.join(ROOT, "scripts", "gunzip_probe")
         if os.path.exists(probe):
             r = subprocess.run([probe, str(T)] + paths, capture_output=True, text=True, timeout=300)
@@ -465,9 +468,10 @@ def files_leg(a, device, steps):
             else:
                 out["pure_decode_error"] = r.stderr[-300:]
         out["note"] = ("kernel-only headline vs this: the same path from gzip files on %d host threads; galah's "
-                       "distances() starts from these paths (src/finch.rs:47); top level: gunzip + parse + pack on "
-                       "the host threads (GALAHGPU_INFLATE=host); device_inflate: gzip bytes to the GPU, inflated "
-                       "and parsed there (inflate.hip, parse.hip)" % T)
+                       "distances() starts from these paths (src/finch.rs:47); top level: the default for gzip "
+                       "files, gzip bytes to the GPU, inflated and parsed there (inflate.hip, parse.hip), the host "
+                       "threads only read; host_inflate: gunzip + parse + pack on the host threads "
+                       "(GALAHGPU_INFLATE=host); pure_decode: read + libdeflate gunzip alone on the same threads" % T)
     finally:
         shutil.rmtree(d, ignore_errors=True)
     return out

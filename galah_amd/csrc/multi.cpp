@@ -320,12 +320,18 @@ bool device_parse() {
   return e && strcmp(e, "device") == 0;
 }
 
-// GALAHGPU_INFLATE=device: gzip files go to the device compressed and are
-// inflated there (inflate.hip), then parsed there (parse.hip); the host
-// threads only read files.
-bool device_inflate() {
+// Device inflate: gzip files go to the device compressed and are inflated
+// there (inflate.hip), then parsed there (parse.hip); the host threads only
+// read files.  The default when the file list starts with a .gz path (the
+// device parses the other files' text too); GALAHGPU_INFLATE=device / host
+// forces either path.
+bool device_inflate(const char* const* paths, uint32_t n) {
   const char* e = getenv("GALAHGPU_INFLATE");
-  return e && strcmp(e, "device") == 0;
+  if (e && strcmp(e, "device") == 0) return true;
+  if (e && strcmp(e, "host") == 0) return false;
+  if (n == 0 || !paths[0]) return false;
+  const size_t l = strlen(paths[0]);
+  return l >= 3 && strcmp(paths[0] + l - 3, ".gz") == 0;
 }
 
 // One batch of FASTA text, already in device memory (d_text, files at
@@ -764,7 +770,7 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
   const uint32_t nm = (uint32_t)miss.size();
   // in-flight packed genomes: ~2 batches per member, at least 1 GiB
   const uint64_t budget = std::max<uint64_t>(1ull << 30, 2ull * M * kBatchWords * sizeof(uint32_t));
-  const bool gz_dev = device_inflate();
+  const bool gz_dev = device_inflate(miss.data(), (uint32_t)miss.size());
   const bool raw = gz_dev || device_parse();
   // staging copies per member: the host threads shared among the members
   const int copy_threads = std::max(1, std::min(16, ingest_threads(c->host_threads)) / (int)M);
