@@ -45,12 +45,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 CLK_GHZ = 2.4          # max engine clock (MI355X_MICROARCH.md chip parameters)
 N_SIMD = 256 * 4       # 256 CUs x 4 SIMDs
 # K1's VALU-issue ceiling (the kernel is bound by VALU issue; its input is
-# 0.25 B per k-mer, ~2% of HBM): profiles/r03_k1_issue_model.json, written by
+# 0.25 B per k-mer, ~2% of HBM): profiles/r04_k1_issue_model.json, written by
 # scripts/k1_issue_model.py from a rocprofv3 PMC pass over K1 at HEAD and the
 # per-opcode issue costs measured by scripts/ubench_dual.hip.  The model
 # records a fingerprint of K1's machine code; bench.py recomputes it from the
 # library it loads and flags the peak as stale when K1 has changed since.
-ISSUE_MODEL = os.path.join(ROOT, "profiles", "r03_k1_issue_model.json")
+ISSUE_MODEL = os.path.join(ROOT, "profiles", "r04_k1_issue_model.json")
 # K2's per-kernel PMC summary (HBM bytes from FETCH_SIZE x 2 and WRITE_SIZE,
 # VALU issue share, LDS-array utilisation) of the bucketed inverted index:
 # scripts/k2_pmc.sh + scripts/k2_pmc_model.py
@@ -260,6 +260,7 @@ def roofline(kst_sk, kst_pr, s, config_note, config=None):
             "frac_vs_guide_valu": round(dom["frac_vs_guide_valu"], 4) if "frac_vs_guide_valu" in dom else None,
             "frac_issue_model": round(dom["frac_issue_model"], 4) if "frac_issue_model" in dom else None,
             "hbm_frac": round(dom["hbm_frac"], 4) if "hbm_frac" in dom else None,
+            "peak_stale": dom.get("peak_stale"),
             "traffic": (round(2 * model["hbm_bytes_per_kmer_pmc"] * kmers) if (model and dom is k1
                         and model.get("hbm_bytes_per_kmer_pmc")) else None),
             "kernel": dom["kernel"], "avg_launch_ms": round(dom["avg_ms"], 4),
@@ -267,7 +268,7 @@ def roofline(kst_sk, kst_pr, s, config_note, config=None):
                      "%.1f GHz x 64 k-mers / (K1's VALU instructions per wave-k-mer, PMC at HEAD, x 2 cycles: "
                      "MI355X_MICROARCH.md's wave64 VALU issue); frac_issue_model prices the same instructions at the "
                      "issue cost of their class measured on this chip (simple 32-bit ~2.3 cycles, other 32-bit ~4.2, "
-                     "64-bit ~5.0; profiles/r03_k1_issue_model.json, DESIGN §4); traffic = HBM bytes per launch "
+                     "64-bit ~5.0; profiles/r04_k1_issue_model.json, DESIGN §4); traffic = HBM bytes per launch "
                      "from the PMC pass: FETCH_SIZE x 2 (the gfx950 factor, calibrated for 4-, 8- and 16-B loads by "
                      "scripts/ubench_fetch.hip) per k-mer x k-mers; %s"
                      % (CLK_GHZ, config_note)),

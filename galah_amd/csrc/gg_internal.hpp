@@ -433,6 +433,9 @@ class PackStream {
                 std::string* err);
   // raw streams: genome i's FASTA text.  Valid until release(i).
   gg_status get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err, bool* gz = nullptr);
+  // raw streams: genome i's bytes (keep_gzip: a gzip file may be mapped
+  // rather than read; get_raw then gives an empty text).  Valid until release(i).
+  gg_status get_bytes(uint32_t i, const uint8_t** data, size_t* len, std::string* err, bool* gz);
   // The file's size and mtime as stat'ed just before it was read (valid
   // after get(i) succeeded; the streams are built with stamp_files).
   FileStamp stamp(uint32_t i);

@@ -282,12 +282,12 @@ gg_status pairs_with_ani(gg_ctx* c, const std::vector<gg_pair>& res, gg_pair** p
 constexpr uint32_t kBatchGenomes = 32;          // genomes per K1 batch
 constexpr uint64_t kBatchWords = 64ull << 20;   // or 1 Gbases of packed words, whichever first
 constexpr uint64_t kBatchText = 1ull << 30;     // raw (device-parsed) batches: 1 GiB of FASTA text
-// device-inflate batches: up to 4096 files, 384 MiB of gzip data or 960 MiB
+// device-inflate batches: up to 4096 files, 192 MiB of gzip data or 600 MiB
 // of text (the inflate's parallel units are the streams' blocks, ~30 per
 // 3 Mbp genome: a batch needs hundreds of files to fill the GPU)
 constexpr uint32_t kBatchGenomesGz = 4096;
-constexpr uint64_t kBatchGzBytes = 384ull << 20;
-constexpr uint64_t kBatchGzText = 960ull << 20;  // (inflate_batch: text < 1 GiB)
+constexpr uint64_t kBatchGzBytes = 192ull << 20;
+constexpr uint64_t kBatchGzText = 600ull << 20;  // (inflate_batch: text < 1 GiB)
 
 // memcpy on up to T threads (staging copies of a batch into pinned memory:
 // one thread moves ~10 GB/s, a batch of FASTA text is up to 1 GiB)
@@ -559,9 +559,10 @@ class GzPipe {
     uint64_t up = 0;  // bytes [0, up) are queued to sl.dev
     uint64_t gz_bytes = 0, text_est = 0;
     for (uint32_t i = g.b0; i < g.b1; ++i) {
-      const std::vector<uint8_t>* tx;
+      const uint8_t* fb;
+      size_t fl;
       bool gz = false;
-      const gg_status gs = stream_.get_raw(i, &tx, &g.err, &gz);
+      const gg_status gs = stream_.get_bytes(i, &fb, &fl, &g.err, &gz);
       if (gs != GG_OK) {
         g.st = gs;
         g.file_err = true;
@@ -569,12 +570,12 @@ class GzPipe {
         return true;
       }
       InflateFile f;
-      size_t doff = 0, dlen = tx->size();
+      size_t doff = 0, dlen = fl;
       uint32_t isz = 0, crc = 0;
-      const bool member = gz && gzip_member(tx->data(), tx->size(), &doff, &dlen, &isz, &crc);
+      const bool member = gz && gzip_member(fb, fl, &doff, &dlen, &isz, &crc);
       if (gz && !member) g.host_only = true;
       const uint64_t p = (g.at + doff + 3) / 4 * 4 - doff;
-      const uint64_t need = p + tx->size() + 16;
+      const uint64_t need = p + fl + 16;
       if (need > sl.host_cap || need + kInflatePad > sl.dev_cap) {  // grow the slot (a batch of large files)
         if (!hip(hipStreamSynchronize(sl.st), "hipStreamSynchronize")) return true;
         const uint64_t cap = std::max<uint64_t>(need + kInflatePad, 2 * kBatchGzBytes);
@@ -595,22 +596,22 @@ class GzPipe {
           up = 0;  // (queued again from the host copy)
         }
       }
-      parallel_copy(sl.host + p, tx->data(), tx->size(), threads_);
+      parallel_copy(sl.host + p, fb, fl, threads_);
       f.gz = member;
       f.data_off = p + doff;
       f.data_len = dlen;
       f.isize = isz;
       f.crc = crc;
       g.files.push_back(f);
-      g.held.push_back(GzHeld{p, tx->size(), gz});
-      g.at = p + tx->size();
+      g.held.push_back(GzHeld{p, fl, gz});
+      g.at = p + fl;
       if (g.at - up >= kUpPiece) {
         if (!hip(hipMemcpyAsync(sl.dev + up, sl.host + up, g.at - up, hipMemcpyHostToDevice, sl.st), "hipMemcpyAsync"))
           return true;
         up = g.at;
       }
-      gz_bytes += gz ? tx->size() : 0;
-      text_est += member ? isz : tx->size();
+      gz_bytes += gz ? fl : 0;
+      text_est += member ? isz : fl;
       g.row_of.push_back(miss_at_[i]);
       stream_.release(i);
       if ((gz_bytes >= kBatchGzBytes || text_est >= kBatchGzText) && i + 1 < g.b1) {  // cut the batch here
@@ -802,7 +803,9 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
     std::vector<uint64_t> out_rows;
     std::vector<uint32_t> out_lens;
     std::unique_ptr<GzPipe> pipe;
-    if (gz_dev) pipe.reset(new GzPipe(m, stream, nm, cursor_mu, cursor, stop, copy_threads, miss_at));
+    // (the staging copies of compressed files need few threads: the
+    // PackStream workers reading the files share the host's CPUs)
+    if (gz_dev) pipe.reset(new GzPipe(m, stream, nm, cursor_mu, cursor, stop, std::min(copy_threads, 4), miss_at));
     for (;;) {
       uint32_t b0, b1;
       GzStaged* staged = nullptr;

@@ -17,6 +17,10 @@
 #include <sched.h>
 #include <smmintrin.h>
 #include <tmmintrin.h>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -77,6 +81,13 @@ struct GenomePacker {
   int k;
   std::vector<uint8_t> text;  // raw streams: the FASTA text (parse.hip), or the gzip file itself (gz)
   bool gz = false;
+  // keep_gzip streams: the gzip file mapped (its page-cache pages, no copy)
+  // instead of read into text
+  const uint8_t* map = nullptr;
+  size_t map_len = 0;
+  ~GenomePacker() {
+    if (map) munmap((void*)map, map_len);
+  }
   std::vector<uint32_t> words;
   std::vector<gg_run> runs;  // base relative to this genome's first word
   uint64_t n_bases = 0;
@@ -234,6 +245,32 @@ struct Deflate {
 const Deflate& deflate_lib() {
   static const Deflate d;
   return d;
+}
+
+// A gzip file mapped read-only with its pages populated (the page cache's
+// own pages: the device-inflate staging copies straight from them); false
+// (nothing mapped) for an empty, unreadable or non-gzip file, which then
+// takes the read path and its error.
+bool map_gzip(const char* path, GenomePacker& gp) {
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return false;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || sb.st_size < 18) {
+    close(fd);
+    return false;
+  }
+  void* p = mmap(nullptr, (size_t)sb.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return false;
+  const uint8_t* b = (const uint8_t*)p;
+  if (b[0] != 0x1f || b[1] != 0x8b) {
+    munmap(p, (size_t)sb.st_size);
+    return false;
+  }
+  gp.map = b;
+  gp.map_len = (size_t)sb.st_size;
+  gp.gz = true;
+  return true;
 }
 
 bool read_raw(const char* path, std::vector<uint8_t>& raw, std::string& err) {
@@ -528,6 +565,7 @@ struct PackStream::Impl {
       if (!paths[i]) {
         s = GG_ERR_INVALID_ARG;
         e = "null path";
+      } else if (raw && keep_gzip && map_gzip(paths[i], *gp)) {  // gzip, mapped: stays compressed (device inflate)
       } else if (raw && keep_gzip) {  // gzip files stay compressed (device inflate)
         if (!read_raw(paths[i], buf, e)) {
           s = GG_ERR_IO;
@@ -548,7 +586,8 @@ struct PackStream::Impl {
       if (buf.capacity() > (256u << 20)) std::vector<uint8_t>().swap(buf);  // do not pin a huge buffer
       {
         std::lock_guard<std::mutex> lk(mu);
-        inflight += gp->words.size() * sizeof(uint32_t) + gp->runs.size() * sizeof(gg_run) + gp->text.size();
+        inflight += gp->words.size() * sizeof(uint32_t) + gp->runs.size() * sizeof(gg_run) + gp->text.size() +
+                    gp->map_len;
         g[i] = std::move(gp);
         st[i] = s;
         err[i] = std::move(e);
@@ -629,6 +668,17 @@ gg_status PackStream::get_raw(uint32_t i, const std::vector<uint8_t>** text, std
   return GG_OK;
 }
 
+gg_status PackStream::get_bytes(uint32_t i, const uint8_t** data, size_t* len, std::string* err, bool* gz) {
+  const std::vector<uint8_t>* t = nullptr;
+  const gg_status st = get_raw(i, &t, err, gz);
+  if (st != GG_OK) return st;
+  std::lock_guard<std::mutex> lk(p_->mu);
+  const GenomePacker& g = *p_->g[i];
+  *data = g.map ? g.map : g.text.data();
+  *len = g.map ? g.map_len : g.text.size();
+  return GG_OK;
+}
+
 gg_status host_text_from_gzip(const std::vector<uint8_t>& gz, const char* name, std::vector<uint8_t>& text,
                               std::string& err) {
   std::vector<uint8_t> buf;
@@ -678,7 +728,8 @@ void PackStream::release(uint32_t i) {
   {
     std::lock_guard<std::mutex> lk(m.mu);
     if (m.state[i] != 2) return;
-    m.inflight -= m.g[i]->words.size() * sizeof(uint32_t) + m.g[i]->runs.size() * sizeof(gg_run) + m.g[i]->text.size();
+    m.inflight -= m.g[i]->words.size() * sizeof(uint32_t) + m.g[i]->runs.size() * sizeof(gg_run) + m.g[i]->text.size() +
+                  m.g[i]->map_len;
     m.g[i].reset();
     m.state[i] = 3;
     while (m.frontier < m.n && m.state[m.frontier] == 3) ++m.frontier;

@@ -1,4 +1,4 @@
-"""K1's VALU-issue ceiling at HEAD -> profiles/r03_k1_issue_model.json.
+"""K1's VALU-issue ceiling at HEAD -> profiles/r04_k1_issue_model.json.
 
 Inputs (all measured on the MI355X, committed under profiles/):
   * a rocprofv3 --pmc pass over one K1 launch at C3 (scripts/pmc_head.sh):
@@ -72,10 +72,10 @@ def class_costs(ubench_csv):
 
 def main():
     pmc_dir = sys.argv[1]
-    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "profiles", "r03_k1_issue_model.json")
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "profiles", "r04_k1_issue_model.json")
     lib = os.path.join(ROOT, "galah_amd", "lib", "libgalahgpu.so")
     c, dur = counters(pmc_dir, "sketch_candidates_kernel<21")
-    costs = class_costs(os.path.join(ROOT, "profiles", "r02_pmc_ubench_dual.csv"))
+    costs = class_costs(os.path.join(ROOT, "profiles", "ubench", "r02_pmc_ubench_dual.csv"))
     listing = k1_isa.kernel_listing(lib)
     hs = k1_isa.histogram(listing)
     h = k1_isa.histogram(k1_isa.hot_path(k1_isa.kernel_listing(lib, with_addr=True)))
