@@ -286,8 +286,23 @@ constexpr uint64_t kBatchText = 1ull << 30;     // raw (device-parsed) batches: 
 // of text (the inflate's parallel units are the streams' blocks, ~30 per
 // 3 Mbp genome: a batch needs hundreds of files to fill the GPU)
 constexpr uint32_t kBatchGenomesGz = 4096;
-constexpr uint64_t kBatchGzBytes = 192ull << 20;
-constexpr uint64_t kBatchGzText = 600ull << 20;  // (inflate_batch: text < 1 GiB)
+// (GALAHGPU_GZ_BATCH_MB sets the gzip bytes per batch, the text cap follows
+// at 3x, at most 960 MiB: tuning only, no result depends on it)
+uint64_t gz_batch_bytes() {
+  static const uint64_t v = [] {
+    const char* e = getenv("GALAHGPU_GZ_BATCH_MB");
+    const long mb = e ? atol(e) : 0;
+    return (uint64_t)(mb > 0 ? std::min(mb, 320L) : 192L) << 20;
+  }();
+  return v;
+}
+uint64_t gz_batch_text() { return std::min<uint64_t>(3 * gz_batch_bytes(), 960ull << 20); }  // (text < 1 GiB)
+// staging copy threads per member (GALAHGPU_GZ_COPY_THREADS; tuning only)
+int gz_copy_threads(int copy_threads) {
+  const char* e = getenv("GALAHGPU_GZ_COPY_THREADS");
+  const int t = e ? atoi(e) : 0;
+  return std::max(1, t > 0 ? std::min(t, copy_threads) : std::min(copy_threads, 4));
+}
 
 // memcpy on up to T threads (staging copies of a batch into pinned memory:
 // one thread moves ~10 GB/s, a batch of FASTA text is up to 1 GiB)
@@ -482,7 +497,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
 // into the slot's pinned buffer (gzip files compressed, each positioned so
 // its deflate data starts on a 4-byte boundary) and queued to the slot's
 // device buffer on the slot's stream as they are staged.  A batch is cut
-// early at kBatchGzBytes of gzip data or kBatchGzText of text (the rest
+// early at gz_batch_bytes() of gzip data or gz_batch_text() of text (the rest
 // goes back through the cursor).  A batch the device inflate does not take
 // is decoded on the host threads instead (GG_FALLBACK_INFLATE_HOST).
 struct GzHeld {
@@ -578,7 +593,7 @@ class GzPipe {
       const uint64_t need = p + fl + 16;
       if (need > sl.host_cap || need + kInflatePad > sl.dev_cap) {  // grow the slot (a batch of large files)
         if (!hip(hipStreamSynchronize(sl.st), "hipStreamSynchronize")) return true;
-        const uint64_t cap = std::max<uint64_t>(need + kInflatePad, 2 * kBatchGzBytes);
+        const uint64_t cap = std::max<uint64_t>(need + kInflatePad, 2 * gz_batch_bytes());
         if (need > sl.host_cap) {
           uint8_t* h = nullptr;
           if (!hip(hipHostMalloc((void**)&h, cap, hipHostMallocDefault), "hipHostMalloc")) return true;
@@ -614,7 +629,7 @@ class GzPipe {
       text_est += member ? isz : fl;
       g.row_of.push_back(miss_at_[i]);
       stream_.release(i);
-      if ((gz_bytes >= kBatchGzBytes || text_est >= kBatchGzText) && i + 1 < g.b1) {  // cut the batch here
+      if ((gz_bytes >= gz_batch_bytes() || text_est >= gz_batch_text()) && i + 1 < g.b1) {  // cut the batch here
         std::lock_guard<std::mutex> lk(mu_);
         if (cursor_ == g.b1) {
           cursor_ = i + 1;
@@ -775,7 +790,7 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
   const bool raw = gz_dev || device_parse();
   // staging copies per member: the host threads shared among the members
   const int copy_threads = std::max(1, std::min(16, ingest_threads(c->host_threads)) / (int)M);
-  PackStream stream(miss.data(), nm, c->k, c->host_threads, gz_dev ? std::max<uint64_t>(budget, 3 * kBatchGzBytes) : budget,
+  PackStream stream(miss.data(), nm, c->k, c->host_threads, gz_dev ? std::max<uint64_t>(budget, 3 * gz_batch_bytes()) : budget,
                     cache_dir != nullptr, raw, gz_dev);
   std::mutex cursor_mu;
   uint32_t cursor = 0;
@@ -805,7 +820,7 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
     std::unique_ptr<GzPipe> pipe;
     // (the staging copies of compressed files need few threads: the
     // PackStream workers reading the files share the host's CPUs)
-    if (gz_dev) pipe.reset(new GzPipe(m, stream, nm, cursor_mu, cursor, stop, std::min(copy_threads, 4), miss_at));
+    if (gz_dev) pipe.reset(new GzPipe(m, stream, nm, cursor_mu, cursor, stop, gz_copy_threads(copy_threads), miss_at));
     for (;;) {
       uint32_t b0, b1;
       GzStaged* staged = nullptr;

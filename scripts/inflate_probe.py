@@ -38,7 +38,7 @@ try:
     for mode in modes:
         os.environ["GALAHGPU_INFLATE"] = mode
         with ga.Context(k=21, sketch_size=1000, host_threads=16) as ctx:
-            ctx.precluster_files(paths[:8], 0.95)
+            ctx.precluster_files(paths, np.float32(0.95))  # (warm-up: buffers sized for the batches)
             ts = []
             for _ in range(steps):
                 t0 = time.perf_counter()
