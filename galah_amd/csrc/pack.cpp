@@ -252,11 +252,8 @@ const Deflate& deflate_lib() {
 // (nothing mapped) for an empty, unreadable or non-gzip file, which then
 // takes the read path and its error.
 bool map_gzip(const char* path, GenomePacker& gp) {
-  static const bool off = [] {  // GALAHGPU_GZ_MMAP=0: read instead (tuning only)
-    const char* e = getenv("GALAHGPU_GZ_MMAP");
-    return e && *e == '0';
-  }();
-  if (off) return false;
+  const char* e = getenv("GALAHGPU_GZ_MMAP");  // =0: read instead (tuning only)
+  if (e && *e == '0') return false;
   const int fd = open(path, O_RDONLY);
   if (fd < 0) return false;
   struct stat sb;

@@ -157,3 +157,24 @@ def test_device_inflate_corrupt_and_empty_fail_as_host(tmp_path, monkeypatch):
                     ctx.sketch_files([str(p)])
                 errs[mode] = (e.value.status, str(e.value))
         assert errs["device"] == errs["host"], name
+
+
+@pytest.mark.gpu
+def test_device_inflate_is_the_default_and_knobs_change_nothing(golden, monkeypatch):
+    """A .gz list takes the device path with no knob set (the info line
+    counts no host-inflated batch); mapped vs read files, small batches and
+    one staging thread (tuning knobs) give the same sketches."""
+    monkeypatch.delenv("GALAHGPU_INFLATE", raising=False)
+    with ga.Context(k=21, sketch_size=1000) as ctx:
+        sk0, l0, _ = ctx.sketch_files([str(p) for p in golden["paths"]])
+        assert ctx.fallbacks()["inflate_host"] == 0
+        assert "host-inflated batches 0" in ctx.info_line()
+    assert (l0 == golden["lens"]).all()
+    for knobs in ({"GALAHGPU_GZ_MMAP": "0"}, {"GALAHGPU_GZ_COPY_THREADS": "1"}):
+        for k, v in knobs.items():
+            monkeypatch.setenv(k, v)
+        sk, lens, fb = sketch_files(golden["paths"], monkeypatch, "device")
+        for k in knobs:
+            monkeypatch.delenv(k)
+        assert fb["inflate_host"] == 0
+        assert (lens == l0).all() and all((sk[g][:lens[g]] == sk0[g][:l0[g]]).all() for g in range(len(lens)))
