@@ -693,6 +693,7 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
     for (uint32_t i = tid; i < nb; i += kExpandThreads) {
       const uint32_t x = v[i];
       a.val[base + i] = x;
+      a.text[base + i] = x >> 31 ? (uint8_t)x : kTextPtr;  // (kTextPtr: the resolve pass follows val there)
       ring[(uint32_t)(base + i) & (kRing - 1)] =
           x >> 31 ? (uint16_t)(x & 0xFFu) : (uint16_t)(kRingPtr | (uint32_t)(o0 - 1 - x));
     }
@@ -701,21 +702,32 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
     t0 += nt;
   }
   // a file's last segment: the padding up to the next file ('\n' parses as nothing)
-  for (uint64_t i = base + tid; i < a.lane_pad[seg]; i += kExpandThreads) a.val[i] = 0x80000000u | '\n';
+  for (uint64_t i = base + tid; i < a.lane_pad[seg]; i += kExpandThreads) a.text[i] = '\n';
   if (bad) atomicOr(a.flags, 1u);
 }
 
-// Pointers (into earlier segments) followed to their literals: 16 output
-// bytes per thread from one 64-byte load of val, every pointer of the 16
-// followed at once (independent loads), hop after hop until none is left
-// (one or two hops: a pointer's target is a literal or, if it lies in the
-// first 32 KB of its own segment, a pointer one segment further back).
+// Pointers (into earlier segments) followed to their literals, 16 text
+// bytes per thread: a group with no kTextPtr byte is done as the expand
+// wrote it; the others load their 16 val entries (one 64-byte load) and
+// follow every pointer at once (independent loads), hop after hop until
+// none is left (one or two hops: a pointer's target is a literal or, if it
+// lies in the first 32 KB of its own segment, a pointer one segment further
+// back).  (A literal 0xFF byte only sends its group down the val path.)
 __global__ __launch_bounds__(256) void inflate_resolve_kernel(const uint32_t* __restrict__ val,
                                                               uint8_t* __restrict__ text, uint64_t n,
                                                               uint32_t* __restrict__ flags) {
   for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g * 16 < n; g += (uint64_t)gridDim.x * 256) {
+    const bool whole = g * 16 + 16 <= n;
+    if (whole) {
+      const uint4 q = *(const uint4*)(text + g * 16);
+      const uint32_t w[4] = {~q.x, ~q.y, ~q.z, ~q.w};  // (a kTextPtr byte: a zero byte of ~w)
+      bool any = false;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) any |= ((w[k] - 0x01010101u) & ~w[k] & 0x80808080u) != 0;
+      if (!any) continue;
+    }
     uint32_t x[16];
-    if (g * 16 + 16 <= n) {
+    if (whole) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint4 w = *(const uint4*)(val + g * 16 + 4 * q);
@@ -744,7 +756,7 @@ __global__ __launch_bounds__(256) void inflate_resolve_kernel(const uint32_t* __
     uint32_t out[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int b = 0; b < 16; ++b) out[b >> 2] |= (x[b] & 0xFFu) << (8 * (b & 3));
-    if (g * 16 + 16 <= n) *(uint4*)(text + g * 16) = make_uint4(out[0], out[1], out[2], out[3]);
+    if (whole) *(uint4*)(text + g * 16) = make_uint4(out[0], out[1], out[2], out[3]);
     else
       for (int b = 0; b < 16 && g * 16 + b < n; ++b) text[g * 16 + b] = (uint8_t)(out[b >> 2] >> (8 * (b & 3)));
   }
@@ -906,7 +918,7 @@ hipError_t launch_inflate_place(const InflatePlace& a, uint64_t text_len, uint8_
   const uint64_t groups = (text_len + 15) / 16;
   if (groups)
     hipLaunchKernelGGL(inflate_resolve_kernel, dim3((uint32_t)std::min<uint64_t>(65536, (groups + 255) / 256)),
-                       dim3(256), 0, st, a.val, text, text_len, a.flags);
+                       dim3(256), 0, st, a.val, a.text, text_len, a.flags);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (n_segs)

@@ -305,9 +305,9 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   d_flen = d_ftext + nf;
   GG_HIP(m, scratch_t(m, "gz_flags", 2 * (size_t)nf + 1, &d_flags));
   d_crc = d_flags + 1;
-  for (uint32_t f = 0; f < nf; ++f)  // (plain files: their text is copied in after the resolve)
-    if (!files[f].gz && foff[f + 1] > foff[f])
-      GG_HIP(m, hipMemsetD32Async((hipDeviceptr_t)(d_val + foff[f]), 0x80000000u | '\n', foff[f + 1] - foff[f], st));
+  for (uint32_t f = 0; f < nf; ++f)  // (plain files: their text is copied in after the resolve; until then
+    if (!files[f].gz && foff[f + 1] > foff[f])  //  no byte of theirs may send the resolve to val)
+      GG_HIP(m, hipMemsetAsync(*d_text + foff[f], '\n', foff[f + 1] - foff[f], st));
   GG_HIP(m, hipMemsetAsync(d_flags, 0, sizeof(uint32_t), st));
   std::vector<uint64_t> ftext(2 * (size_t)nf);
   for (uint32_t f = 0; f < nf; ++f) {
@@ -333,6 +333,7 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   p.lane_out = d_lout;
   p.file_text = d_ftext;
   p.n_lanes = (uint32_t)live.size();
+  p.text = *d_text;
   p.val = d_val;
   p.flags = d_flags;
   std::vector<uint32_t> seg_first(nf + 1, 0);
@@ -353,7 +354,8 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   GG_HIP(m, hipMemcpyAsync(chk.data(), d_flags, chk.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   GG_HIP(m, hipStreamSynchronize(st));
   stamp("expand + resolve + crc");
-  if (chk[0]) return hand_back(chk[0] & 1 ? "distance before the file start" : "pointer chain", 0);
+  if (chk[0])
+    return hand_back(chk[0] & 1 ? "distance before the file start" : "pointer chain", 0);
   for (uint32_t f = 0; f < nf; ++f)
     if (files[f].gz && (chk[1 + f] != files[f].crc || chk[1 + nf + f] != '>'))  // (FASTQ, malformed: the host path)
       return hand_back(chk[1 + f] != files[f].crc ? "CRC-32" : "not FASTA", f);

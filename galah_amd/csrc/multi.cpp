@@ -497,8 +497,8 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
 // into the slot's pinned buffer (gzip files compressed, each positioned so
 // its deflate data starts on a 4-byte boundary) and queued to the slot's
 // device buffer on the slot's stream as they are staged.  A batch is cut
-// early at gz_batch_bytes() of gzip data or gz_batch_text() of text (the rest
-// goes back through the cursor).  A batch the device inflate does not take
+// early at gz_batch_bytes() of gzip data or gz_batch_text() of text (the
+// first two at 1/4 and 1/2 of that; the rest goes back through the cursor).  A batch the device inflate does not take
 // is decoded on the host threads instead (GG_FALLBACK_INFLATE_HOST).
 struct GzHeld {
   uint64_t pos, len;
@@ -515,6 +515,7 @@ struct GzStaged {
   bool file_err = false;
   std::string err;
   double ms = 0;
+  Clock::time_point t0;  // when staging began (debug)
 };
 
 class GzPipe {
@@ -562,6 +563,7 @@ class GzPipe {
       cursor_ = g.b1;
     }
     const auto t0 = Clock::now();
+    g.t0 = t0;
     gg_ctx::GzSlot& sl = m_->gz_slot[si];
     auto hip = [&](hipError_t e, const char* what) {
       if (e != hipSuccess && g.st == GG_OK) {
@@ -573,6 +575,11 @@ class GzPipe {
     if (!sl.st && !hip(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking), "hipStreamCreate")) return true;
     uint64_t up = 0;  // bytes [0, up) are queued to sl.dev
     uint64_t gz_bytes = 0, text_est = 0;
+    // the first batches smaller (1/4, 1/2): the device starts while the
+    // full-size ones are staged
+    const int ramp = n_staged_ < 2 ? 2 - n_staged_ : 0;
+    ++n_staged_;
+    const uint64_t cut_gz = gz_batch_bytes() >> ramp, cut_text = gz_batch_text() >> ramp;
     for (uint32_t i = g.b0; i < g.b1; ++i) {
       const uint8_t* fb;
       size_t fl;
@@ -629,7 +636,7 @@ class GzPipe {
       text_est += member ? isz : fl;
       g.row_of.push_back(miss_at_[i]);
       stream_.release(i);
-      if ((gz_bytes >= gz_batch_bytes() || text_est >= gz_batch_text()) && i + 1 < g.b1) {  // cut the batch here
+      if ((gz_bytes >= cut_gz || text_est >= cut_text) && i + 1 < g.b1) {  // cut the batch here
         std::lock_guard<std::mutex> lk(mu_);
         if (cursor_ == g.b1) {
           cursor_ = i + 1;
@@ -646,6 +653,7 @@ class GzPipe {
 
   gg_ctx* m_;
   PackStream& stream_;
+  int n_staged_ = 0;  // batches staged so far
   uint32_t nm_;
   std::mutex& mu_;
   uint32_t& cursor_;
@@ -681,7 +689,11 @@ gg_status inflate_staged_batch(gg_ctx* m, GzPipe& pipe, GzStaged& g, int copy_th
   up_done = m->copy_done;
   GG_HIP(m, hipEventRecord(up_done, pipe.up_stream()));
   GG_HIP(m, hipStreamWaitEvent(m->stream, up_done, 0));
-  if (dbg) fprintf(stderr, "[inflate] batch of %zu files staged in %.3f ms\n", g.files.size(), g.ms);
+  static const Clock::time_point t_proc = Clock::now();  // (debug: times since the process's first batch)
+  if (dbg)
+    fprintf(stderr, "[inflate] at %.3f ms: batch of %zu files staged in %.3f ms (staging began at %.3f ms)\n",
+            ms_since(t_proc), g.files.size(), g.ms,
+            std::chrono::duration<double, std::milli>(g.t0 - t_proc).count());
   uint8_t* d_text = nullptr;
   std::vector<uint64_t> foff;
   bool ok = false;
@@ -726,7 +738,7 @@ gg_status inflate_staged_batch(gg_ctx* m, GzPipe& pipe, GzStaged& g, int copy_th
     GG_HIP(m, hipStreamSynchronize(m->stream));
   }
   const gg_status ps = parse_raw_batch(m, d_text, foff, d_words, nw, runs);
-  if (dbg) fprintf(stderr, "[inflate] batch inflated and parsed in %.3f ms\n", ms_since(t0));
+  if (dbg) fprintf(stderr, "[inflate] at %.3f ms: batch inflated and parsed in %.3f ms\n", ms_since(t_proc), ms_since(t0));
   return ps;
 }
 
