@@ -394,6 +394,7 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
   uint64_t n_out = 0, out_bytes = 0;
   uint32_t status = kDecOk, fin = 0;
   for (;;) {
+    const uint64_t blk0 = pos;  // (this block's start)
     if (pos == end) {
       status = kDecOk;
       break;
@@ -514,9 +515,9 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
       }
       const uint64_t e_end = sE[c_end];
       const uint32_t st_end = sSt[c_end];
-      if (overrun) {
+      if (overrun) {  // (the host decodes again from this block's start, the tokens before it kept)
         status = kDecOverrun;
-        pos = e_end;
+        pos = blk0;
         break;
       }
       if (st_end == kSpanBad) {

@@ -151,6 +151,7 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     uint32_t file;
     uint64_t start, end, tok_off, cap, scr_off;
     uint64_t n_tok = 0, out_len = 0, last_end = 0;
+    uint64_t done_tok = 0, done_out = 0;  // tokens and bytes of the blocks before `start` (a resumed lane)
     uint32_t status = 0, bfin = 0;
     bool redo = true, alive = true;
   };
@@ -185,8 +186,8 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
       arg[k] = x.file;
       arg[nl + k] = x.start;
       arg[2 * (size_t)nl + k] = x.end;
-      arg[3 * (size_t)nl + k] = x.tok_off;
-      arg[4 * (size_t)nl + k] = x.cap;
+      arg[3 * (size_t)nl + k] = x.tok_off + x.done_tok;
+      arg[4 * (size_t)nl + k] = x.cap - x.done_tok;
       arg[5 * (size_t)nl + k] = x.scr_off;
     }
     uint64_t *d_arg, *d_res;
@@ -240,8 +241,8 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     const uint32_t* r32 = (const uint32_t*)(res.data() + 3 * (size_t)nl);
     for (uint32_t k = 0; k < nl; ++k) {
       Lane& x = lanes[redo[k]];
-      x.n_tok = res[k];
-      x.out_len = res[nl + k];
+      x.n_tok = x.done_tok + res[k];
+      x.out_len = x.done_out + res[nl + k];
       x.last_end = res[2 * (size_t)nl + k];
       x.status = r32[k];
       x.bfin = r32[nl + k];
@@ -249,7 +250,9 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     }
     // a lane that passed the next start without landing on it: that start is
     // not a block boundary -- the lane takes the next lane's range and token
-    // region (they follow its own) and is decoded again, alone
+    // region (they follow its own) and is decoded again, alone, from the
+    // start of the block that ran past (last_end), its earlier blocks' tokens
+    // kept (and its scratch, which the next lane's follows)
     for (uint32_t l = 0; l < (uint32_t)lanes.size(); ++l) {
       Lane& x = lanes[l];
       if (!x.alive || x.redo) continue;
@@ -258,6 +261,9 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
       const bool has_next = nx < lanes.size() && lanes[nx].file == x.file;
       if (x.status == inflate::kDecOverrun && has_next) {
         Lane& y = lanes[nx];
+        x.done_tok = x.n_tok;
+        x.done_out = x.out_len;
+        x.start = x.last_end;
         x.end = y.end;
         x.cap = y.tok_off + y.cap - x.tok_off;
         x.redo = true;
