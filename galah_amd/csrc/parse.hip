@@ -25,8 +25,11 @@
 //      base, and the block's last non-dropped byte;
 //   3. with those prefixes: every base's 2-bit code into its packed word
 //      (assembled in LDS) and every run start.
+// Passes 2 and 3 classify a thread's 32 bytes bit-parallel (parse_core.hpp:
+// masks, carry chains, compress) with two rounds of block scans each.
 #include "device_util.hpp"
 #include "gg_internal.hpp"
+#include "parse_core.hpp"
 
 namespace gg {
 namespace {
@@ -34,22 +37,6 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kPerThread = 32;
 constexpr uint32_t kBlockBytes = kThreads * kPerThread;  // 8 KiB
-
-enum : uint32_t { kCodeBreak = 4, kCodeSkip = 5 };
-// byte class: ACGTU (either case) -> code, whitespace -> skip, else break
-__device__ __forceinline__ uint32_t byte_class(uint32_t c) {
-  const uint32_t l = c | 0x20u;
-  if (l == 'a') return 0;
-  if (l == 'c') return 1;
-  if (l == 'g') return 2;
-  if (l == 't' || l == 'u') return 3;
-  if (c == ' ' || c == '\t' || c == '\r' || c == '\n') return kCodeSkip;
-  return kCodeBreak;
-}
-
-// last-non-dropped-byte record: (index + 1) << 2 | kind, 0 = none;
-// kind 0 = base, 1 = break or header
-__device__ __forceinline__ uint64_t later(uint64_t a, uint64_t b) { return b ? b : a; }
 
 __device__ __forceinline__ int64_t block_max_i64(int64_t v, int64_t* sh) {
   for (int o = 32; o > 0; o >>= 1) v = max(v, (int64_t)__shfl_xor((long long)v, o));
@@ -59,29 +46,6 @@ __device__ __forceinline__ int64_t block_max_i64(int64_t v, int64_t* sh) {
   for (int w = 1; w < kThreads / 64; ++w) r = max(r, sh[w]);
   __syncthreads();
   return r;
-}
-
-// exclusive scan across the block of a per-thread value with an
-// associative op; returns the thread's exclusive prefix (identity for 0)
-template <class T, class Op>
-__device__ __forceinline__ T block_exclusive(T v, T identity, Op op, T* sh, T* total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  T inc = v;
-  for (int o = 1; o < 64; o <<= 1) {
-    const T y = (T)__shfl_up(inc, o);
-    if (lane >= o) inc = op(y, inc);
-  }
-  if (lane == 63) sh[w] = inc;
-  __syncthreads();
-  T pre = identity;
-  for (int x = 0; x < w; ++x) pre = op(pre, sh[x]);
-  T all = identity;
-  for (int x = 0; x < kThreads / 64; ++x) all = op(all, sh[x]);
-  const T up = (T)__shfl_up(inc, 1);
-  const T excl = lane ? op(pre, up) : pre;
-  __syncthreads();
-  if (total) *total = all;
-  return excl;
 }
 
 struct BlockArgs {
@@ -125,134 +89,134 @@ __global__ __launch_bounds__(kThreads) void parse_nl_kernel(BlockArgs a, const u
   if (threadIdx.x == 0) blk_nl[b] = (uint64_t)last;
 }
 
-// The per-byte classes of one thread's chunk, given the line-start state at
-// its first byte.  cls: 0..3 base, kCodeBreak (break or header), kCodeSkip.
-struct ChunkClass {
-  uint32_t cls[kPerThread];
-};
-
-__device__ __forceinline__ void classify(const BlockArgs& a, uint64_t fstart, uint64_t nl_before /* index+1 or 0 */,
-                                         uint64_t b1, const uint32_t (&c)[kPerThread], uint64_t i0, ChunkClass& out) {
-  // line start of the chunk's first byte, and whether that line is a header
-  const uint64_t ls = nl_before > fstart ? nl_before : fstart;  // (<= i0)
-  bool hdr = ls < a.n && a.raw[ls] == '>';
-  int32_t lsr = ls == i0 ? 0 : -1;  // a line start inside the chunk, relative to i0
-  const uint32_t lim = b1 > i0 ? (uint32_t)min<uint64_t>(b1 - i0, kPerThread) : 0u;  // bytes of the block in the chunk
+// One round of block scans over the 256 threads: an exclusive max of vm and
+// an exclusive sum of vs, with both totals.  sh: [4][2], this round's own.
+__device__ __forceinline__ void block_scan(uint32_t vm, uint32_t vs, uint32_t (*sh)[2], uint32_t& exm, uint32_t& exs,
+                                           uint32_t& totm, uint32_t& tots) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t im = vm, is = vs;
 #pragma unroll
-  for (int j = 0; j < kPerThread; ++j) {
-    uint32_t k;
-    if ((uint32_t)j >= lim) {
-      k = kCodeSkip;
-    } else {
-      if (j == lsr) hdr = c[j] == '>';  // (a new line began at j)
-      if (c[j] == '\n') {
-        k = kCodeSkip;
-        lsr = j + 1;
-      } else {
-        k = hdr ? (uint32_t)kCodeBreak : byte_class(c[j]);
-      }
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t ym = __shfl_up(im, o), ys = __shfl_up(is, o);
+    if (lane >= o) {
+      im = max(im, ym);
+      is += ys;
     }
-    out.cls[j] = k;
   }
-}
-
-// line-start prefix of each thread: the block's prefix, then the threads
-// before it (max of last '\n' index + 1)
-__device__ __forceinline__ uint64_t thread_nl_prefix(const uint32_t (&c)[kPerThread], uint64_t i0, uint64_t b1,
-                                                     uint64_t block_pre, int64_t* sh) {
-  int64_t last = 0;
-#pragma unroll
-  for (int j = 0; j < kPerThread; ++j)
-    if (c[j] == '\n' && i0 + j < b1) last = (int64_t)(i0 + j + 1);
-  auto mx = [](int64_t x, int64_t y) { return x > y ? x : y; };
-  const int64_t ex = block_exclusive<int64_t>(last, 0, mx, sh, nullptr);
-  return (uint64_t)(ex > (int64_t)block_pre ? ex : (int64_t)block_pre);
-}
-
-// run-start flags of one chunk given the last non-dropped byte before it
-__device__ __forceinline__ uint32_t run_starts(const ChunkClass& k, uint64_t prev, uint64_t fstart, bool (&start)[kPerThread],
-                                               uint64_t i0) {
-  // prev: (index + 1) << 2 | kind of the last non-dropped byte before the
-  // chunk (0 = none); bytes before the file do not count
-  bool prev_base = prev && ((prev >> 2) - 1) >= fstart && (prev & 3u) == 0;
-  uint32_t n = 0;
-#pragma unroll
-  for (int j = 0; j < kPerThread; ++j) {
-    const uint32_t x = k.cls[j];
-    start[j] = x < 4 && !prev_base;
-    n += start[j];
-    if (x != kCodeSkip) prev_base = x < 4;
+  const uint32_t up = __shfl_up(im, 1);
+  if (lane == 63) {
+    sh[w][0] = im;
+    sh[w][1] = is;
   }
-  (void)i0;
-  return n;
+  __syncthreads();
+  uint32_t pm = 0, ps = 0;
+  totm = 0;
+  tots = 0;
+#pragma unroll
+  for (int x = 0; x < kThreads / 64; ++x) {
+    if (x < w) {
+      pm = max(pm, sh[x][0]);
+      ps += sh[x][1];
+    }
+    totm = max(totm, sh[x][0]);
+    tots += sh[x][1];
+  }
+  exm = lane ? max(pm, up) : pm;
+  exs = ps + is - vs;
 }
 
-__device__ __forceinline__ uint64_t thread_last_prefix(const ChunkClass& k, uint64_t i0, uint64_t block_pre,
-                                                       uint64_t* sh) {
-  uint64_t last = 0;
+// A thread's 32 bytes classified and placed on their lines (parse_core.hpp).
+// The line-start prefix (the last '\n' before the chunk: in the threads
+// before it in the block, else the block's prefix pre_nl) says whether byte
+// 0 starts a line, or else whether its line is a header.  Bytes past the
+// block are dropped.
+struct Chunk {
+  parse::Masks m;
+  parse::Roles r;
+  uint32_t rel;  // block-relative index of byte 0
+};
+__device__ __forceinline__ Chunk chunk_roles(const BlockArgs& a, uint64_t b0, uint64_t b1, uint64_t fstart,
+                                             uint64_t pre_nl, uint32_t (*sh)[2]) {
+  Chunk c;
+  c.rel = threadIdx.x * kPerThread;
+  const uint64_t i0 = b0 + c.rel;
+  uint32_t w[8];
 #pragma unroll
-  for (int j = 0; j < kPerThread; ++j)
-    if (k.cls[j] != kCodeSkip) last = ((i0 + j + 1) << 2) | (k.cls[j] < 4 ? 0u : 1u);
-  auto lat = [](uint64_t x, uint64_t y) { return later(x, y); };
-  const uint64_t ex = block_exclusive<uint64_t>(last, 0, lat, sh, nullptr);
-  return later(block_pre, ex);
+  for (int h = 0; h < 2; ++h) {
+    const uint64_t at = i0 + 16 * h;
+    uint4 v = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+    if (at < b1) v = *(const uint4*)(a.raw + at);
+    w[4 * h] = v.x;
+    w[4 * h + 1] = v.y;
+    w[4 * h + 2] = v.z;
+    w[4 * h + 3] = v.w;
+  }
+  const uint32_t lim = b1 > i0 ? (uint32_t)min<uint64_t>(b1 - i0, kPerThread) : 0u;
+  c.m = parse::classify(w, lim);
+  const uint32_t nlv = c.m.nl ? c.rel + 32u - (uint32_t)parse::clz(c.m.nl) : 0u;  // (last '\n': relative index + 1)
+  uint32_t ex, exs, tm, ts;
+  block_scan(nlv, 0, sh, ex, exs, tm, ts);
+  const uint64_t nlp = ex ? b0 + ex : pre_nl;       // (absolute index + 1, 0: none)
+  const uint64_t ls = nlp > fstart ? nlp : fstart;  // the line start of byte 0 (<= i0)
+  const bool line0 = ls == i0;
+  const bool hdr0 = !line0 && ls < a.n && a.raw[ls] == '>';
+  c.r = parse::roles(c.m, line0, hdr0);
+  return c;
+}
+
+// the chunk's last kept byte as (block-relative index + 1) << 1 | is a
+// break, 0 = none (a later byte compares greater)
+__device__ __forceinline__ uint32_t last_kept(const Chunk& c) {
+  if (!c.r.keep) return 0;
+  const uint32_t j = 31u - (uint32_t)parse::clz(c.r.keep);
+  return ((c.rel + j + 1u) << 1) | ((c.r.brk >> j) & 1u);
+}
+__device__ __forceinline__ bool first_is_base(const Chunk& c) {
+  return c.r.keep && ((c.r.base >> parse::ctz(c.r.keep)) & 1u);
 }
 
 // pass 2: per block its bases, its run starts counted as if no base came
-// before it (runs0), whether its first non-dropped byte is a base (the host
-// then takes one start off when the block before ends in a base), and its
-// last non-dropped byte
+// before it (runs0), whether its first kept byte is a base (the host then
+// takes one start off when the block before ends in a base), and its last
+// kept byte
 __global__ __launch_bounds__(kThreads) void parse_count_kernel(BlockArgs a, const uint64_t* __restrict__ blk_end,
                                                               const uint64_t* __restrict__ pre_nl,
                                                               uint64_t* __restrict__ blk_bases,
                                                               uint64_t* __restrict__ blk_runs0,
                                                               uint64_t* __restrict__ blk_first,
                                                               uint64_t* __restrict__ blk_last) {
-  __shared__ int64_t shi[kThreads / 64];
-  __shared__ uint64_t shu[kThreads / 64];
+  __shared__ uint32_t sh1[kThreads / 64][2], sh2[kThreads / 64][2];
+  __shared__ uint32_t fix, first;
   const uint32_t b = blockIdx.x;
-  const uint64_t b1 = blk_end[b];
-  const uint64_t fstart = a.file_start[a.blk_file[b]];
-  uint32_t c[kPerThread];
-  uint64_t i0;
-  load_chunk(a, a.blk_start[b], b1, c, i0);
-  const uint64_t nlp = thread_nl_prefix(c, i0, b1, pre_nl[b], shi);
-  ChunkClass k;
-  classify(a, fstart, nlp, b1, c, i0, k);
-  // within the block: the last non-dropped byte before this thread's chunk
-  const uint64_t prev = thread_last_prefix(k, i0, 0, shu);
-  bool st[kPerThread];
-  uint64_t nr = run_starts(k, prev, 0, st, i0);  // (fstart 0: a byte before the chunk inside the block counts)
-  uint64_t bases = 0, last = 0, first = ~0ull;  // first: (index << 2 | kind) of the chunk's first non-dropped byte
-#pragma unroll
-  for (int j = kPerThread - 1; j >= 0; --j)
-    if (k.cls[j] != kCodeSkip) first = ((uint64_t)j << 2) | (k.cls[j] < 4 ? 0u : 1u);
-#pragma unroll
-  for (int j = 0; j < kPerThread; ++j) {
-    if (k.cls[j] < 4) ++bases;
-    if (k.cls[j] != kCodeSkip) last = ((i0 + j + 1) << 2) | (k.cls[j] < 4 ? 0u : 1u);
-  }
-  if (first != ~0ull) first += (uint64_t)threadIdx.x << 7;  // (block-relative index: thread * 32 + j)
-  uint64_t tb, tl, tr, tf;
-  auto add = [](uint64_t x, uint64_t y) { return x + y; };
-  (void)block_exclusive<uint64_t>(bases, 0, add, shu, &tb);
-  auto lat = [](uint64_t x, uint64_t y) { return later(x, y); };
-  (void)block_exclusive<uint64_t>(last, 0, lat, shu, &tl);
-  (void)block_exclusive<uint64_t>(nr, 0, add, shu, &tr);
-  auto mn = [](uint64_t x, uint64_t y) { return x < y ? x : y; };
-  (void)block_exclusive<uint64_t>(first, ~0ull, mn, shu, &tf);
+  const uint64_t b0 = a.blk_start[b], b1 = blk_end[b];
   if (threadIdx.x == 0) {
-    blk_bases[b] = tb;
-    blk_last[b] = tl;
-    blk_runs0[b] = tr;
-    blk_first[b] = tf != ~0ull && (tf & 3u) == 0;
+    fix = 0;
+    first = 0;
+  }
+  const Chunk c = chunk_roles(a, b0, b1, a.file_start[a.blk_file[b]], pre_nl[b], sh1);
+  // starts counted with no base before the chunk; the chunks that begin
+  // with a base after a base (earlier in the block) then count one too many
+  const uint32_t nb = (uint32_t)parse::popc(c.r.base);
+  const uint32_t nr = (uint32_t)parse::popc(parse::run_starts(c.r, false));
+  uint32_t prev, exs, tot_last, tot;
+  block_scan(last_kept(c), nb | (nr << 16), sh2, prev, exs, tot_last, tot);
+  const bool fb = first_is_base(c);
+  const uint64_t dm = __ballot(fb && prev && !(prev & 1u));
+  if ((threadIdx.x & 63) == 0 && dm) atomicAdd(&fix, (uint32_t)__popcll(dm));
+  if (fb && !prev) first = 1;  // (the chunk holding the block's first kept byte)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    blk_bases[b] = tot & 0xFFFFu;
+    blk_runs0[b] = (tot >> 16) - fix;
+    blk_first[b] = first;
+    blk_last[b] = tot_last ? ((b0 + (tot_last >> 1)) << 2) | (tot_last & 1u) : 0;
   }
 }
 
 // pass 3: 2-bit codes straight into the packed words (the block's words
-// assembled in LDS; the first and last, which a neighbouring block may
-// share, merged with atomicOr; words pre-cleared), and every run start
-// (packed position)
+// assembled in LDS, three atomicOr per thread at most; the first and last,
+// which a neighbouring block may share, merged into global with atomicOr;
+// words pre-cleared), and every run start (packed position)
 __global__ __launch_bounds__(kThreads) void parse_emit_kernel(BlockArgs a, const uint64_t* __restrict__ blk_end,
                                                              const uint64_t* __restrict__ pre_nl,
                                                              const uint64_t* __restrict__ pre_last,
@@ -260,41 +224,58 @@ __global__ __launch_bounds__(kThreads) void parse_emit_kernel(BlockArgs a, const
                                                              const uint64_t* __restrict__ run_off,
                                                              uint32_t* __restrict__ words,
                                                              uint64_t* __restrict__ starts) {
-  __shared__ int64_t shi[kThreads / 64];
-  __shared__ uint64_t shu[kThreads / 64];
+  __shared__ uint32_t sh1[kThreads / 64][2], sh2[kThreads / 64][2];
+  __shared__ uint32_t fixw[kThreads / 64];
   __shared__ uint32_t wl[kBlockBytes / 16 + 2];
   const uint32_t b = blockIdx.x;
-  const uint64_t b1 = blk_end[b];
+  const uint64_t b0 = a.blk_start[b], b1 = blk_end[b];
   const uint64_t fstart = a.file_start[a.blk_file[b]];
   for (uint32_t i = threadIdx.x; i < kBlockBytes / 16 + 2; i += kThreads) wl[i] = 0;
-  uint32_t c[kPerThread];
-  uint64_t i0;
-  load_chunk(a, a.blk_start[b], b1, c, i0);
-  const uint64_t nlp = thread_nl_prefix(c, i0, b1, pre_nl[b], shi);
-  ChunkClass k;
-  classify(a, fstart, nlp, b1, c, i0, k);
-  const uint64_t prev = thread_last_prefix(k, i0, pre_last[b], shu);
-  bool st[kPerThread];
-  const uint64_t nr = run_starts(k, prev, fstart, st, i0);
-  uint64_t nb = 0;
-#pragma unroll
-  for (int j = 0; j < kPerThread; ++j) nb += k.cls[j] < 4;
-  auto add = [](uint64_t x, uint64_t y) { return x + y; };
-  uint64_t total;
-  const uint64_t p0 = base_off[b];
-  const uint64_t w0 = p0 >> 4;
-  uint64_t pos = p0 + block_exclusive<uint64_t>(nb, 0, add, shu, &total);
-  uint64_t rr = run_off[b] + block_exclusive<uint64_t>(nr, 0, add, shu, nullptr);
-  __syncthreads();  // (wl cleared)
-#pragma unroll
-  for (int j = 0; j < kPerThread; ++j) {
-    if (k.cls[j] >= 4) continue;
-    if (st[j]) starts[rr++] = pos;
-    atomicOr(&wl[(uint32_t)((pos >> 4) - w0)], k.cls[j] << (30u - 2u * (uint32_t)(pos & 15u)));
-    ++pos;
+  const Chunk c = chunk_roles(a, b0, b1, fstart, pre_nl[b], sh1);
+  const uint32_t nb = (uint32_t)parse::popc(c.r.base);
+  const uint32_t starts0 = parse::run_starts(c.r, false);
+  uint32_t prev, exs, tot_last, tot;
+  block_scan(last_kept(c), nb | ((uint32_t)parse::popc(starts0) << 16), sh2, prev, exs, tot_last, tot);
+  // the last kept byte before the chunk: in the block, else before it (in
+  // the same file)
+  bool prev_base;
+  if (prev) {
+    prev_base = !(prev & 1u);
+  } else {
+    const uint64_t pl = pre_last[b];
+    prev_base = pl && ((pl >> 2) - 1) >= fstart && (pl & 3u) == 0;
+  }
+  const bool fix = prev_base && first_is_base(c);  // (one start fewer than starts0 counts)
+  const uint32_t st = fix ? starts0 & (starts0 - 1u) : starts0;
+  // the fixes before this chunk: ballots per wave, wave totals in LDS
+  const uint64_t fm = __ballot(fix);
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  if (lane == 0) fixw[wv] = (uint32_t)__popcll(fm);
+  __syncthreads();  // (also: wl cleared)
+  uint32_t fix_before = (uint32_t)__popcll(fm & ((1ull << lane) - 1ull));
+  for (uint32_t x = 0; x < wv; ++x) fix_before += fixw[x];
+  uint64_t pos = base_off[b] + (exs & 0xFFFFu);
+  uint64_t rr = run_off[b] + (exs >> 16) - fix_before;
+  const uint64_t w0 = base_off[b] >> 4;
+  // run starts (few per chunk)
+  for (uint32_t m = st; m;) {
+    const uint32_t j = (uint32_t)parse::ctz(m);
+    m &= m - 1u;
+    starts[rr++] = pos + (uint64_t)parse::popc(c.r.base & ((1u << j) - 1u));
+  }
+  if (nb) {
+    const uint64_t R = parse::packed_codes(c.m, c.r.base);
+    uint32_t x0, x1, x2;
+    parse::place(R, (uint32_t)(pos & 15u), x0, x1, x2);
+    const uint32_t k = (uint32_t)((pos >> 4) - w0);
+    atomicOr(&wl[k], x0);
+    if (x1) atomicOr(&wl[k + 1], x1);
+    if (x2) atomicOr(&wl[k + 2], x2);
   }
   __syncthreads();
+  const uint32_t total = tot & 0xFFFFu;
   if (total) {
+    const uint64_t p0 = base_off[b];
     const uint32_t nw = (uint32_t)(((p0 + total - 1) >> 4) - w0 + 1);
     for (uint32_t i = threadIdx.x; i < nw; i += kThreads) {
       if (i == 0 || i + 1 == nw) atomicOr(&words[w0 + i], wl[i]);
