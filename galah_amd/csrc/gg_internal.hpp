@@ -247,6 +247,7 @@ struct InflateSearch {
   uint32_t chunk_bits;         // bits searched per chunk
   uint32_t n_chunks;
   uint64_t* start;             // [n_chunks] first block header found (~0: none)
+  uint64_t* prof = nullptr;    // (GALAHGPU_INFLATE_DEBUG) cycles scanning, cycles checking, steps, check rounds, candidates checked
 };
 struct InflateDecode {
   const uint32_t* in;

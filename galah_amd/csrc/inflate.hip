@@ -121,6 +121,17 @@ __global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(Infla
   const Bits in{stream};
   uint64_t found = ~0ull;
   uint32_t nc = 0;  // candidates listed, not yet checked (uniform)
+  uint64_t tp = a.prof ? clock64() : 0;
+  auto phase = [&](int k) {  // (GALAHGPU_INFLATE_DEBUG: cycles per phase)
+    if (a.prof) {
+      const uint64_t t = clock64();
+      if (lane == 0) {
+        atomicAdd((unsigned long long*)&a.prof[k], (unsigned long long)(t - tp));
+        atomicAdd((unsigned long long*)&a.prof[k + 2], 1ull);
+      }
+      tp = t;
+    }
+  };
   for (uint64_t s0 = b0; found == ~0ull;) {  // (uniform per wave)
     if (s0 < b1) {
       const uint64_t s1 = min(s0 + kSearchStep, b1);
@@ -163,9 +174,11 @@ __global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(Infla
         nc += total;
         s0 = s1;
       }
+      phase(0);
       if (nc < kCheckAt && s0 < b1) continue;  // (check in groups: a start found early ends the scan)
     }
     // the full checks of the listed candidates, in order
+    if (a.prof && lane == 0) atomicAdd((unsigned long long*)&a.prof[4], (unsigned long long)nc);
     for (uint32_t k0 = 0; k0 < nc; k0 += 64) {
       bool ok = false;
       if (k0 + lane < nc) {
@@ -179,6 +192,7 @@ __global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(Infla
       }
     }
     __builtin_amdgcn_wave_barrier();
+    phase(1);
     nc = 0;
     if (s0 >= b1) break;
   }

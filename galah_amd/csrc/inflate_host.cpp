@@ -126,7 +126,21 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     s.chunk_bits = kChunkBytes * 8;
     s.n_chunks = nc;
     s.start = d_start;
+    uint64_t* d_sprof = nullptr;
+    if (inflate_debug()) {
+      GG_HIP(m, scratch_t(m, "gz_sprof", 8, &d_sprof));
+      GG_HIP(m, hipMemsetAsync(d_sprof, 0, 8 * sizeof(uint64_t), st));
+      s.prof = d_sprof;
+    }
     GG_HIP(m, launch_inflate_search(s, st));
+    if (d_sprof) {
+      uint64_t pr[8];
+      GG_HIP(m, hipStreamSynchronize(st));
+      GG_HIP(m, hipMemcpy(pr, d_sprof, sizeof pr, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[inflate] search: %u chunks; per chunk: %.1f steps (%.0f cycles each), %.1f check rounds "
+              "(%.0f cycles each), %.1f candidates\n", nc, pr[2] / (double)nc, pr[0] / (double)std::max<uint64_t>(pr[2], 1),
+              pr[3] / (double)nc, pr[1] / (double)std::max<uint64_t>(pr[3], 1), pr[4] / (double)nc);
+    }
     GG_HIP(m, hipMemcpyAsync(start.data(), d_start, nc * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   }
   GG_HIP(m, hipStreamSynchronize(st));
