@@ -179,17 +179,37 @@ __global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(Infla
     }
     // the full checks of the listed candidates, in order
     if (a.prof && lane == 0) atomicAdd((unsigned long long*)&a.prof[4], (unsigned long long)nc);
-    for (uint32_t k0 = 0; k0 < nc; k0 += 64) {
-      bool ok = false;
-      if (k0 + lane < nc) {
-        uint64_t q = cw[k0 + lane];
-        ok = block_header_ok(in, q, cl);
+    // (each lane walks one candidate a symbol per step and takes the next
+    // unclaimed one when its own is decided; done when a candidate passed
+    // and none before it is still walking, or all are decided)
+    {
+      HeaderWalk hw;
+      int mine = -1;          // the candidate this lane walks
+      uint32_t next = 0;      // candidates claimed (uniform)
+      uint32_t best = nc;     // the first that passed (uniform)
+      for (;;) {
+        const bool need = mine < 0;
+        const uint64_t nm = __ballot(need);
+        const uint32_t lim = min(nc, best);
+        if (need) {
+          const uint32_t k = next + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
+          if (k < lim) mine = hw.start(in, cw[k], cl) ? (int)k : -1;  // (rejected at once: the lane claims again)
+        }
+        next = min(lim, next + (uint32_t)__popcll(nm));
+        int r = 0;
+        if (mine >= 0) r = hw.step(in, cl);
+        const uint64_t pm = __ballot(r == 1);
+        if (pm) {
+          uint32_t b = r == 1 ? (uint32_t)mine : ~0u;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) b = min(b, (uint32_t)__shfl_xor(b, o));
+          best = min(best, b);
+        }
+        if (r != 0) mine = -1;
+        const bool pending = mine >= 0 && (uint32_t)mine < best;
+        if (!__ballot(pending) && next >= min(nc, best)) break;
       }
-      const uint64_t bm = __ballot(ok);
-      if (bm) {
-        found = cw[k0 + (uint32_t)__ffsll((unsigned long long)bm) - 1u];
-        break;
-      }
+      if (best < nc) found = cw[best];
     }
     __builtin_amdgcn_wave_barrier();
     phase(1);

@@ -403,6 +403,89 @@ GG_HD bool block_header_ok(const B& in, uint64_t& pos, ClS& st) {
   return true;
 }
 
+// block_header_ok as a walk of one code-length symbol per step, so that the
+// lanes of a wave can each walk a different candidate and take the next one
+// as soon as theirs is decided (the search's checks; a wave-wide round of
+// block_header_ok lasts as long as its longest walk).  start() reads the
+// fields and the code-length code (false: rejected already); step() returns
+// 0 (more), 1 (a valid header) or -1 (rejected).  A repeat code's lengths
+// are added at once: the Kraft sums only grow, so the verdict is
+// block_header_ok's.
+struct HeaderWalk {
+  uint64_t pos;
+  ClCode cl;
+  uint32_t i, n, hlit, prev;
+  uint32_t kl, kd, nd, ml, md;
+  bool eob;
+
+  template <class ClS, class B>
+  GG_HD bool start(const B& in, uint64_t p, ClS& st) {
+    if (!block_header_quick(in, p)) return false;
+    const uint32_t h = in.peek(p);
+    hlit = ((h >> 3) & 31u) + 257u;
+    n = hlit + ((h >> 8) & 31u) + 1u;
+    pos = p + 17;
+    if (!read_cl_code(in, pos, ((h >> 13) & 15u) + 4u, cl, st)) return false;
+    i = prev = kl = kd = nd = ml = md = 0;
+    eob = false;
+    return true;
+  }
+  GG_HD void add(uint32_t len, uint32_t rep) {  // lengths i .. i + rep - 1 = len (> 0)
+    const uint32_t rl = i < hlit ? (rep < hlit - i ? rep : hlit - i) : 0u, rd = rep - rl;
+    if (rl) {
+      kl += rl << (kMaxBits - len);
+      ml = len > ml ? len : ml;
+      eob |= i <= 256u && 256u < i + rl;
+    }
+    if (rd) {
+      kd += rd << (kMaxBits - len);
+      nd += rd;
+      md = len > md ? len : md;
+    }
+  }
+  template <class ClS, class B>
+  GG_HD int step(const B& in, ClS& st) {
+    const uint32_t x = in.peek(pos);
+    const uint32_t y = rev15(x) >> (kMaxBits - kClBits);  // left-justified 7 bits
+    if (y >= cl.limit[kClBits]) return -1;
+    uint32_t L = 1;
+#pragma unroll
+    for (int l = 1; l < kClBits; ++l) L += y >= cl.limit[l] ? 1u : 0u;
+    const int s = st.sym(st.base((int)L) + (int)(y >> (kClBits - L)));
+    pos += L;
+    if (s < 16) {
+      if (s) add((uint32_t)s, 1);
+      prev = (uint32_t)s;
+      ++i;
+    } else {
+      const uint32_t e = x >> L;  // (the repeat's extra bits follow the code)
+      uint32_t rep, val = 0;
+      if (s == 16) {
+        if (i == 0) return -1;
+        rep = 3 + (e & 3u);
+        pos += 2;
+        val = prev;
+      } else if (s == 17) {
+        rep = 3 + (e & 7u);
+        pos += 3;
+      } else {
+        rep = 11 + (e & 127u);
+        pos += 7;
+      }
+      if (i + rep > n) return -1;
+      if (val) add(val, rep);
+      i += rep;
+      if (s != 16) prev = 0;
+    }
+    if (kl > (1u << kMaxBits) || kd > (1u << kMaxBits)) return -1;
+    if (i < n) return 0;
+    if (!eob) return -1;
+    if (kl != (1u << kMaxBits) && ml != 1) return -1;
+    if (nd && kd != (1u << kMaxBits) && md != 1) return -1;
+    return 1;
+  }
+};
+
 // One lane's tables for its current block.  The limits are indexed by
 // constants only (code_len unrolled: registers on the device); the bases,
 // the symbols sorted by (length, value) and the per-length counts a header

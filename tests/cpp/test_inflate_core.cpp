@@ -285,6 +285,14 @@ int main(int argc, char** argv) {
           fprintf(stderr, "%s: header check through SeqBits differs at bit %llu\n", argv[a], (unsigned long long)p);
           ++failures;
         }
+        // the search's stepwise walk (HeaderWalk) gives the same verdict
+        HeaderWalk hw;
+        int v = hw.start(in, p, cla) ? 0 : -1;
+        while (v == 0) v = hw.step(in, cla);
+        if ((v == 1) != ok1) {
+          fprintf(stderr, "%s: HeaderWalk differs from block_header_ok at bit %llu\n", argv[a], (unsigned long long)p);
+          ++failures;
+        }
         if (ok1) {
           starts.push_back(p);
           break;
