@@ -276,11 +276,13 @@ struct InflatePlace {
   const uint32_t* lane_file;
   const uint64_t* lane_out;    // [n_lanes] text position of the lane's first byte
   const uint64_t* lane_pad;    // [n_lanes] its file's last lane: end of the '\n' padding after it (else 0)
+  const uint64_t* lane_len;    // [n_lanes] the bytes the decode counted for it (its tokens must make as many)
   const uint64_t* file_text;   // [n_files] text position of the file's first byte
   uint32_t n_lanes;
   uint8_t* text;               // [text_len] the bytes, kTextPtr where the byte is still a pointer
   uint32_t* val;               // [text_len] literal (0x80000000 | byte) or the position copied
-  uint32_t* flags;             // bit 0: a distance before its file's start, bit 1: a runaway chain
+  uint32_t* flags;             // bit 0: a distance before its file's start, bit 1: a runaway chain or a
+                               // pointer out of range, bit 2: a lane's tokens make other than lane_len bytes
 };
 constexpr uint8_t kTextPtr = 0xFF;  // (a literal 0xFF byte is also read through val: still exact)
 // one file of an inflate batch (inflate_host.cpp): its bytes at

@@ -652,6 +652,8 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
   const uint64_t n = a.n_tok[seg];
   const uint64_t o0 = a.lane_out[seg];                 // the segment's first text position
   const uint64_t f0 = a.file_text[a.lane_file[seg]];  // its file's
+  const uint64_t lim = o0 + a.lane_len[seg];           // (a corrupt stream's tokens may make more or fewer bytes
+                                                       //  than the decode counted: nothing is written past lim)
   uint64_t base = o0;
   bool bad = false;
   uint32_t tk_next = tid < n ? tok[tid] : 0u;  // (the next step's token, loaded a step ahead)
@@ -725,7 +727,8 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
       }
       if (!__syncthreads_or(more)) break;
     }
-    for (uint32_t i = tid; i < nb; i += kExpandThreads) {
+    const uint32_t nw = base + nb <= lim ? nb : base < lim ? (uint32_t)(lim - base) : 0u;
+    for (uint32_t i = tid; i < nw; i += kExpandThreads) {
       const uint32_t x = v[i];
       a.val[base + i] = x;
       a.text[base + i] = x >> 31 ? (uint8_t)x : kTextPtr;  // (kTextPtr: the resolve pass follows val there)
@@ -737,8 +740,9 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
     t0 += nt;
   }
   // a file's last segment: the padding up to the next file ('\n' parses as nothing)
-  for (uint64_t i = base + tid; i < a.lane_pad[seg]; i += kExpandThreads) a.text[i] = '\n';
+  for (uint64_t i = lim + tid; i < a.lane_pad[seg]; i += kExpandThreads) a.text[i] = '\n';
   if (bad) atomicOr(a.flags, 1u);
+  if (base != lim && tid == 0) atomicOr(a.flags, 4u);
 }
 
 // Pointers (into earlier segments) followed to their literals, 16 text
@@ -786,7 +790,14 @@ __global__ __launch_bounds__(256) void inflate_resolve_kernel(const uint32_t* __
       }
 #pragma unroll
       for (int b = 0; b < 16; ++b)
-        if (!(x[b] >> 31)) x[b] = val[x[b]];
+        if (!(x[b] >> 31)) {
+          if (x[b] < n) {
+            x[b] = val[x[b]];
+          } else {  // (only in a batch the expand flagged: the host decodes it)
+            atomicOr(flags, 2u);
+            x[b] = 0x80000000u | '\n';
+          }
+        }
     }
     uint32_t out[4] = {0, 0, 0, 0};
 #pragma unroll

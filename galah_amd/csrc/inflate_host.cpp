@@ -319,8 +319,8 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   // padding after it (its file's last lane: the next file's start; else 0)
   // (u64), then its file (u32)
   const size_t NL = std::max<size_t>(live.size(), 1);
-  GG_HIP(m, scratch_t(m, "gz_lout", 4 * NL + (NL + 1) / 2, &d_lout));
-  d_lfile = (uint32_t*)(d_lout + 4 * NL);
+  GG_HIP(m, scratch_t(m, "gz_lout", 5 * NL + (NL + 1) / 2, &d_lout));
+  d_lfile = (uint32_t*)(d_lout + 5 * NL);
   GG_HIP(m, scratch_t(m, "gz_ftext", 2 * (size_t)nf + 1, &d_ftext));
   d_flen = d_ftext + nf;
   GG_HIP(m, scratch_t(m, "gz_flags", 2 * (size_t)nf + 1, &d_flags));
@@ -335,13 +335,14 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     ftext[nf + f] = flen[f];
   }
   GG_HIP(m, hipMemcpyAsync(d_ftext, ftext.data(), ftext.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-  std::vector<uint64_t> lv(4 * NL + (NL + 1) / 2, 0);
+  std::vector<uint64_t> lv(5 * NL + (NL + 1) / 2, 0);
   for (size_t l = 0; l < live.size(); ++l) {
     lv[l] = lane_out[l];
     lv[NL + l] = live[l].tok_off;
     lv[2 * NL + l] = live[l].n_tok;
     if (l + 1 == live.size() || live[l + 1].file != live[l].file) lv[3 * NL + l] = foff[live[l].file + 1];
-    ((uint32_t*)(lv.data() + 4 * NL))[l] = live[l].file;
+    lv[4 * NL + l] = live[l].out_len;
+    ((uint32_t*)(lv.data() + 5 * NL))[l] = live[l].file;
   }
   GG_HIP(m, hipMemcpyAsync(d_lout, lv.data(), lv.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   InflatePlace p;
@@ -349,6 +350,7 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   p.tok_off = d_lout + NL;
   p.n_tok = d_lout + 2 * NL;
   p.lane_pad = d_lout + 3 * NL;
+  p.lane_len = d_lout + 4 * NL;
   p.lane_file = d_lfile;
   p.lane_out = d_lout;
   p.file_text = d_ftext;
@@ -375,7 +377,10 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   GG_HIP(m, hipStreamSynchronize(st));
   stamp("expand + resolve + crc");
   if (chk[0])
-    return hand_back(chk[0] & 1 ? "distance before the file start" : "pointer chain", 0);
+    return hand_back(chk[0] & 1   ? "distance before the file start"
+                     : chk[0] & 4 ? "token bytes disagree with the decode's count"
+                                  : "pointer chain",
+                     0);
   for (uint32_t f = 0; f < nf; ++f)
     if (files[f].gz && (chk[1 + f] != files[f].crc || chk[1 + nf + f] != '>'))  // (FASTQ, malformed: the host path)
       return hand_back(chk[1 + f] != files[f].crc ? "CRC-32" : "not FASTA", f);
