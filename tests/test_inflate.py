@@ -160,6 +160,33 @@ def test_device_inflate_corrupt_and_empty_fail_as_host(tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_device_inflate_corrupt_streams_fail_as_host(tmp_path, monkeypatch):
+    """Bytes flipped at several places of a multi-block stream: whatever the
+    lanes decode (garbage that may still add up to ISIZE), the device path
+    hands the batch to the host and reports the host's error -- no device
+    fault, no other error."""
+    rng = np.random.default_rng(5)
+    seq = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 600000)].tobytes()
+    good = gzip.compress(b">c\n" + b"\n".join(seq[i:i + 80] for i in range(0, len(seq), 80)) + b"\n", 6)
+    for frac in (0.2, 0.35, 0.5, 0.65, 0.8):
+        for pat in (0x55, 0x01, 0xFF):
+            bad = bytearray(good)
+            bad[int(len(bad) * frac)] ^= pat
+            p = tmp_path / ("c%d_%d.fa.gz" % (int(frac * 100), pat))
+            p.write_bytes(bytes(bad))
+            errs = {}
+            for mode in ("host", "device"):
+                monkeypatch.setenv("GALAHGPU_INFLATE", mode)
+                with ga.Context(k=21, sketch_size=1000) as ctx:
+                    try:
+                        ctx.sketch_files([str(p)])
+                        errs[mode] = None
+                    except ga.GalahGpuError as e:
+                        errs[mode] = (e.status, str(e))
+            assert errs["device"] == errs["host"], p.name
+
+
+@pytest.mark.gpu
 def test_device_inflate_is_the_default_and_knobs_change_nothing(golden, monkeypatch):
     """A .gz list takes the device path with no knob set (the info line
     counts no host-inflated batch); mapped vs read files, small batches and
