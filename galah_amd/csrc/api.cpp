@@ -39,15 +39,28 @@ gg_status hip_fail(gg_ctx* c, hipError_t e, const char* what) {
 hipError_t scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
   auto& e = c->scratch[key];
   if (e.second < bytes) {
+    // a buffer that grows again grows by a quarter at least: batches of
+    // slightly different sizes (the device-inflate batches are cut at a file
+    // boundary) would otherwise reallocate it call after call, and hipFree
+    // waits for every stream of the device
+    const size_t grown = e.second ? e.second + e.second / 4 : 0;
     if (e.first) {
       hipError_t err = hipFree(e.first);
       if (err != hipSuccess) return err;
       e.first = nullptr;
       e.second = 0;
     }
-    size_t want = std::max<size_t>(bytes, 256);
+    size_t want = std::max<size_t>(std::max(bytes, grown), 256);
     hipError_t err = hipMalloc(&e.first, want);
-    if (err != hipSuccess) return err;
+    if (err == hipErrorOutOfMemory && want > bytes) {  // (no room for the headroom: just what is asked)
+      (void)hipGetLastError();
+      want = std::max<size_t>(bytes, 256);
+      err = hipMalloc(&e.first, want);
+    }
+    if (err != hipSuccess) {
+      e.first = nullptr;
+      return err;
+    }
     e.second = want;
   }
   *out = e.first;
@@ -1103,6 +1116,26 @@ std::vector<uint32_t> build_cmin(uint32_t s, int k, float min_ani) {
   return cmin;
 }
 
+gg_ctx* lane_ctx(gg_ctx* m, size_t i) {
+  if (m->lanes.size() <= i) m->lanes.resize(i + 1, nullptr);
+  gg_ctx*& l = m->lanes[i];
+  if (l) return l;
+  gg_ctx* x = new (std::nothrow) gg_ctx();
+  if (!x) return nullptr;
+  x->k = m->k;
+  x->s = m->s;
+  x->seed = m->seed;
+  x->device = m->device;
+  x->pairs_kernel = m->pairs_kernel;
+  x->host_threads = m->host_threads;
+  if (hipSetDevice(m->device) != hipSuccess || hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete x;
+    return nullptr;
+  }
+  l = x;
+  return l;
+}
+
 }  // namespace gg
 
 using namespace gg;
@@ -1191,6 +1224,7 @@ void gg_destroy(gg_ctx* ctx) {
   if (!ctx) return;
   ctx->pool.reset();  // (member threads idle between calls: joined here)
   for (gg_ctx* m : ctx->devs) gg_destroy(m);
+  for (gg_ctx* l : ctx->lanes) gg_destroy(l);
   for (auto& kv : ctx->host_scratch)
     if (kv.second.first) (void)hipHostFree(kv.second.first);
   ctx->host_scratch.clear();
@@ -1386,15 +1420,17 @@ gg_status gg_info_line(const gg_ctx* ctx, char* buf, size_t cap) {
   const size_t M = ctx->devs.empty() ? 1 : ctx->devs.size();
   uint64_t staged_links = 0;
   for (size_t x = 0; x < ctx->peer_direct.size(); ++x) staged_links += ctx->peer_direct[x] ? 0 : 1;
-  char line[512];
+  uint64_t dev_batches = ctx->inflate_dev_batches;
+  for (const gg_ctx* m : ctx->devs) dev_batches += m->inflate_dev_batches;
+  char line[600];
   snprintf(line, sizeof line,
            "galahgpu: %zu device(s) [%s]; sketch %.1f ms, replicate %.2f ms, pairs %.2f ms, merge %.2f ms; "
            "fallbacks: index->gate %llu, index full sort %llu, host-staged peer copies %llu (links without peer "
-           "access %llu), sketch retry passes %llu, host-inflated batches %llu",
+           "access %llu), sketch retry passes %llu, host-inflated batches %llu (device-inflated %llu)",
            M, ords.c_str(), ctx->phase_ms[GG_PHASE_SKETCH], ctx->phase_ms[GG_PHASE_REPLICATE],
            ctx->phase_ms[GG_PHASE_PAIRS], ctx->phase_ms[GG_PHASE_MERGE], (unsigned long long)fb[0],
            (unsigned long long)fb[1], (unsigned long long)fb[2], (unsigned long long)staged_links,
-           (unsigned long long)fb[3], (unsigned long long)fb[4]);
+           (unsigned long long)fb[3], (unsigned long long)fb[4], (unsigned long long)dev_batches);
   const size_t n = std::min(cap - 1, strlen(line));
   memcpy(buf, line, n);
   buf[n] = 0;

@@ -97,7 +97,7 @@ struct gg_ctx {
   // grow-only pinned host staging buffer (streamed ingest)
   void* pinned = nullptr;
   size_t pinned_bytes = 0;
-  // device-inflate staging slots (multi.cpp GzPipe): batch N is inflated
+  // device-inflate staging slots (ingest_gz.cpp GzStager): batch N is inflated
   // from one while N + 1 is staged into the other by a helper thread, which
   // touches only its slot (grow-only pinned and device buffers, its stream)
   struct GzSlot {
@@ -129,6 +129,11 @@ struct gg_ctx {
   std::vector<hipEvent_t> spare_events;
   // multi-device context: the members (owned) and their host threads
   std::vector<gg_ctx*> devs;
+  // helper contexts of this device (owned; created on first use, kept for
+  // the context's life): the device-inflate ingest runs several batches at
+  // once, each processing lane on its own stream with its own scratch
+  // (ingest_gz.cpp); lanes[0] is unused (lane 0 is this context)
+  std::vector<gg_ctx*> lanes;
   std::unique_ptr<MemberPool> pool;
   // a member's copy streams, one per peer it gathers rows from (created on
   // first use), so the copies from different peers run at once
@@ -136,6 +141,7 @@ struct gg_ctx {
   uint64_t pair_paths[GG_PATH_COUNT] = {};  // gg_pair_paths
   // gg_fallbacks (the two index entries are read from pair_paths)
   uint64_t fallbacks[GG_FALLBACK_COUNT] = {};
+  uint64_t inflate_dev_batches = 0;  // gzip batches inflated on the device (gg_info_line)
   // multi-device context: [a * M + b] = 1 when member a reaches member b's
   // memory directly (same device, or peer access enabled), gg_peer_links
   std::vector<uint8_t> peer_direct;
@@ -218,6 +224,55 @@ gg_status pairs_range_to_host(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d
 constexpr uint64_t kInflatePad = 4096;  // device bytes past a batch's last file (readers run past its end)
 gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const std::vector<InflateFile>& files,
                         uint8_t** d_text, std::vector<uint64_t>& foff, bool* ok, uint8_t* d_in = nullptr);
+
+// One batch of FASTA text already in device memory (d_text, file f at
+// foff[f]) parsed on the device: 2-bit words into *d_words (scratch of m),
+// runs of >= k bases (genome = file index in the batch) into runs.
+// Synchronises m->stream.  (multi.cpp)
+gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<uint64_t>& foff, uint32_t** d_words,
+                          uint64_t* n_words, std::vector<gg_run>& runs);
+
+// Helper context i >= 1 of single-device context m: the same device, k, s
+// and seed, its own stream and scratch (api.cpp; owned by m).
+gg_ctx* lane_ctx(gg_ctx* m, size_t i);
+
+// The file list of one device-inflate ingest call, shared by every member
+// and lane (ingest_gz.cpp).  Files are claimed one at a time, so each batch
+// is cut at its size limits whatever the number of stagers; a claimed file
+// that does not fit its batch is given back and claimed again first.
+struct GzClaims {
+  const char* const* paths = nullptr;  // the files to sketch (not found in the cache)
+  const uint32_t* row_of = nullptr;    // their rows in the call's sketch array
+  uint32_t n = 0;
+  const char* cache_dir = nullptr;     // new sketches stored there (files stamped before they are read)
+  std::mutex mu;
+  uint32_t cursor = 0;
+  std::vector<uint32_t> back;  // claimed, given back
+  uint32_t batches = 0;        // batches begun (the first ones are cut smaller)
+  bool stop = false;           // no more claims: a failure
+  // the failing file with the lowest index (a file that did not read, or
+  // did not decode or parse on the host): the call's error, as a serial
+  // reader meets it
+  uint32_t err_idx = UINT32_MAX;
+  gg_status err_st = GG_OK;
+  std::string err_msg;
+  bool claim(uint32_t* i);
+  void give_back(uint32_t i);
+  void file_error(uint32_t i, gg_status st, const std::string& msg);
+  void halt();
+};
+// Member m's share of the list: inflated, parsed and sketched on m's device
+// by several lanes at once, rows into d_sk / d_len (m's [n x s] arrays);
+// the rows sketched are appended to owned.  host_threads: the host threads
+// this member may use (staging reads, host decodes).
+gg_status gz_member_ingest(gg_ctx* m, GzClaims& cl, uint64_t* d_sk, uint32_t* d_len, int host_threads,
+                           std::vector<uint32_t>& owned);
+// After a file error: files given back (never read) below the failing index
+// are read on the host, so the lowest failing index is reported.
+void gz_settle_errors(GzClaims& cl);
+// Whether a file list takes the device inflate: GALAHGPU_INFLATE=device /
+// host, else when one of its first files is gzip (by its magic bytes).
+bool gz_device_list(const char* const* paths, uint32_t n);
 
 template <typename T>
 T* copy_out(const std::vector<T>& v) {

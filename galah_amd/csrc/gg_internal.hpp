@@ -295,9 +295,13 @@ struct InflateFile {
   bool gz = false;
 };
 bool gzip_member(const uint8_t* buf, size_t n, size_t* data_off, size_t* data_len, uint32_t* isize, uint32_t* crc);
+// The gzip header at the start of buf[0, n) (of a file of file_size bytes):
+// its length (*data_off); false when it is not gzip (CM 8), has reserved
+// flags, or does not end within buf and before the trailer.
+bool gzip_header(const uint8_t* buf, size_t n, uint64_t file_size, size_t* data_off);
 hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st);
 hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st);
-// expand + resolve (text[0, text_len), val pre-set to literal '\n') + CRC-32 per file
+// expand + resolve (text[0, text_len); val is read only where the expand wrote it) + CRC-32 per file
 // (file f's 4 KB segments are seg_first[f] .. seg_first[f + 1] - 1; crc
 // receives n_files CRCs, then each file's first byte)
 constexpr uint32_t kInflateCrcSeg = 4096;
@@ -422,13 +426,12 @@ bool file_stamp(const char* path, FileStamp* out);
 int ingest_threads(int n_threads);
 class PackStream {
  public:
-  // raw: the workers only read (and gunzip) each file and keep its FASTA
-  // text for the device parser (parse.hip); FASTQ files are rewritten as
-  // FASTA records on the way.  Otherwise they pack on the host.
-  // keep_gzip (raw streams): gzip files are kept as read, compressed, for
-  // the device inflate (inflate_host.cpp); get_raw reports them with *gz.
+  // raw: the workers only read (and decompress) each file and keep its
+  // FASTA text for the device parser (parse.hip); FASTQ files are rewritten
+  // as FASTA records on the way.  Otherwise they pack on the host.  (Gzip
+  // lists for the device inflate are read by ingest_gz.cpp's stagers.)
   PackStream(const char* const* paths, uint32_t n, int k, int n_threads, uint64_t budget_bytes,
-             bool stamp_files = false, bool raw = false, bool keep_gzip = false);
+             bool stamp_files = false, bool raw = false);
   ~PackStream();
   PackStream(const PackStream&) = delete;
   PackStream& operator=(const PackStream&) = delete;
@@ -437,10 +440,7 @@ class PackStream {
   gg_status get(uint32_t i, const std::vector<uint32_t>** words, const std::vector<gg_run>** runs,
                 std::string* err);
   // raw streams: genome i's FASTA text.  Valid until release(i).
-  gg_status get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err, bool* gz = nullptr);
-  // raw streams: genome i's bytes (keep_gzip: a gzip file may be mapped
-  // rather than read; get_raw then gives an empty text).  Valid until release(i).
-  gg_status get_bytes(uint32_t i, const uint8_t** data, size_t* len, std::string* err, bool* gz);
+  gg_status get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err);
   // The file's size and mtime as stat'ed just before it was read (valid
   // after get(i) succeeded; the streams are built with stamp_files).
   FileStamp stamp(uint32_t i);
@@ -456,10 +456,11 @@ class PackStream {
   std::unique_ptr<Impl> p_;
 };
 
-// The FASTA text of a gzip file's bytes as the raw streams give it (host
-// gunzip, FASTQ records rewritten): the host fallback of the device inflate.
-gg_status host_text_from_gzip(const std::vector<uint8_t>& gz, const char* name, std::vector<uint8_t>& text,
-                              std::string& err);
+// The FASTA text of a file's bytes as the raw streams give it (gzip, bzip2
+// or xz decoded on the host by their magic, FASTQ records rewritten): the
+// host fallback of the device inflate.  bytes may be consumed.
+gg_status host_text_from_bytes(std::vector<uint8_t>& bytes, const char* name, std::vector<uint8_t>& text,
+                               std::string& err);
 
 // api.cpp helpers used by pack.cpp
 void set_thread_error(const std::string& msg);

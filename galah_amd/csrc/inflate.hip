@@ -220,6 +220,8 @@ __global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(Infla
 }
 
 struct LdsStore {
+  uint32_t* ll;
+  uint32_t* dl;
   int32_t* lb;
   int32_t* db;
   uint32_t* lc;
@@ -230,6 +232,8 @@ struct LdsStore {
   uint32_t* df;
   __device__ uint32_t& lfast(int i) { return lf[i]; }
   __device__ uint32_t& dfast(int i) { return df[i]; }
+  __device__ uint32_t& llim(int l) { return ll[l]; }
+  __device__ uint32_t& dlim(int l) { return dl[l]; }
   __device__ int32_t& lbase(int l) { return lb[l]; }
   __device__ int32_t& dbase(int l) { return db[l]; }
   __device__ uint32_t& lcnt(int l) { return lc[l]; }
@@ -268,7 +272,7 @@ struct TokSink {
 // A block's header read by the whole wave.  Lane 0 parses the fields and
 // walks the code lengths (SeqBits) into LDS (lens); then every lane counts
 // them per length by ballots, builds the canonical limits in its registers
-// (tab.llim / dlim) and the bases, and the symbols sorted by (length, value)
+// (tab.s.llim / dlim) and the bases, and the symbols sorted by (length, value)
 // are placed in the LDS tables by ballot ranks.  Returns btype (0 stored,
 // 1 fixed, 2 dynamic) or -1 for a header zlib refuses (inflate_core.hpp
 // read_block_header, the same checks).
@@ -401,7 +405,11 @@ __device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restri
 // of its checkpoints agrees with the first decode.  The right spans up to
 // the one that decoded end-of-block are the block; their tokens are copied
 // to the segment's tokens.
-__global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecode a) {
+#ifndef GG_DECODE_MIN_WAVES
+#define GG_DECODE_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decode_kernel(InflateDecode a) {
+  __shared__ uint32_t llm[kMaxBits + 1], dlm[kMaxBits + 1];
   __shared__ int32_t lb[kMaxBits + 1], db[kMaxBits + 1];
   __shared__ uint32_t lcn[kMaxBits + 1], dcn[kMaxBits + 1];
   __shared__ ClLds hcl;  // (lane 0's, while it reads a header)
@@ -415,7 +423,7 @@ __global__ __launch_bounds__(kSpanLanes) void inflate_decode_kernel(InflateDecod
   const uint32_t seg = blockIdx.x;
   if (seg >= a.n_lanes) return;
   LaneTables<LdsStore> tab;
-  tab.s = LdsStore{lb, db, lcn, dcn, ls, ds, lf, df};
+  tab.s = LdsStore{llm, dlm, lb, db, lcn, dcn, ls, ds, lf, df};
   const uint32_t f = a.lane_file[seg];
   const Bits in{a.in + a.file_word[f]};
   const uint64_t limit = a.file_bits[f];
@@ -765,19 +773,29 @@ __global__ __launch_bounds__(256) void inflate_resolve_kernel(const uint32_t* __
       for (int k = 0; k < 4; ++k) any |= ((w[k] - 0x01010101u) & ~w[k] & 0x80808080u) != 0;
       if (!any) continue;
     }
+    // only the kTextPtr bytes are read through val: the other bytes are
+    // final as the expand wrote them, and val holds nothing at a file's
+    // padding (the '\n' up to the next file), which is never written
     uint32_t x[16];
     if (whole) {
+      const uint4 t = *(const uint4*)(text + g * 16);
+      const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint4 w = *(const uint4*)(val + g * 16 + 4 * q);
-        x[4 * q] = w.x;
-        x[4 * q + 1] = w.y;
-        x[4 * q + 2] = w.z;
-        x[4 * q + 3] = w.w;
+        const uint32_t v[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t byte = (tw[q] >> (8 * k)) & 0xFFu;
+          x[4 * q + k] = byte == kTextPtr ? v[k] : 0x80000000u | byte;
+        }
       }
     } else {
 #pragma unroll
-      for (int b = 0; b < 16; ++b) x[b] = g * 16 + b < n ? val[g * 16 + b] : 0x80000000u | '\n';
+      for (int b = 0; b < 16; ++b) {
+        const uint64_t i = g * 16 + b;
+        x[b] = i < n && text[i] == kTextPtr ? val[i] : 0x80000000u | (i < n ? text[i] : (uint32_t)'\n');
+      }
     }
     for (uint32_t hop = 0;; ++hop) {
       bool any = false;

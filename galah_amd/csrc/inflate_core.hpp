@@ -486,13 +486,12 @@ struct HeaderWalk {
   }
 };
 
-// One lane's tables for its current block.  The limits are indexed by
-// constants only (code_len unrolled: registers on the device); the bases,
-// the symbols sorted by (length, value) and the per-length counts a header
-// read keeps are indexed by data, so they live in the Store (host: arrays;
-// device: LDS):
-//   int32_t& lbase(int), dbase(int); uint32_t& lcnt(int), dcnt(int);
-//   uint16_t& lsym(int); uint8_t& dsym(int)
+// One lane's tables for its current block, in the Store (host: arrays;
+// device: LDS): the limits (only the long codes past the one-lookup tables
+// read them), the bases, the symbols sorted by (length, value) and the
+// per-length counts a header read keeps:
+//   uint32_t& llim(int), dlim(int); int32_t& lbase(int), dbase(int);
+//   uint32_t& lcnt(int), dcnt(int); uint16_t& lsym(int); uint8_t& dsym(int)
 // Decode entries: the value in bits 0..15 (a literal byte, a length base or
 // a distance base), its extra bits in 16..19, the code length in 20..23
 // (fast tables only; 0 = not in the table), the kind in 24..25.
@@ -519,19 +518,18 @@ GG_HD uint32_t dist_value(int d) {  // distance symbol -> entry
 
 template <class Store>
 struct LaneTables {
-  uint32_t llim[kMaxBits + 1], dlim[kMaxBits + 1];
   Store s;
   GG_HD void set_lit(const Canon& c) {
 #pragma unroll
     for (int l = 0; l <= kMaxBits; ++l) {
-      llim[l] = c.limit[l];
+      s.llim(l) = c.limit[l];
       s.lbase(l) = c.base[l];
     }
   }
   GG_HD void set_dist(const Canon& c) {
 #pragma unroll
     for (int l = 0; l <= kMaxBits; ++l) {
-      dlim[l] = c.limit[l];
+      s.dlim(l) = c.limit[l];
       s.dbase(l) = c.base[l];
     }
   }
@@ -558,13 +556,13 @@ struct LaneTables {
   }
   // The fast entry of the kFastBits stream bits i (LSB first) for the lit/len
   // (dist = false) or distance code: 0 when the code there is longer.
-  GG_HD uint32_t fast_entry(uint32_t i, bool dist_code) const {
+  GG_HD uint32_t fast_entry(uint32_t i, bool dist_code) {
     const uint32_t x = rev15(i);  // (bits past the kFastBits read as 0)
     int L = 1;  // the smallest l with x < limit[l] (15: none below 15)
 #pragma unroll
-    for (int l = 1; l < kMaxBits; ++l) L += x >= (dist_code ? dlim[l] : llim[l]) ? 1 : 0;
+    for (int l = 1; l < kMaxBits; ++l) L += x >= (dist_code ? s.dlim(l) : s.llim(l)) ? 1 : 0;
     if (L > kFastBits) return 0;
-    Store& st = const_cast<Store&>(s);
+    Store& st = s;
     const uint32_t v = dist_code ? dist_value(st.dsym(st.dbase(L) + (int)(x >> (kMaxBits - L))))
                                  : lit_value(st.lsym(st.lbase(L) + (int)(x >> (kMaxBits - L))));
     return v | ((uint32_t)L << kFastLenShift);
@@ -579,8 +577,8 @@ struct LaneTables {
     const uint32_t x = rev15(cur.peek());
     int L = 1;
 #pragma unroll
-    for (int l = 1; l < kMaxBits; ++l) L += x >= llim[l] ? 1 : 0;
-    if (x >= llim[kMaxBits]) return -1;
+    for (int l = 1; l < kMaxBits; ++l) L += x >= s.llim(l) ? 1 : 0;
+    if (x >= s.llim(kMaxBits)) return -1;
     cur.skip((uint32_t)L);
     return s.lsym(s.lbase(L) + (int)(x >> (kMaxBits - L)));
   }
@@ -588,8 +586,8 @@ struct LaneTables {
     const uint32_t x = rev15(cur.peek());
     int L = 1;
 #pragma unroll
-    for (int l = 1; l < kMaxBits; ++l) L += x >= dlim[l] ? 1 : 0;
-    if (x >= dlim[kMaxBits]) return -1;
+    for (int l = 1; l < kMaxBits; ++l) L += x >= s.dlim(l) ? 1 : 0;
+    if (x >= s.dlim(kMaxBits)) return -1;
     cur.skip((uint32_t)L);
     return s.dsym(s.dbase(L) + (int)(x >> (kMaxBits - L)));
   }
@@ -598,6 +596,7 @@ struct LaneTables {
 // Host store: plain arrays.  (lcnt / dcnt: counts per length, then the
 // next slot per length, while a header is read.)
 struct ArrayStore {
+  uint32_t ll[kMaxBits + 1], dl[kMaxBits + 1];
   int32_t lb[kMaxBits + 1], db[kMaxBits + 1];
   uint32_t lc[kMaxBits + 1], dc[kMaxBits + 1];
   uint16_t ls[kLitSyms];
@@ -605,6 +604,8 @@ struct ArrayStore {
   uint32_t lf[kFastSize], df[kFastSize];
   uint32_t& lfast(int i) { return lf[i]; }
   uint32_t& dfast(int i) { return df[i]; }
+  uint32_t& llim(int l) { return ll[l]; }
+  uint32_t& dlim(int l) { return dl[l]; }
   int32_t& lbase(int l) { return lb[l]; }
   int32_t& dbase(int l) { return db[l]; }
   uint32_t& lcnt(int l) { return lc[l]; }

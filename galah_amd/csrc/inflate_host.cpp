@@ -26,8 +26,8 @@ namespace gg {
 // and ISIZE.  False when buf is not gzip (CM 8) or too short.  Whether the
 // deflate stream ends exactly at the trailer (one member) is checked after
 // decoding.
-bool gzip_member(const uint8_t* buf, size_t n, size_t* data_off, size_t* data_len, uint32_t* isize, uint32_t* crc) {
-  if (n < 18 || buf[0] != 0x1f || buf[1] != 0x8b || buf[2] != 8) return false;
+bool gzip_header(const uint8_t* buf, size_t n, uint64_t file_size, size_t* data_off) {
+  if (n < 10 || file_size < 18 || buf[0] != 0x1f || buf[1] != 0x8b || buf[2] != 8) return false;
   const uint8_t flg = buf[3];
   if (flg & 0xE0) return false;  // reserved bits
   size_t p = 10;
@@ -41,7 +41,14 @@ bool gzip_member(const uint8_t* buf, size_t n, size_t* data_off, size_t* data_le
       ++p;
     }
   if (flg & 2) p += 2;
-  if (p + 8 > n) return false;
+  if (p > n || p + 8 > file_size) return false;
+  *data_off = p;
+  return true;
+}
+
+bool gzip_member(const uint8_t* buf, size_t n, size_t* data_off, size_t* data_len, uint32_t* isize, uint32_t* crc) {
+  size_t p;
+  if (!gzip_header(buf, n, n, &p)) return false;
   *data_off = p;
   *data_len = n - 8 - p;
   *crc = (uint32_t)buf[n - 8] | ((uint32_t)buf[n - 7] << 8) | ((uint32_t)buf[n - 6] << 16) | ((uint32_t)buf[n - 5] << 24);
@@ -62,6 +69,18 @@ gg_status hand_back(const char* why, uint32_t f) {
   if (inflate_debug()) fprintf(stderr, "[inflate] batch handed back to the host: %s (file %u of the batch)\n", why, f);
   return GG_OK;
 }
+// A scratch buffer that does not fit the device's memory hands the batch
+// to the host decoder (counted like any other hand-back) instead of failing
+// the call: the host path needs no device memory beyond the text.
+#define GZ_SCRATCH(m, key, count, out)                                           \
+  do {                                                                           \
+    const hipError_t _e = scratch_t((m), (key), (count), (out));                 \
+    if (_e == hipErrorOutOfMemory) {                                             \
+      (void)hipGetLastError();                                                   \
+      return hand_back("device memory for " key, 0);                             \
+    }                                                                            \
+    if (_e != hipSuccess) return hip_fail((m), _e, "scratch " key);             \
+  } while (0)
 constexpr uint32_t kChunkBytes = 16384;  // search granularity: a zlib -6 block of FASTA is ~25-30 KB
 constexpr int kMaxRelaunch = 8;         // decode passes that may drop wrong starts before giving up
 }  // namespace
@@ -184,8 +203,8 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
       scr += inflate::decode_scratch(bits);
     }
   uint32_t *d_tok = nullptr, *d_scr = nullptr;
-  GG_HIP(m, scratch_t(m, "gz_tok", std::max<uint64_t>(toks, 4), &d_tok));
-  GG_HIP(m, scratch_t(m, "gz_scr", std::max<uint64_t>(scr, 4), &d_scr));
+  GZ_SCRATCH(m, "gz_tok", std::max<uint64_t>(toks, 4), &d_tok);
+  GZ_SCRATCH(m, "gz_scr", std::max<uint64_t>(scr, 4), &d_scr);
   for (int pass = 0;; ++pass) {
     std::vector<uint32_t> redo;
     for (uint32_t l = 0; l < (uint32_t)lanes.size(); ++l)
@@ -313,7 +332,13 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   for (size_t l = 0; l < lane_out.size(); ++l) lane_out[l] += foff[live[l].file];
   uint32_t *d_val, *d_flags, *d_crc, *d_lfile;
   uint64_t *d_lout, *d_ftext, *d_flen;
-  GG_HIP(m, scratch_t(m, "gz_val", std::max<uint64_t>(text_len, 1), &d_val));
+  GZ_SCRATCH(m, "gz_val", std::max<uint64_t>(text_len, 1), &d_val);
+  // (tests: GALAHGPU_TEST_POISON_VAL=<u32> fills val with that word first --
+  // what a previous batch or another allocation left there -- and no result
+  // may change: the resolve reads val only where the expand wrote it)
+  const char* poison = getenv("GALAHGPU_TEST_POISON_VAL");
+  if (poison && *poison && text_len)
+    GG_HIP(m, hipMemsetD32Async(d_val, (int)strtoul(poison, nullptr, 0), text_len, st));
   GG_HIP(m, scratch_t(m, "stage_text", std::max<uint64_t>(text_len, 16) + 16, d_text));
   // per live lane: text position, token offset, token count, end of the
   // padding after it (its file's last lane: the next file's start; else 0)

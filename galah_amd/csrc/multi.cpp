@@ -282,28 +282,6 @@ gg_status pairs_with_ani(gg_ctx* c, const std::vector<gg_pair>& res, gg_pair** p
 constexpr uint32_t kBatchGenomes = 32;          // genomes per K1 batch
 constexpr uint64_t kBatchWords = 64ull << 20;   // or 1 Gbases of packed words, whichever first
 constexpr uint64_t kBatchText = 1ull << 30;     // raw (device-parsed) batches: 1 GiB of FASTA text
-// device-inflate batches: up to 4096 files, 192 MiB of gzip data or 600 MiB
-// of text (the inflate's parallel units are the streams' blocks, ~30 per
-// 3 Mbp genome: a batch needs hundreds of files to fill the GPU)
-constexpr uint32_t kBatchGenomesGz = 4096;
-// (GALAHGPU_GZ_BATCH_MB sets the gzip bytes per batch, the text cap follows
-// at 3x, at most 960 MiB: tuning only, no result depends on it)
-uint64_t gz_batch_bytes() {
-  static const uint64_t v = [] {
-    const char* e = getenv("GALAHGPU_GZ_BATCH_MB");
-    const long mb = e ? atol(e) : 0;
-    return (uint64_t)(mb > 0 ? std::min(mb, 320L) : 192L) << 20;
-  }();
-  return v;
-}
-uint64_t gz_batch_text() { return std::min<uint64_t>(3 * gz_batch_bytes(), 960ull << 20); }  // (text < 1 GiB)
-// staging copy threads per member (GALAHGPU_GZ_COPY_THREADS; tuning only)
-int gz_copy_threads(int copy_threads) {
-  const char* e = getenv("GALAHGPU_GZ_COPY_THREADS");
-  const int t = e ? atoi(e) : 0;
-  return std::max(1, t > 0 ? std::min(t, copy_threads) : std::min(copy_threads, 4));
-}
-
 // memcpy on up to T threads (staging copies of a batch into pinned memory:
 // one thread moves ~10 GB/s, a batch of FASTA text is up to 1 GiB)
 void parallel_copy(void* dst, const void* src, size_t bytes, int T) {
@@ -335,19 +313,7 @@ bool device_parse() {
   return e && strcmp(e, "device") == 0;
 }
 
-// Device inflate: gzip files go to the device compressed and are inflated
-// there (inflate.hip), then parsed there (parse.hip); the host threads only
-// read files.  The default when the file list starts with a .gz path (the
-// device parses the other files' text too); GALAHGPU_INFLATE=device / host
-// forces either path.
-bool device_inflate(const char* const* paths, uint32_t n) {
-  const char* e = getenv("GALAHGPU_INFLATE");
-  if (e && strcmp(e, "device") == 0) return true;
-  if (e && strcmp(e, "host") == 0) return false;
-  if (n == 0 || !paths[0]) return false;
-  const size_t l = strlen(paths[0]);
-  return l >= 3 && strcmp(paths[0] + l - 3, ".gz") == 0;
-}
+}  // namespace
 
 // One batch of FASTA text, already in device memory (d_text, files at
 // foff[0..nf]), parsed on the device: 2-bit words into *d_words (scratch of
@@ -490,257 +456,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   return GG_OK;
 }
 
-// Device-inflate batches of the streamed file list (GALAHGPU_INFLATE=
-// device), pipelined per member: while the member inflates, parses and
-// sketches batch N on its stream, a helper thread stages batch N + 1 into
-// the member's other slot -- files read by the PackStream workers, copied
-// into the slot's pinned buffer (gzip files compressed, each positioned so
-// its deflate data starts on a 4-byte boundary) and queued to the slot's
-// device buffer on the slot's stream as they are staged.  A batch is cut
-// early at gz_batch_bytes() of gzip data or gz_batch_text() of text (the
-// first two at 1/4 and 1/2 of that; the rest goes back through the cursor).  A batch the device inflate does not take
-// is decoded on the host threads instead (GG_FALLBACK_INFLATE_HOST).
-struct GzHeld {
-  uint64_t pos, len;
-  bool gz;
-};
-struct GzStaged {
-  uint32_t b0 = 0, b1 = 0;  // the files taken
-  std::vector<InflateFile> files;
-  std::vector<GzHeld> held;
-  std::vector<uint32_t> row_of;
-  uint64_t at = 0;          // bytes staged
-  bool host_only = false;   // a gzip header the device path does not read
-  gg_status st = GG_OK;     // a file that did not read (err), or a HIP failure
-  bool file_err = false;
-  std::string err;
-  double ms = 0;
-  Clock::time_point t0;  // when staging began (debug)
-};
-
-class GzPipe {
- public:
-  GzPipe(gg_ctx* m, PackStream& stream, uint32_t nm, std::mutex& cursor_mu, uint32_t& cursor, bool& stop,
-         int copy_threads, const std::vector<uint32_t>& miss_at)
-      : m_(m), stream_(stream), nm_(nm), mu_(cursor_mu), cursor_(cursor), stop_(stop), threads_(copy_threads),
-        miss_at_(miss_at) {}
-  ~GzPipe() {
-    if (next_.valid()) next_.wait();
-  }
-  // The next staged batch (nullptr: no more); starts staging the one after.
-  GzStaged* next() {
-    bool have;
-    if (next_.valid()) {
-      have = next_.get();
-    } else {
-      have = stage(slot_, staged_[slot_]);
-    }
-    if (!have) return nullptr;
-    cur_ = slot_;
-    slot_ ^= 1;
-    if (staged_[cur_].st == GG_OK)
-      next_ = std::async(std::launch::async, [this] {
-        (void)hipSetDevice(m_->device);
-        return stage(slot_, staged_[slot_]);
-      });
-    return &staged_[cur_];
-  }
-  const uint8_t* host() const { return m_->gz_slot[cur_].host; }
-  uint8_t* dev() const { return m_->gz_slot[cur_].dev; }
-  hipStream_t up_stream() const { return m_->gz_slot[cur_].st; }
-
- private:
-  static constexpr uint64_t kUpPiece = 16ull << 20;  // device copies of >= 16 MiB as the batch is staged
-
-  // Claims and stages one batch into slot si; false when no files are left.
-  bool stage(int si, GzStaged& g) {
-    g = GzStaged{};
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      if (stop_ || cursor_ >= nm_) return false;
-      g.b0 = cursor_;
-      g.b1 = std::min(nm_, g.b0 + kBatchGenomesGz);
-      cursor_ = g.b1;
-    }
-    const auto t0 = Clock::now();
-    g.t0 = t0;
-    gg_ctx::GzSlot& sl = m_->gz_slot[si];
-    auto hip = [&](hipError_t e, const char* what) {
-      if (e != hipSuccess && g.st == GG_OK) {
-        g.st = e == hipErrorOutOfMemory ? GG_ERR_OUT_OF_MEMORY : GG_ERR_HIP;
-        g.err = std::string(what) + ": " + hipGetErrorString(e);
-      }
-      return e == hipSuccess;
-    };
-    if (!sl.st && !hip(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking), "hipStreamCreate")) return true;
-    uint64_t up = 0;  // bytes [0, up) are queued to sl.dev
-    uint64_t gz_bytes = 0, text_est = 0;
-    // the first batches smaller (1/4, 1/2): the device starts while the
-    // full-size ones are staged
-    const int ramp = n_staged_ < 2 ? 2 - n_staged_ : 0;
-    ++n_staged_;
-    const uint64_t cut_gz = gz_batch_bytes() >> ramp, cut_text = gz_batch_text() >> ramp;
-    for (uint32_t i = g.b0; i < g.b1; ++i) {
-      const uint8_t* fb;
-      size_t fl;
-      bool gz = false;
-      const gg_status gs = stream_.get_bytes(i, &fb, &fl, &g.err, &gz);
-      if (gs != GG_OK) {
-        g.st = gs;
-        g.file_err = true;
-        g.b1 = i;
-        return true;
-      }
-      InflateFile f;
-      size_t doff = 0, dlen = fl;
-      uint32_t isz = 0, crc = 0;
-      const bool member = gz && gzip_member(fb, fl, &doff, &dlen, &isz, &crc);
-      if (gz && !member) g.host_only = true;
-      const uint64_t p = (g.at + doff + 3) / 4 * 4 - doff;
-      const uint64_t need = p + fl + 16;
-      if (need > sl.host_cap || need + kInflatePad > sl.dev_cap) {  // grow the slot (a batch of large files)
-        if (!hip(hipStreamSynchronize(sl.st), "hipStreamSynchronize")) return true;
-        const uint64_t cap = std::max<uint64_t>(need + kInflatePad, 2 * gz_batch_bytes());
-        if (need > sl.host_cap) {
-          uint8_t* h = nullptr;
-          if (!hip(hipHostMalloc((void**)&h, cap, hipHostMallocDefault), "hipHostMalloc")) return true;
-          if (g.at) memcpy(h, sl.host, g.at);
-          if (sl.host) (void)hipHostFree(sl.host);
-          sl.host = h;
-          sl.host_cap = cap;
-        }
-        if (need + kInflatePad > sl.dev_cap) {
-          if (sl.dev) (void)hipFree(sl.dev);
-          sl.dev = nullptr;
-          sl.dev_cap = 0;
-          if (!hip(hipMalloc((void**)&sl.dev, cap), "hipMalloc")) return true;
-          sl.dev_cap = cap;
-          up = 0;  // (queued again from the host copy)
-        }
-      }
-      parallel_copy(sl.host + p, fb, fl, threads_);
-      f.gz = member;
-      f.data_off = p + doff;
-      f.data_len = dlen;
-      f.isize = isz;
-      f.crc = crc;
-      g.files.push_back(f);
-      g.held.push_back(GzHeld{p, fl, gz});
-      g.at = p + fl;
-      if (g.at - up >= kUpPiece) {
-        if (!hip(hipMemcpyAsync(sl.dev + up, sl.host + up, g.at - up, hipMemcpyHostToDevice, sl.st), "hipMemcpyAsync"))
-          return true;
-        up = g.at;
-      }
-      gz_bytes += gz ? fl : 0;
-      text_est += member ? isz : fl;
-      g.row_of.push_back(miss_at_[i]);
-      stream_.release(i);
-      if ((gz_bytes >= cut_gz || text_est >= cut_text) && i + 1 < g.b1) {  // cut the batch here
-        std::lock_guard<std::mutex> lk(mu_);
-        if (cursor_ == g.b1) {
-          cursor_ = i + 1;
-          g.b1 = i + 1;
-        }
-      }
-    }
-    if (g.at > up &&
-        !hip(hipMemcpyAsync(sl.dev + up, sl.host + up, g.at - up, hipMemcpyHostToDevice, sl.st), "hipMemcpyAsync"))
-      return true;
-    g.ms = ms_since(t0);
-    return true;
-  }
-
-  gg_ctx* m_;
-  PackStream& stream_;
-  int n_staged_ = 0;  // batches staged so far
-  uint32_t nm_;
-  std::mutex& mu_;
-  uint32_t& cursor_;
-  bool& stop_;
-  int threads_;
-  const std::vector<uint32_t>& miss_at_;
-  GzStaged staged_[2];
-  int slot_ = 0, cur_ = 0;
-  std::future<bool> next_;
-};
-
-// Inflates (or, when the device path does not take it, decodes on the host
-// threads) and parses one staged batch on m's stream: 2-bit words into
-// *d_words, runs into runs.
-gg_status inflate_staged_batch(gg_ctx* m, GzPipe& pipe, GzStaged& g, int copy_threads, std::mutex& cursor_mu,
-                               bool& stop, bool& file_error, uint32_t** d_words, uint64_t* nw,
-                               std::vector<gg_run>& runs, const char* const* names) {
-  static const bool dbg = [] {
-    const char* e = getenv("GALAHGPU_INFLATE_DEBUG");
-    return e && *e == '1';
-  }();
-  const auto t0 = Clock::now();
-  if (g.st != GG_OK) {
-    if (g.file_err) {
-      std::lock_guard<std::mutex> lk(cursor_mu);
-      if (!stop) file_error = true;
-    }
-    return fail(m, g.st, g.err);
-  }
-  // the stream waits for the batch's copies (queued on the slot's stream)
-  hipEvent_t up_done = m->copy_done;
-  if (!up_done) GG_HIP(m, hipEventCreateWithFlags(&m->copy_done, hipEventDisableTiming));
-  up_done = m->copy_done;
-  GG_HIP(m, hipEventRecord(up_done, pipe.up_stream()));
-  GG_HIP(m, hipStreamWaitEvent(m->stream, up_done, 0));
-  static const Clock::time_point t_proc = Clock::now();  // (debug: times since the process's first batch)
-  if (dbg)
-    fprintf(stderr, "[inflate] at %.3f ms: batch of %zu files staged in %.3f ms (staging began at %.3f ms)\n",
-            ms_since(t_proc), g.files.size(), g.ms,
-            std::chrono::duration<double, std::milli>(g.t0 - t_proc).count());
-  uint8_t* d_text = nullptr;
-  std::vector<uint64_t> foff;
-  bool ok = false;
-  if (!g.host_only) {
-    const gg_status is = inflate_batch(m, pipe.host(), g.at, g.files, &d_text, foff, &ok, pipe.dev());
-    if (is != GG_OK) return is;
-  }
-  if (!ok) {  // the host decodes this batch (and reports a corrupt file)
-    ++m->fallbacks[GG_FALLBACK_INFLATE_HOST];
-    const size_t nf = g.files.size();
-    std::vector<std::vector<uint8_t>> texts(nf);
-    std::vector<gg_status> sts(nf, GG_OK);
-    std::vector<std::string> errs(nf);
-    std::vector<std::thread> th;
-    const int T = std::max(1, std::min<int>(copy_threads, (int)nf));
-    auto work = [&](int t) {
-      for (size_t f = (size_t)t; f < nf; f += (size_t)T) {
-        const uint8_t* b = pipe.host() + g.held[f].pos;
-        if (g.held[f].gz) {
-          const std::vector<uint8_t> gzb(b, b + g.held[f].len);
-          sts[f] = host_text_from_gzip(gzb, names[g.b0 + f], texts[f], errs[f]);
-        } else {
-          texts[f].assign(b, b + g.held[f].len);
-        }
-      }
-    };
-    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
-    for (size_t f = 0; f < nf; ++f)
-      if (sts[f] != GG_OK) {
-        std::lock_guard<std::mutex> lk(cursor_mu);
-        if (!stop) file_error = true;
-        return fail(m, sts[f], errs[f]);
-      }
-    foff.assign(nf + 1, 0);
-    for (size_t f = 0; f < nf; ++f) foff[f + 1] = foff[f] + (texts[f].size() + 15) / 16 * 16;
-    std::vector<uint8_t> all(foff[nf], '\n');
-    for (size_t f = 0; f < nf; ++f) memcpy(all.data() + foff[f], texts[f].data(), texts[f].size());
-    GG_HIP(m, scratch_t(m, "stage_text", std::max<uint64_t>(foff[nf], 16) + 16, &d_text));
-    if (foff[nf]) GG_HIP(m, hipMemcpyAsync(d_text, all.data(), foff[nf], hipMemcpyHostToDevice, m->stream));
-    GG_HIP(m, hipStreamSynchronize(m->stream));
-  }
-  const gg_status ps = parse_raw_batch(m, d_text, foff, d_words, nw, runs);
-  if (dbg) fprintf(stderr, "[inflate] at %.3f ms: batch inflated and parsed in %.3f ms\n", ms_since(t_proc), ms_since(t0));
-  return ps;
-}
+namespace {
 
 // Sketches of paths[0..n) into every member's full array (rows[i]); spans
 // receives the rows each member sketched.  Genomes with a valid entry in
@@ -798,12 +514,19 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
   const uint32_t nm = (uint32_t)miss.size();
   // in-flight packed genomes: ~2 batches per member, at least 1 GiB
   const uint64_t budget = std::max<uint64_t>(1ull << 30, 2ull * M * kBatchWords * sizeof(uint32_t));
-  const bool gz_dev = device_inflate(miss.data(), (uint32_t)miss.size());
-  const bool raw = gz_dev || device_parse();
-  // staging copies per member: the host threads shared among the members
+  const bool gz_dev = gz_device_list(miss.data(), nm);
+  const bool raw = device_parse();
+  // host threads per member: the host threads shared among the members
   const int copy_threads = std::max(1, std::min(16, ingest_threads(c->host_threads)) / (int)M);
-  PackStream stream(miss.data(), nm, c->k, c->host_threads, gz_dev ? std::max<uint64_t>(budget, 3 * gz_batch_bytes()) : budget,
-                    cache_dir != nullptr, raw, gz_dev);
+  // gzip lists: ingest_gz.cpp's stagers read the files; otherwise the
+  // PackStream workers read (and pack) them
+  std::unique_ptr<PackStream> streamp;
+  if (!gz_dev) streamp.reset(new PackStream(miss.data(), nm, c->k, c->host_threads, budget, cache_dir != nullptr, raw));
+  GzClaims claims;
+  claims.paths = miss.data();
+  claims.row_of = miss_at.data();
+  claims.n = nm;
+  claims.cache_dir = cache_dir;
   std::mutex cursor_mu;
   uint32_t cursor = 0;
   bool stop = false;        // a member failed: the others take no more batches
@@ -825,23 +548,15 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
                                hipMemcpyHostToDevice, m->stream));
     }
     GG_HIP(m, hipStreamSynchronize(m->stream));
+    if (gz_dev) return gz_member_ingest(m, claims, r.sk, r.len, copy_threads, owned[mi]);
+    PackStream& stream = *streamp;
     std::vector<gg_run> runs;
     std::vector<uint32_t> row_of;
     std::vector<uint64_t> out_rows;
     std::vector<uint32_t> out_lens;
-    std::unique_ptr<GzPipe> pipe;
-    // (the staging copies of compressed files need few threads: the
-    // PackStream workers reading the files share the host's CPUs)
-    if (gz_dev) pipe.reset(new GzPipe(m, stream, nm, cursor_mu, cursor, stop, gz_copy_threads(copy_threads), miss_at));
     for (;;) {
       uint32_t b0, b1;
-      GzStaged* staged = nullptr;
-      if (gz_dev) {
-        staged = pipe->next();
-        if (!staged) break;
-        b0 = staged->b0;
-        b1 = staged->b1;
-      } else {
+      {
         std::lock_guard<std::mutex> lk(cursor_mu);
         if (stop || cursor >= nm) break;
         b0 = cursor;
@@ -854,12 +569,7 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
       uint64_t nw = 0;
       uint32_t g = 0;
       uint32_t* d_words = nullptr;
-      if (gz_dev) {  // gzip -> device inflate -> device parser
-        const gg_status gs = inflate_staged_batch(m, *pipe, *staged, copy_threads, cursor_mu, stop, file_error,
-                                                  &d_words, &nw, runs, miss.data());
-        if (gs != GG_OK) return gs;
-        row_of = staged->row_of;
-      } else if (raw) {  // FASTA text -> device parser
+      if (raw) {  // FASTA text -> device parser
         std::vector<uint64_t> foff(1, 0);
         for (uint32_t i = b0; i < b1; ++i) {
           const std::vector<uint8_t>* tx;
@@ -966,13 +676,18 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
         if (!file_error && first_fail < 0) first_fail = (int)mi;
         stop = true;
       }
-      stream.abort();  // wakes members waiting for genomes nobody will pack now
+      claims.halt();
+      if (streamp) streamp->abort();  // wakes members waiting for genomes nobody will pack now
     }
     return r;
   });
+  if (gz_dev) {  // a file that did not read or decode: the lowest failing index, as a serial reader meets it
+    gz_settle_errors(claims);
+    if (claims.err_idx != UINT32_MAX) return fail(c, claims.err_st, claims.err_msg);
+  }
   if (file_error) {  // report the lowest failing file, as a serial reader would meet it
     std::string err;
-    const gg_status fs = stream.first_error(&err);
+    const gg_status fs = streamp->first_error(&err);
     if (fs != GG_OK) return fail(c, fs, err);
   }
   if (first_fail >= 0 && ms[first_fail]->err.size()) {

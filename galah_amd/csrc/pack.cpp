@@ -79,15 +79,7 @@ __attribute__((target("sse4.1"))) inline uint32_t pack16(const uint8_t* p, uint3
 // Packs the runs of ONE genome; bases start at word 0 of its own buffer.
 struct GenomePacker {
   int k;
-  std::vector<uint8_t> text;  // raw streams: the FASTA text (parse.hip), or the gzip file itself (gz)
-  bool gz = false;
-  // keep_gzip streams: the gzip file mapped (its page-cache pages, no copy)
-  // instead of read into text
-  const uint8_t* map = nullptr;
-  size_t map_len = 0;
-  ~GenomePacker() {
-    if (map) munmap((void*)map, map_len);
-  }
+  std::vector<uint8_t> text;  // raw streams: the FASTA text (parse.hip)
   std::vector<uint32_t> words;
   std::vector<gg_run> runs;  // base relative to this genome's first word
   uint64_t n_bases = 0;
@@ -247,34 +239,6 @@ const Deflate& deflate_lib() {
   return d;
 }
 
-// A gzip file mapped read-only with its pages populated (the page cache's
-// own pages: the device-inflate staging copies straight from them); false
-// (nothing mapped) for an empty, unreadable or non-gzip file, which then
-// takes the read path and its error.
-bool map_gzip(const char* path, GenomePacker& gp) {
-  const char* e = getenv("GALAHGPU_GZ_MMAP");  // =0: read instead (tuning only)
-  if (e && *e == '0') return false;
-  const int fd = open(path, O_RDONLY);
-  if (fd < 0) return false;
-  struct stat sb;
-  if (fstat(fd, &sb) != 0 || sb.st_size < 18) {
-    close(fd);
-    return false;
-  }
-  void* p = mmap(nullptr, (size_t)sb.st_size, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
-  close(fd);
-  if (p == MAP_FAILED) return false;
-  const uint8_t* b = (const uint8_t*)p;
-  if (b[0] != 0x1f || b[1] != 0x8b) {
-    munmap(p, (size_t)sb.st_size);
-    return false;
-  }
-  gp.map = b;
-  gp.map_len = (size_t)sb.st_size;
-  gp.gz = true;
-  return true;
-}
-
 bool read_raw(const char* path, std::vector<uint8_t>& raw, std::string& err) {
   FILE* f = fopen(path, "rb");
   if (!f) {
@@ -332,14 +296,204 @@ bool gunzip_libdeflate(const std::vector<uint8_t>& raw, std::vector<uint8_t>& bu
   return ok;
 }
 
+// gzip members with zlib (no libdeflate on the system).
+bool gunzip_zlib(const std::vector<uint8_t>& raw, std::vector<uint8_t>& buf, const char* path, std::string& err) {
+  z_stream zs{};
+  if (inflateInit2(&zs, 15 + 32) != Z_OK) {
+    err = "zlib: out of memory";
+    return false;
+  }
+  zs.next_in = const_cast<uint8_t*>(raw.data());
+  zs.avail_in = (uInt)raw.size();
+  buf.resize(std::max<size_t>(raw.size() * 4, 1 << 16));
+  size_t out = 0;
+  for (;;) {
+    if (out == buf.size()) buf.resize(buf.size() * 2);
+    zs.next_out = buf.data() + out;
+    zs.avail_out = (uInt)std::min<size_t>(buf.size() - out, 1u << 30);
+    const uInt room = zs.avail_out;
+    const int r = inflate(&zs, Z_NO_FLUSH);
+    out += room - zs.avail_out;
+    if (r == Z_STREAM_END) {
+      if (zs.avail_in < 18) break;  // (trailing bytes shorter than a member)
+      inflateReset(&zs);  // the next member
+      continue;
+    }
+    if ((r != Z_OK && r != Z_BUF_ERROR) || (r == Z_BUF_ERROR && zs.avail_in == 0)) {
+      inflateEnd(&zs);
+      err = std::string("gzip decode error in ") + path;
+      return false;
+    }
+  }
+  buf.resize(out);
+  inflateEnd(&zs);
+  return true;
+}
+
+// bzip2 and xz, the other compressions needletail 0.5 reads by their magic
+// bytes (finch's parser behind src/finch.rs:47; needletail source absent:
+// parity unpinned).  libbz2 / liblzma are loaded at run time, as libdeflate
+// is, through their stable C ABIs (the image has the libraries, not their
+// headers); concatenated streams are all decoded, as for gzip members.
+struct Bz2Lib {  // bz_stream of bzlib.h 1.0
+  struct Stream {
+    char* next_in;
+    unsigned int avail_in, total_in_lo32, total_in_hi32;
+    char* next_out;
+    unsigned int avail_out, total_out_lo32, total_out_hi32;
+    void* state;
+    void* (*bzalloc)(void*, int, int);
+    void (*bzfree)(void*, void*);
+    void* opaque;
+  };
+  int (*init)(Stream*, int, int) = nullptr;
+  int (*run)(Stream*) = nullptr;
+  int (*end)(Stream*) = nullptr;
+  bool ok = false;
+  Bz2Lib() {
+    void* h = dlopen("libbz2.so.1.0", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("libbz2.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    init = (int (*)(Stream*, int, int))dlsym(h, "BZ2_bzDecompressInit");
+    run = (int (*)(Stream*))dlsym(h, "BZ2_bzDecompress");
+    end = (int (*)(Stream*))dlsym(h, "BZ2_bzDecompressEnd");
+    ok = init && run && end;
+  }
+};
+struct XzLib {  // lzma_stream of liblzma 5 (its leading fields; the rest zeroed, LZMA_STREAM_INIT)
+  struct Stream {
+    const uint8_t* next_in;
+    size_t avail_in;
+    uint64_t total_in;
+    uint8_t* next_out;
+    size_t avail_out;
+    uint64_t total_out;
+    uint8_t rest[256];
+  };
+  int (*decoder)(Stream*, uint64_t, uint32_t) = nullptr;
+  int (*code)(Stream*, int) = nullptr;
+  void (*end)(Stream*) = nullptr;
+  bool ok = false;
+  XzLib() {
+    void* h = dlopen("liblzma.so.5", RTLD_NOW | RTLD_LOCAL);
+    if (!h) return;
+    decoder = (int (*)(Stream*, uint64_t, uint32_t))dlsym(h, "lzma_stream_decoder");
+    code = (int (*)(Stream*, int))dlsym(h, "lzma_code");
+    end = (void (*)(Stream*))dlsym(h, "lzma_end");
+    ok = decoder && code && end;
+  }
+};
+
+bool is_gzip(const uint8_t* b, size_t n) { return n >= 2 && b[0] == 0x1f && b[1] == 0x8b; }
+bool is_bzip2(const uint8_t* b, size_t n) { return n >= 4 && b[0] == 'B' && b[1] == 'Z' && b[2] == 'h' && b[3] >= '1' && b[3] <= '9'; }
+bool is_xz(const uint8_t* b, size_t n) {
+  return n >= 6 && b[0] == 0xFD && b[1] == '7' && b[2] == 'z' && b[3] == 'X' && b[4] == 'Z' && b[5] == 0;
+}
+
+bool bunzip2(const std::vector<uint8_t>& raw, std::vector<uint8_t>& buf, const char* path, std::string& err) {
+  static const Bz2Lib lib;
+  if (!lib.ok) {
+    err = std::string("bzip2 file but libbz2 is not available: ") + path;
+    return false;
+  }
+  buf.resize(std::max<size_t>(raw.size() * 4, 1 << 16));
+  size_t in = 0, out = 0;
+  while (in < raw.size()) {
+    Bz2Lib::Stream s{};
+    if (lib.init(&s, 0, 0) != 0) {
+      err = "libbz2: out of memory";
+      return false;
+    }
+    int r = 0;
+    for (;;) {  // one stream
+      if (out == buf.size()) buf.resize(buf.size() * 2);
+      const unsigned int ai = (unsigned int)std::min<size_t>(raw.size() - in, 1u << 30);
+      const unsigned int ao = (unsigned int)std::min<size_t>(buf.size() - out, 1u << 30);
+      s.next_in = (char*)raw.data() + in;
+      s.avail_in = ai;
+      s.next_out = (char*)buf.data() + out;
+      s.avail_out = ao;
+      r = lib.run(&s);
+      in += ai - s.avail_in;
+      out += ao - s.avail_out;
+      if (r != 0) break;  // BZ_OK (0): more; BZ_STREAM_END (4) or an error
+      if (s.avail_in == ai && s.avail_out == ao) break;  // no progress: truncated
+    }
+    lib.end(&s);
+    if (r != 4) {
+      err = std::string("bzip2 decode error in ") + path;
+      return false;
+    }
+    if (raw.size() - in < 4 || !is_bzip2(raw.data() + in, raw.size() - in)) break;  // (trailing bytes)
+  }
+  buf.resize(out);
+  return true;
+}
+
+bool unxz(const std::vector<uint8_t>& raw, std::vector<uint8_t>& buf, const char* path, std::string& err) {
+  static const XzLib lib;
+  if (!lib.ok) {
+    err = std::string("xz file but liblzma is not available: ") + path;
+    return false;
+  }
+  XzLib::Stream s{};
+  if (lib.decoder(&s, ~0ull, 0x08 /* LZMA_CONCATENATED */) != 0) {
+    err = "liblzma: out of memory";
+    return false;
+  }
+  buf.resize(std::max<size_t>(raw.size() * 4, 1 << 16));
+  size_t out = 0;
+  s.next_in = raw.data();
+  s.avail_in = raw.size();
+  int r;
+  for (;;) {
+    if (out == buf.size()) buf.resize(buf.size() * 2);
+    s.next_out = buf.data() + out;
+    s.avail_out = buf.size() - out;
+    const size_t ao = s.avail_out;
+    r = lib.code(&s, 3 /* LZMA_FINISH */);
+    out += ao - s.avail_out;
+    if (r != 0) break;  // LZMA_OK (0): more; LZMA_STREAM_END (1) or an error
+  }
+  lib.end(&s);
+  buf.resize(out);
+  if (r != 1) {
+    err = std::string("xz decode error in ") + path;
+    return false;
+  }
+  return true;
+}
+
+// A bzip2 or xz file (its first bytes): read whole and decoded in memory
+// rather than through zlib's gzread.
+bool compressed_not_gzip(const char* path) {
+  uint8_t h[6] = {0};
+  FILE* f = fopen(path, "rb");
+  if (!f) return false;
+  const size_t got = fread(h, 1, sizeof h, f);
+  fclose(f);
+  return is_bzip2(h, got) || is_xz(h, got);
+}
+
+// A file's bytes decompressed by their magic (gzip members, bzip2 or xz
+// streams; anything else is taken as plain text).
+bool decompress_bytes(std::vector<uint8_t>& raw, std::vector<uint8_t>& buf, const char* path, std::string& err) {
+  if (is_gzip(raw.data(), raw.size())) {
+    if (deflate_lib().ok) return gunzip_libdeflate(raw, buf, path, err);
+    return gunzip_zlib(raw, buf, path, err);
+  }
+  if (is_bzip2(raw.data(), raw.size())) return bunzip2(raw, buf, path, err);
+  if (is_xz(raw.data(), raw.size())) return unxz(raw, buf, path, err);
+  buf.swap(raw);
+  return true;
+}
+
 bool read_file(const char* path, std::vector<uint8_t>& buf, std::string& err) {
   const bool gz_lib = deflate_lib().ok;
-  if (gz_lib) {
+  if (gz_lib || compressed_not_gzip(path)) {
     std::vector<uint8_t> raw;
     if (!read_raw(path, raw, err)) return false;
-    if (raw.size() >= 2 && raw[0] == 0x1f && raw[1] == 0x8b) return gunzip_libdeflate(raw, buf, path, err);
-    buf.swap(raw);
-    return true;
+    return decompress_bytes(raw, buf, path, err);
   }
   gzFile f = gzopen(path, "rb");
   if (!f) {
@@ -532,7 +686,6 @@ struct PackStream::Impl {
   uint64_t budget;
   bool stamping = false;
   bool raw = false;
-  bool keep_gzip = false;
   std::vector<FileStamp> stamps;
   std::mutex mu;
   std::condition_variable cv_done;   // a genome finished packing
@@ -567,16 +720,6 @@ struct PackStream::Impl {
       if (!paths[i]) {
         s = GG_ERR_INVALID_ARG;
         e = "null path";
-      } else if (raw && keep_gzip && map_gzip(paths[i], *gp)) {  // gzip, mapped: stays compressed (device inflate)
-      } else if (raw && keep_gzip) {  // gzip files stay compressed (device inflate)
-        if (!read_raw(paths[i], buf, e)) {
-          s = GG_ERR_IO;
-        } else if (buf.size() >= 2 && buf[0] == 0x1f && buf[1] == 0x8b) {
-          gp->gz = true;
-          gp->text.swap(buf);
-        } else {
-          s = raw_text(buf, paths[i], gp->text, e);
-        }
       } else if (!read_file(paths[i], buf, e)) {
         s = GG_ERR_IO;
       } else if (raw) {
@@ -588,8 +731,7 @@ struct PackStream::Impl {
       if (buf.capacity() > (256u << 20)) std::vector<uint8_t>().swap(buf);  // do not pin a huge buffer
       {
         std::lock_guard<std::mutex> lk(mu);
-        inflight += gp->words.size() * sizeof(uint32_t) + gp->runs.size() * sizeof(gg_run) + gp->text.size() +
-                    gp->map_len;
+        inflight += gp->words.size() * sizeof(uint32_t) + gp->runs.size() * sizeof(gg_run) + gp->text.size();
         g[i] = std::move(gp);
         st[i] = s;
         err[i] = std::move(e);
@@ -601,12 +743,11 @@ struct PackStream::Impl {
 };
 
 PackStream::PackStream(const char* const* paths, uint32_t n, int k, int n_threads, uint64_t budget_bytes,
-                       bool stamp_files, bool raw, bool keep_gzip)
+                       bool stamp_files, bool raw)
     : p_(new Impl()) {
   Impl& m = *p_;
   m.stamping = stamp_files;
   m.raw = raw;
-  m.keep_gzip = keep_gzip;
   m.stamps.resize(stamp_files ? n : 0);
   m.paths = paths;
   m.n = n;
@@ -653,7 +794,7 @@ gg_status PackStream::get(uint32_t i, const std::vector<uint32_t>** words, const
   return GG_OK;
 }
 
-gg_status PackStream::get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err, bool* gz) {
+gg_status PackStream::get_raw(uint32_t i, const std::vector<uint8_t>** text, std::string* err) {
   Impl& m = *p_;
   std::unique_lock<std::mutex> lk(m.mu);
   m.cv_done.wait(lk, [&] { return m.state[i] >= 2 || (m.stop && m.state[i] == 0); });
@@ -666,57 +807,13 @@ gg_status PackStream::get_raw(uint32_t i, const std::vector<uint8_t>** text, std
     return m.st[i];
   }
   *text = &m.g[i]->text;
-  if (gz) *gz = m.g[i]->gz;
   return GG_OK;
 }
 
-gg_status PackStream::get_bytes(uint32_t i, const uint8_t** data, size_t* len, std::string* err, bool* gz) {
-  const std::vector<uint8_t>* t = nullptr;
-  const gg_status st = get_raw(i, &t, err, gz);
-  if (st != GG_OK) return st;
-  std::lock_guard<std::mutex> lk(p_->mu);
-  const GenomePacker& g = *p_->g[i];
-  *data = g.map ? g.map : g.text.data();
-  *len = g.map ? g.map_len : g.text.size();
-  return GG_OK;
-}
-
-gg_status host_text_from_gzip(const std::vector<uint8_t>& gz, const char* name, std::vector<uint8_t>& text,
-                              std::string& err) {
+gg_status host_text_from_bytes(std::vector<uint8_t>& bytes, const char* name, std::vector<uint8_t>& text,
+                               std::string& err) {
   std::vector<uint8_t> buf;
-  if (deflate_lib().ok) {
-    if (!gunzip_libdeflate(gz, buf, name, err)) return GG_ERR_IO;
-  } else {  // zlib, all members
-    z_stream zs{};
-    if (inflateInit2(&zs, 15 + 32) != Z_OK) {
-      err = "zlib: out of memory";
-      return GG_ERR_OUT_OF_MEMORY;
-    }
-    zs.next_in = const_cast<uint8_t*>(gz.data());
-    zs.avail_in = (uInt)gz.size();
-    buf.resize(std::max<size_t>(gz.size() * 4, 1 << 16));
-    size_t out = 0;
-    for (;;) {
-      if (out == buf.size()) buf.resize(buf.size() * 2);
-      zs.next_out = buf.data() + out;
-      zs.avail_out = (uInt)std::min<size_t>(buf.size() - out, 1u << 30);
-      const uInt room = zs.avail_out;
-      const int r = inflate(&zs, Z_NO_FLUSH);
-      out += room - zs.avail_out;
-      if (r == Z_STREAM_END) {
-        if (zs.avail_in < 18) break;  // (trailing bytes shorter than a member)
-        inflateReset(&zs);  // the next member
-        continue;
-      }
-      if ((r != Z_OK && r != Z_BUF_ERROR) || (r == Z_BUF_ERROR && zs.avail_in == 0)) {
-        inflateEnd(&zs);
-        err = std::string("gzip decode error in ") + name;
-        return GG_ERR_IO;
-      }
-    }
-    buf.resize(out);
-    inflateEnd(&zs);
-  }
+  if (!decompress_bytes(bytes, buf, name, err)) return GG_ERR_IO;
   return raw_text(buf, name, text, err);
 }
 
@@ -730,8 +827,7 @@ void PackStream::release(uint32_t i) {
   {
     std::lock_guard<std::mutex> lk(m.mu);
     if (m.state[i] != 2) return;
-    m.inflight -= m.g[i]->words.size() * sizeof(uint32_t) + m.g[i]->runs.size() * sizeof(gg_run) + m.g[i]->text.size() +
-                  m.g[i]->map_len;
+    m.inflight -= m.g[i]->words.size() * sizeof(uint32_t) + m.g[i]->runs.size() * sizeof(gg_run) + m.g[i]->text.size();
     m.g[i].reset();
     m.state[i] = 3;
     while (m.frontier < m.n && m.state[m.frontier] == 3) ++m.frontier;

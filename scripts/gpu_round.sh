@@ -48,6 +48,11 @@ for st in $STAGES; do
     inflate_prof)  # kernel trace + stats of the device inflate probe
       PROBE_MODES=device run inflate_prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o inflate -- \
         python3 -u scripts/inflate_probe.py ${PROBE_FILES:-200} 2 || exit $? ;;
+    files_trace)  # kernels and copies of device-inflate calls on C2-like files (GPU idle gaps between kernels)
+      PROBE_MODES=device run files_trace 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv \
+        -d "$OUT/files_trace" -o t -- python3 -u scripts/inflate_probe.py ${PROBE_FILES:-1000} 2 || exit $? ;;
+    files_probe)  # device-inflate calls on C2-like files, no debug output (the bench's files leg alone)
+      PROBE_MODES=device run files_probe 600 python3 -u scripts/inflate_probe.py ${PROBE_FILES:-1000} 3 || exit $? ;;
     smoke)
       run smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     bench)       bench bench_c3 600 --steps 20 --warmup 5 ;;

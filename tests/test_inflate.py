@@ -187,6 +187,34 @@ def test_device_inflate_corrupt_streams_fail_as_host(tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("poison", ["0", "257", "0x7fffffff"])
+def test_device_inflate_does_not_read_stale_val(golden, monkeypatch, tmp_path, poison):
+    """The resolve pass reads the expand's val array only at the bytes the
+    expand left as pointers.  Before round 5 it read all 16 entries of a
+    group, including the '\\n' padding between files, which no kernel
+    writes, and wrote what those stale words resolved to into the padding:
+    harmless while they held zeros (file 0's '>' started an empty record),
+    but other stale words appended bases to a genome's last record (the
+    round-4 __launch_bounds__(64, 4) build, whose scratch allocation changed
+    what the buffer held).  val filled with a pointer into file 0's sequence
+    (257), with zeros, and with an out-of-range word: the same sketches, no
+    batch handed back; a plain FASTA file first in the batch (its text is
+    never in val) included."""
+    monkeypatch.setenv("GALAHGPU_TEST_POISON_VAL", poison)
+    plain = tmp_path / "plain_first.fna"
+    with gzip.open(golden["paths"][0], "rb") as f:
+        plain.write_bytes(f.read())
+    paths = [str(plain)] + list(golden["paths"])
+    sk, lens, fb = sketch_files(paths, monkeypatch, "device")
+    assert fb["inflate_host"] == 0
+    exp_sk = [golden["sketches"][0]] + list(golden["sketches"])
+    exp_len = [golden["lens"][0]] + list(golden["lens"])
+    assert list(lens) == exp_len
+    for g in range(len(lens)):
+        assert (sk[g][:lens[g]] == exp_sk[g][:lens[g]]).all(), paths[g]
+
+
+@pytest.mark.gpu
 def test_device_inflate_is_the_default_and_knobs_change_nothing(golden, monkeypatch):
     """A .gz list takes the device path with no knob set (the info line
     counts no host-inflated batch); mapped vs read files, small batches and
