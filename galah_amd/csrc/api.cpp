@@ -1116,6 +1116,12 @@ std::vector<uint32_t> build_cmin(uint32_t s, int k, float min_ani) {
   return cmin;
 }
 
+gg_status mark_rows_ready(gg_ctx* m) {
+  if (!m->rows_ready) GG_HIP(m, hipEventCreateWithFlags(&m->rows_ready, hipEventDisableTiming));
+  GG_HIP(m, hipEventRecord(m->rows_ready, m->stream));
+  return GG_OK;
+}
+
 gg_ctx* lane_ctx(gg_ctx* m, size_t i) {
   if (m->lanes.size() <= i) m->lanes.resize(i + 1, nullptr);
   gg_ctx*& l = m->lanes[i];
@@ -1249,6 +1255,7 @@ void gg_destroy(gg_ctx* ctx) {
   for (hipEvent_t e : ctx->rep_done)
     if (e) (void)hipEventDestroy(e);
   if (ctx->copy_done) (void)hipEventDestroy(ctx->copy_done);
+  if (ctx->rows_ready) (void)hipEventDestroy(ctx->rows_ready);
   if (ctx->copy_stream) (void)hipStreamDestroy(ctx->copy_stream);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   for (auto& sl : ctx->gz_slot) {

@@ -101,7 +101,8 @@ struct gg_ctx {
   // from one while N + 1 is staged into the other by a helper thread, which
   // touches only its slot (grow-only pinned and device buffers, its stream)
   struct GzSlot {
-    uint8_t* host = nullptr;
+    uint8_t* host = nullptr;      // (mapped: host_dev is its device address)
+    uint8_t* host_dev = nullptr;
     size_t host_cap = 0;
     uint8_t* dev = nullptr;
     size_t dev_cap = 0;
@@ -149,6 +150,9 @@ struct gg_ctx {
   // time of the copies, read after the pairs phase) and whether they are live
   std::vector<hipEvent_t> rep_start, rep_done;
   std::vector<char> rep_live;
+  // recorded on `stream` when this member's rows of the call are final
+  // (sketch phase done): the other members' replication copies wait on it
+  hipEvent_t rows_ready = nullptr;
   hipStream_t copy_stream = nullptr;  // run-table uploads beside work on `stream` (sketch_core)
   hipEvent_t copy_done = nullptr;
   // host threads for file ingest (<= 0: gg_pack_files' default)
@@ -231,6 +235,9 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
 // Synchronises m->stream.  (multi.cpp)
 gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<uint64_t>& foff, uint32_t** d_words,
                           uint64_t* n_words, std::vector<gg_run>& runs);
+
+// Records m->rows_ready on m->stream (after the member's sketching).
+gg_status mark_rows_ready(gg_ctx* m);
 
 // Helper context i >= 1 of single-device context m: the same device, k, s
 // and seed, its own stream and scratch (api.cpp; owned by m).

@@ -268,7 +268,16 @@ struct InflateDecode {
   uint64_t* out_len;           // [n_lanes] bytes the lane's tokens stand for
   uint64_t* last_end;          // [n_lanes] bit after the lane's last block
   uint32_t* bfinal;            // [n_lanes] the lane decoded the stream's last block
+  // lanes [0, n_staged) take the staged kernel (the segment's compressed
+  // words copied into LDS first; every stream read of the decode is an LDS
+  // read): those whose words fit inflate_stage_words(); the rest read global
+  // memory
+  uint32_t n_staged = 0;
 };
+// A segment (start .. end bits of its file) fits the staged decode when
+// these words hold it (the words its bits touch + the readers' look-ahead).
+uint32_t inflate_stage_words();
+__host__ __device__ inline uint64_t inflate_segment_words(uint64_t start_bit, uint64_t end_bit) { return (end_bit + 31) / 32 - start_bit / 32 + 8; }
 struct InflatePlace {
   const uint32_t* tok;
   const uint64_t* tok_off;
@@ -300,6 +309,9 @@ bool gzip_member(const uint8_t* buf, size_t n, size_t* data_off, size_t* data_le
 // flags, or does not end within buf and before the trailer.
 bool gzip_header(const uint8_t* buf, size_t n, uint64_t file_size, size_t* data_off);
 hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st);
+// bytes from mapped pinned host memory (its device address) to dst by a
+// kernel on st (inflate.hip); both buffers hold a multiple of 16 bytes
+hipError_t launch_slot_upload(uint8_t* dst, const uint8_t* src_mapped, uint64_t bytes, hipStream_t st);
 hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st);
 // expand + resolve (text[0, text_len); val is read only where the expand wrote it) + CRC-32 per file
 // (file f's 4 KB segments are seg_first[f] .. seg_first[f + 1] - 1; crc

@@ -382,6 +382,155 @@ __device__ int wave_header(const Bits& in, uint64_t pos, LaneTables<LdsStore>& t
   return bt;
 }
 
+// The stream read forward from the staged segment in LDS (the staged
+// decode): positions are bit offsets from the staged word 0; the window is
+// the three words from the current one (a peek64 at any bit offset), and the
+// two words after them are read from LDS as a symbol starts, so the rotation
+// after its advance (at most 48 bits: 0, 1 or 2 words) waits on no load.
+struct LdsCursor {
+  const uint32_t* w;  // LDS
+  uint32_t pos, wi;
+  uint32_t a, b, c;    // w[wi], w[wi + 1], w[wi + 2]
+  __device__ void seek(uint32_t p) {
+    pos = p;
+    wi = p >> 5;
+    a = w[wi];
+    b = w[wi + 1];
+    c = w[wi + 2];
+  }
+  __device__ uint32_t peek() const { return __builtin_amdgcn_alignbit(b, a, pos & 31u); }
+  __device__ uint64_t peek64() const {
+    const uint32_t sh = pos & 31u;
+    return (uint64_t)__builtin_amdgcn_alignbit(b, a, sh) | ((uint64_t)__builtin_amdgcn_alignbit(c, b, sh) << 32);
+  }
+  // advance by n <= 48 bits, with x = w[wi + 3], y = w[wi + 4] read beforehand
+  __device__ void advance(uint32_t n, uint32_t x, uint32_t y) {
+    pos += n;
+    const uint32_t d = (pos >> 5) - wi;
+    // (masks, not selects: a select chain over the three words became an
+    // indexed load from a stack copy of them)
+    const uint32_t m1 = 0u - (uint32_t)(d >= 1), m2 = 0u - (uint32_t)(d >= 2);
+    const uint32_t na = (a & ~m1) | (((b & ~m2) | (c & m2)) & m1);
+    const uint32_t nb = (b & ~m1) | (((c & ~m2) | (x & m2)) & m1);
+    const uint32_t nc = (c & ~m1) | (((x & ~m2) | (y & m2)) & m1);
+    a = na;
+    b = nb;
+    c = nc;
+    wi += d;
+  }
+  __device__ void skip(uint32_t n) { advance(n, w[wi + 3], w[wi + 4]); }  // (the slow paths)
+  __device__ uint32_t get(uint32_t n) {
+    const uint32_t v = peek() & ((1u << n) - 1u);
+    skip(n);
+    return v;
+  }
+};
+
+// decode_span (inflate_core.hpp) for the staged decode, the same tokens,
+// checkpoints, status and stop: positions relative to the staged word 0
+// (start, s_nom, range_end and stop are file bit positions, base = the
+// staged word 0's).  A symbol whose codes are all in the one-lookup tables
+// (nearly every one) is decoded without a branch: both the literal and the
+// match reading are computed (the distance lookup happens for a literal
+// too) and the right one selected, so the lanes of a wave do not split on
+// the symbol kind; the rest (long codes, end-of-block, invalid codes) take
+// decode_span's own handling.
+template <class Emit, class Ck>
+__device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_t base, uint64_t start, uint64_t s_nom,
+                                    uint64_t range_end, LaneTables<LdsStore>& t, Emit&& emit, Ck&& ck, uint32_t& n,
+                                    uint64_t& bytes_out, uint64_t& stop) {
+  LdsCursor cur{lds};
+  cur.seek((uint32_t)(start - base));
+  n = 0;
+  uint32_t bytes = 0;
+  uint32_t k = 0;
+  uint32_t next_ck = (uint32_t)(s_nom - base);
+  const uint32_t rend = (uint32_t)(range_end - base);
+  uint32_t next_stop = next_ck < rend ? next_ck : rend;
+  uint32_t st = kSpanBad;
+  for (;;) {
+    if (cur.pos >= next_stop) {
+      if (cur.pos >= rend) {
+        st = kSpanRange;
+        break;
+      }
+      if (cur.pos >= next_ck) {
+        if (!ck(k, ck_pack(cur.pos - next_ck, n, bytes))) {
+          st = kSpanSynced;
+          break;
+        }
+        ++k;
+        next_ck += kCkBits;
+      }
+      next_stop = next_ck < rend ? next_ck : rend;
+    }
+    const uint32_t x = cur.w[cur.wi + 3], y = cur.w[cur.wi + 4];  // (the words the advance may bring in)
+    const uint64_t bb = cur.peek64();
+    const uint32_t lo = (uint32_t)bb, hi = (uint32_t)(bb >> 32);
+    const uint32_t e = t.s.lfast((int)(lo & (kFastSize - 1)));
+    const uint32_t l1 = (e >> kFastLenShift) & 15u, lx = entry_extra(e);
+    const uint32_t lenv = entry_value(e) + (__builtin_amdgcn_alignbit(hi, lo, l1) & ((1u << lx) - 1u));
+    const uint32_t u = l1 + lx;  // (<= 15)
+    const uint32_t de = t.s.dfast((int)(__builtin_amdgcn_alignbit(hi, lo, u) & (kFastSize - 1)));
+    const uint32_t dl = (de >> kFastLenShift) & 15u, dx = entry_extra(de);
+    const uint32_t distv = entry_value(de) + (__builtin_amdgcn_alignbit(hi, lo, u + dl) & ((1u << dx) - 1u));
+    const uint32_t kind = entry_kind(e);
+    const bool lit = kind == kEntryLit && l1 != 0;
+    const bool mat = kind == kEntryLen && l1 != 0 && dl != 0 && entry_kind(de) == kEntryLen;
+    if (lit || mat) {
+      cur.advance(lit ? l1 : u + dl + dx, x, y);
+      if (!emit(lit ? entry_value(e) : tok_match(lenv, distv))) break;
+      ++n;
+      bytes += lit ? 1u : lenv;
+      continue;
+    }
+    // decode_span's handling of the other symbols
+    uint32_t used = l1;
+    if (used == 0) {  // a long lit/len code
+      const uint32_t e2 = t.lit_entry(cur);
+      if (entry_kind(e2) != kEntryLen) {
+        if (entry_kind(e2) == kEntryLit) {
+          if (!emit(entry_value(e2))) break;
+          ++n;
+          bytes += 1;
+          continue;
+        }
+        if (entry_kind(e2) == kEntryEob) st = kSpanEob;
+        break;
+      }
+      const uint32_t len = entry_value(e2) + cur.get(entry_extra(e2));
+      const uint32_t d2 = t.dist_entry(cur);
+      if (entry_kind(d2) != kEntryLen) break;
+      const uint32_t dist = entry_value(d2) + cur.get(entry_extra(d2));
+      if (!emit(tok_match(len, dist))) break;
+      ++n;
+      bytes += len;
+      continue;
+    }
+    if (kind != kEntryLen) {  // end-of-block or an invalid code (a literal took the fast path)
+      cur.skip(used);
+      if (kind == kEntryEob) st = kSpanEob;
+      break;
+    }
+    used += lx;
+    if (dl == 0) {  // a long distance code
+      cur.skip(used);
+      const uint32_t d2 = t.dist_entry(cur);
+      if (entry_kind(d2) != kEntryLen) break;
+      const uint32_t dist = entry_value(d2) + cur.get(entry_extra(d2));
+      if (!emit(tok_match(lenv, dist))) break;
+      ++n;
+      bytes += lenv;
+      continue;
+    }
+    cur.skip(used + dl);  // an invalid distance code
+    break;
+  }
+  bytes_out = bytes;
+  stop = base + cur.pos;
+  return st;
+}
+
 // n tokens from a lane's scratch to the segment's tokens, 8 loads in flight
 // (a plain loop waited on each load in turn).
 __device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint32_t n) {
@@ -405,10 +554,22 @@ __device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restri
 // of its checkpoints agrees with the first decode.  The right spans up to
 // the one that decoded end-of-block are the block; their tokens are copied
 // to the segment's tokens.
+//
+// Staged form (kStaged, the lanes [0, n_staged)): the segment's compressed
+// words are first copied into LDS by the whole wave (coalesced, one wait),
+// so the header walk, the sub-span decodes and their cursor refills read LDS
+// only.  Read from global memory, every cursor refill waited for its load
+// (the window rotation copies the loaded registers at once), a latency of
+// thousands of cycles every ~2.5 symbols.
 #ifndef GG_DECODE_MIN_WAVES
 #define GG_DECODE_MIN_WAVES 1
 #endif
+// (30 KB + the static tables ~10 KB: four waves per CU; a zlib -6 block of
+// FASTA is 24-27 KB)
+constexpr uint32_t kStageWords = 30 * 1024 / 4;
+template <bool kStaged>
 __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decode_kernel(InflateDecode a) {
+  extern __shared__ uint32_t stage[];  // (kStaged: kStageWords words)
   __shared__ uint32_t llm[kMaxBits + 1], dlm[kMaxBits + 1];
   __shared__ int32_t lb[kMaxBits + 1], db[kMaxBits + 1];
   __shared__ uint32_t lcn[kMaxBits + 1], dcn[kMaxBits + 1];
@@ -420,15 +581,26 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
   __shared__ uint64_t sE[kSpanLanes];
   __shared__ uint32_t sSt[kSpanLanes];
   const uint32_t j = threadIdx.x;
-  const uint32_t seg = blockIdx.x;
-  if (seg >= a.n_lanes) return;
+  const uint32_t seg = blockIdx.x + (kStaged ? 0u : a.n_staged);
+  if (seg >= a.n_lanes || (kStaged && seg >= a.n_staged)) return;
   LaneTables<LdsStore> tab;
   tab.s = LdsStore{llm, dlm, lb, db, lcn, dcn, ls, ds, lf, df};
   const uint32_t f = a.lane_file[seg];
-  const Bits in{a.in + a.file_word[f]};
+  const uint32_t* gin = a.in + a.file_word[f];
   const uint64_t limit = a.file_bits[f];
   const uint64_t end = a.lane_end[seg];  // ~0: the file's last segment (ends with the BFINAL block)
   const bool final_seg = end == ~0ull;
+  Bits in{gin};
+  uint64_t sbase = 0;  // (kStaged: the file bit position of stage[0])
+  if (kStaged) {  // words [w0, w0 + nw) of the file into LDS; `in` reads them at their file positions
+    const uint64_t s0 = a.lane_start[seg];
+    const uint64_t w0 = s0 >> 5;
+    sbase = w0 * 32;
+    const uint32_t nw = (uint32_t)inflate_segment_words(s0, final_seg ? limit : end);
+    for (uint32_t i = j; i < nw; i += kSpanLanes) stage[i] = gin[w0 + i];
+    __syncthreads();
+    in.w = stage - w0;  // (only words [w0, w0 + nw) are read)
+  }
   uint32_t* out = a.tok + a.tok_off[seg];
   const uint64_t cap = a.tok_cap[seg];
   uint32_t* scr_all = a.scr + a.scr_off[seg];
@@ -494,15 +666,15 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       uint64_t ba = 0, Ea = S;
       if (act) {
         TokSink sink{A, (uint32_t)capL};
-        sa = decode_span(in, S, S, R, tab, sink,
-                         [&](uint32_t k, uint64_t c) {
-                           if (k < ncks) {
-                             ck[k] = c;
-                             nck = k + 1;
-                           }
-                           return true;
-                         },
-                         na, ba, Ea);
+        auto ck1 = [&](uint32_t k, uint64_t c) {
+          if (k < ncks) {
+            ck[k] = c;
+            nck = k + 1;
+          }
+          return true;
+        };
+        if constexpr (kStaged) sa = decode_span_lds(stage, sbase, S, S, R, tab, sink, ck1, na, ba, Ea);
+        else sa = decode_span(in, S, S, R, tab, sink, ck1, na, ba, Ea);
         sink.flush();
       }
       phase(1);
@@ -543,15 +715,15 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
           synced = -1;
           first = eprev;
           TokSink sink{B, (uint32_t)capL};
-          sb = decode_span(in, eprev, S, R, tab, sink,
-                           [&](uint32_t k, uint64_t cc) {
-                             if (k < nck && ck_off(cc) == ck_off(ck[k])) {
-                               synced = (int)k;
-                               return false;
-                             }
-                             return true;
-                           },
-                           nb, bb, Eb);
+          auto ck2 = [&](uint32_t k, uint64_t cc) {
+            if (k < nck && ck_off(cc) == ck_off(ck[k])) {
+              synced = (int)k;
+              return false;
+            }
+            return true;
+          };
+          if constexpr (kStaged) sb = decode_span_lds(stage, sbase, eprev, S, R, tab, sink, ck2, nb, bb, Eb);
+          else sb = decode_span(in, eprev, S, R, tab, sink, ck2, nb, bb, Eb);
           sink.flush();
         }
       }
@@ -908,57 +1080,111 @@ __global__ __launch_bounds__(kCrcThreads) void inflate_crc_seg_kernel(const uint
 }
 
 // One workgroup per file: each thread folds a contiguous run of the file's
-// segments, then the runs are folded pairwise in a tree.
+// segments, and the file's CRC is the XOR of every run's CRC shifted past
+// the bytes after it, crc(A || B) = x^(8|B|) crc(A) ^ crc(B) applied to all
+// runs at once (no tree of dependent rounds).  x^(2^k) mod P comes from the
+// host (a serial chain of 64 squarings each workgroup once began with).
 constexpr int kFoldThreads = 256;
+struct CrcPowers {
+  uint32_t x2k[64];  // x^(2^k) mod P
+  uint32_t xseg;     // x^(8 kCrcSeg) mod P
+};
 __global__ __launch_bounds__(kFoldThreads) void inflate_crc_fold_kernel(const uint8_t* __restrict__ text,
                                                                         const uint64_t* __restrict__ file_text,
                                                                         const uint64_t* __restrict__ file_len,
                                                                         const uint32_t* __restrict__ seg_first,
                                                                         const uint32_t* __restrict__ seg_crc,
-                                                                        uint32_t n_files, uint32_t* __restrict__ crc_out) {
+                                                                        uint32_t n_files, uint32_t* __restrict__ crc_out,
+                                                                        CrcPowers pw) {
   __shared__ uint32_t x2k[64];
-  __shared__ uint32_t pc[kFoldThreads];
-  __shared__ uint64_t pl[kFoldThreads];
+  __shared__ uint32_t part[kFoldThreads / 64];
   const uint32_t tid = threadIdx.x;
-  if (tid == 0) {  // x^(2^k) mod P
-    uint32_t p = 1u << 30;  // x^1
-    for (int k = 0; k < 64; ++k) {
-      x2k[k] = p;
-      p = crc_mul(p, p);
-    }
-  }
+  if (tid < 64) x2k[tid] = pw.x2k[tid];
   __syncthreads();
   const uint32_t f = blockIdx.x;
   const uint64_t len = file_len[f];
   const uint32_t g0 = seg_first[f], ns = seg_first[f + 1] - g0;
   const uint32_t per = (ns + kFoldThreads - 1) / kFoldThreads;
   const uint32_t a0 = min(ns, tid * per), a1 = min(ns, a0 + per);
-  const uint32_t xseg = crc_x8n(kCrcSeg, x2k);
   uint32_t crc = 0;  // of this thread's run (standard CRC-32; 0 for none)
-  uint64_t bytes = 0;
   for (uint32_t k = a0; k < a1; ++k) {
     const uint64_t bl = min<uint64_t>(kCrcSeg, len - (uint64_t)k * kCrcSeg);
-    crc = crc_mul(bl == kCrcSeg ? xseg : crc_x8n(bl, x2k), crc) ^ seg_crc[g0 + k];
-    bytes += bl;
+    crc = crc_mul(bl == kCrcSeg ? pw.xseg : crc_x8n(bl, x2k), crc) ^ seg_crc[g0 + k];
   }
-  pc[tid] = crc;
-  pl[tid] = bytes;
+  // shifted past the bytes of the runs after it
+  const uint64_t after = a1 < ns ? len - (uint64_t)a1 * kCrcSeg : 0;
+  if (crc && after) crc = crc_mul(crc_x8n(after, x2k), crc);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) crc ^= __shfl_xor(crc, o);
+  if ((tid & 63u) == 0) part[tid >> 6] = crc;
   __syncthreads();
-  for (uint32_t w = 1; w < kFoldThreads; w <<= 1) {  // crc(A || B) = x^(8|B|) crc(A) ^ crc(B)
-    if ((tid & (2 * w - 1)) == 0) {
-      const uint64_t lb = pl[tid + w];
-      pc[tid] = (lb ? crc_mul(crc_x8n(lb, x2k), pc[tid]) : pc[tid]) ^ pc[tid + w];
-      pl[tid] += lb;
-    }
-    __syncthreads();
-  }
   if (tid == 0) {
-    crc_out[f] = pc[0];
+    uint32_t c = 0;
+    for (int w = 0; w < kFoldThreads / 64; ++w) c ^= part[w];
+    crc_out[f] = c;
     crc_out[n_files + f] = len ? text[file_text[f]] : 0u;  // (the caller checks the format: FASTA starts with '>')
   }
 }
 
+// The powers the fold kernel takes, on the host (the same arithmetic).
+uint32_t crc_mul_host(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (uint32_t m = 1u << 31; m; m >>= 1) {
+    if (a & m) p ^= b;
+    b = b & 1 ? (b >> 1) ^ kCrcPoly : b >> 1;
+  }
+  return p;
+}
+const CrcPowers& crc_powers() {
+  static const CrcPowers pw = [] {
+    CrcPowers x{};
+    uint32_t p = 1u << 30;  // x^1
+    for (int k = 0; k < 64; ++k) {
+      x.x2k[k] = p;
+      p = crc_mul_host(p, p);
+    }
+    uint32_t r = 1u << 31;  // x^(8 kCrcSeg): the bits of 8 kCrcSeg
+    uint64_t n = 8ull * kCrcSeg;
+    for (int k = 0; n; ++k, n >>= 1)
+      if (n & 1) r = crc_mul_host(x.x2k[k], r);
+    x.xseg = r;
+    return x;
+  }();
+  return pw;
+}
+
+// A staged batch from its pinned host slot to the device, read by the
+// kernel over PCIe (the host memory is mapped into the device's address
+// space): the bulk of a call's host-to-device bytes goes this way instead of
+// through the DMA engine, where every small copy of the processing lanes (a
+// decode pass's lane table, a parse pass's counts) would wait behind
+// hundreds of MB of queued uploads.  A few workgroups, each thread with four
+// 16-byte loads in flight, keep PCIe busy without taking the CUs.
+constexpr int kUploadThreads = 256, kUploadBlocks = 64;
+__global__ __launch_bounds__(kUploadThreads) void slot_upload_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                                     uint64_t n16) {
+  const uint64_t stride = (uint64_t)gridDim.x * kUploadThreads;
+  uint64_t i = (uint64_t)blockIdx.x * kUploadThreads + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+    dst[i] = a;
+    dst[i + stride] = b;
+    dst[i + 2 * stride] = c;
+    dst[i + 3 * stride] = d;
+  }
+  for (; i < n16; i += stride) dst[i] = src[i];
+}
+
 }  // namespace
+
+hipError_t launch_slot_upload(uint8_t* dst, const uint8_t* src_mapped, uint64_t bytes, hipStream_t st) {
+  const uint64_t n16 = (bytes + 15) / 16;  // (both buffers are padded past bytes to a 16-byte multiple)
+  if (n16 == 0) return hipSuccess;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(kUploadBlocks, (n16 + kUploadThreads - 1) / kUploadThreads);
+  hipLaunchKernelGGL(slot_upload_kernel, dim3(blocks), dim3(kUploadThreads), 0, st, (uint4*)dst, (const uint4*)src_mapped,
+                     n16);
+  return hipGetLastError();
+}
 
 hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st) {
   if (a.n_chunks == 0) return hipSuccess;
@@ -967,9 +1193,13 @@ hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+uint32_t inflate_stage_words() { return kStageWords; }
+
 hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st) {
-  if (a.n_lanes == 0) return hipSuccess;
-  hipLaunchKernelGGL(inflate_decode_kernel, dim3(a.n_lanes), dim3(kSpanLanes), 0, st, a);
+  if (a.n_staged)
+    hipLaunchKernelGGL(inflate_decode_kernel<true>, dim3(a.n_staged), dim3(kSpanLanes), kStageWords * 4, st, a);
+  if (a.n_lanes > a.n_staged)
+    hipLaunchKernelGGL(inflate_decode_kernel<false>, dim3(a.n_lanes - a.n_staged), dim3(kSpanLanes), 0, st, a);
   return hipGetLastError();
 }
 
@@ -992,7 +1222,7 @@ hipError_t launch_inflate_place(const InflatePlace& a, uint64_t text_len, uint8_
   if (e != hipSuccess) return e;
   if (n_files)
     hipLaunchKernelGGL(inflate_crc_fold_kernel, dim3(n_files), dim3(kFoldThreads), 0, st, text, file_text, file_len,
-                       seg_first, seg_crc, n_files, crc);
+                       seg_first, seg_crc, n_files, crc, crc_powers());
   return hipGetLastError();
 }
 

@@ -536,7 +536,8 @@ struct LaneTables {
   // A symbol as a table entry (fast_entry): codes of <= kFastBits bits in
   // one lookup of the next kFastBits stream bits, longer ones by the limits.
   // The entry is consumed from the cursor.
-  GG_HD uint32_t lit_entry(Cursor& cur) {
+  template <class Cur>
+  GG_HD uint32_t lit_entry(Cur& cur) {
     const uint32_t e = s.lfast(cur.peek() & (kFastSize - 1));
     if (e & kFastLenMask) {
       cur.skip((e >> kFastLenShift) & 15u);
@@ -545,7 +546,8 @@ struct LaneTables {
     const int sy = lit(cur);
     return sy < 0 ? kEntryBad : lit_value(sy);
   }
-  GG_HD uint32_t dist_entry(Cursor& cur) {
+  template <class Cur>
+  GG_HD uint32_t dist_entry(Cur& cur) {
     const uint32_t e = s.dfast(cur.peek() & (kFastSize - 1));
     if (e & kFastLenMask) {
       cur.skip((e >> kFastLenShift) & 15u);
@@ -573,7 +575,8 @@ struct LaneTables {
       s.dfast((int)i) = fast_entry(i, true);
     }
   }
-  GG_HD int lit(Cursor& cur) {
+  template <class Cur>
+  GG_HD int lit(Cur& cur) {
     const uint32_t x = rev15(cur.peek());
     int L = 1;
 #pragma unroll
@@ -582,7 +585,8 @@ struct LaneTables {
     cur.skip((uint32_t)L);
     return s.lsym(s.lbase(L) + (int)(x >> (kMaxBits - L)));
   }
-  GG_HD int dist(Cursor& cur) {
+  template <class Cur>
+  GG_HD int dist(Cur& cur) {
     const uint32_t x = rev15(cur.peek());
     int L = 1;
 #pragma unroll

@@ -211,6 +211,12 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
       if (lanes[l].alive && lanes[l].redo) redo.push_back(l);
     const uint32_t nl = (uint32_t)redo.size();
     if (nl == 0) break;
+    // the lanes whose segment fits the staged (LDS) decode first
+    auto fits = [&](uint32_t l) {
+      const Lane& x = lanes[l];
+      return inflate_segment_words(x.start, x.end == ~0ull ? fbits[x.file] : x.end) <= inflate_stage_words();
+    };
+    const uint32_t n_staged = (uint32_t)(std::stable_partition(redo.begin(), redo.end(), fits) - redo.begin());
     if (pass >= kMaxRelaunch) return hand_back("block starts did not chain", 0);  // (ok = false)
     // the lanes to decode: 6 arrays of nl u64 (file, start, end, tok_off, cap, scr_off)
     std::vector<uint64_t> arg((size_t)nl * 6);
@@ -241,6 +247,7 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     d.lane_start = d_arg + nl;
     d.lane_end = d_arg + 2 * (size_t)nl;
     d.n_lanes = nl;
+    d.n_staged = n_staged;
     d.tok = d_tok;
     d.tok_off = d_arg + 3 * (size_t)nl;
     d.tok_cap = d_arg + 4 * (size_t)nl;

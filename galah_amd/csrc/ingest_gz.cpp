@@ -12,8 +12,8 @@
 // processes batch N, a helper thread stages batch N + 1 into the lane's
 // other pinned slot -- its pool of threads claims files one at a time from
 // the call's shared list (GzClaims), reads each straight into its place in
-// the slot (pread: no intermediate copy) and queues it to the slot's device
-// buffer.  A batch is cut at its size limits (the first batches of a call
+// the slot (pread: no intermediate copy), and the batch goes to the slot's
+// device buffer by a kernel reading the mapped slot over PCIe.  A batch is cut at its size limits (the first batches of a call
 // smaller, so the GPU starts sooner); a claimed file that does not fit is
 // given back and claimed again first.
 //
@@ -280,7 +280,8 @@ class GzStager {
         if (sl.host) (void)hipHostFree(sl.host);
         sl.host = nullptr;
         sl.host_cap = 0;
-        if (!hip(hipHostMalloc((void**)&sl.host, cap, hipHostMallocDefault), "hipHostMalloc")) return false;
+        if (!hip(hipHostMalloc((void**)&sl.host, cap, hipHostMallocMapped), "hipHostMalloc")) return false;
+        if (!hip(hipHostGetDevicePointer((void**)&sl.host_dev, sl.host, 0), "hipHostGetDevicePointer")) return false;
         sl.host_cap = cap;
       }
       if (cap > sl.dev_cap) {
@@ -358,20 +359,20 @@ class GzStager {
         } else {
           ok = pread_all(pr.fd, sl.host + p, len, 0);
         }
-        const hipError_t e = ok && len ? hipMemcpyAsync(sl.dev + p, sl.host + p, len, hipMemcpyHostToDevice, sl.st)
-                                       : hipSuccess;
-        std::lock_guard<std::mutex> lk(bm);
         if (!ok) {
+          std::lock_guard<std::mutex> lk(bm);
           cl_.file_error(i, GG_ERR_IO, std::string("read error in ") + cl_.paths[i]);
           g.file_err = true;
         }
-        hip(e, "hipMemcpyAsync");
       }
     };
     std::vector<std::thread> th;
     for (int t = 1; t < threads_; ++t) th.emplace_back(worker);
     worker();
     for (auto& x : th) x.join();
+    // the batch to the device by a kernel reading the mapped slot (inflate.hip
+    // launch_slot_upload): no DMA-engine queue for the lanes' small copies to wait behind
+    if (g.st == GG_OK && !g.file_err && g.at) hip(launch_slot_upload(sl.dev, sl.host_dev, g.at, sl.st), "slot upload");
     g.ms = ms_since(g.t0);
     return !g.idx.empty() || g.st != GG_OK || g.file_err;
   }
@@ -526,7 +527,12 @@ gg_status gz_member_ingest(gg_ctx* m, GzClaims& cl, uint64_t* d_sk, uint32_t* d_
   for (int l = 1; l < L; ++l) th.emplace_back(lane, l);
   lane(0);
   for (auto& t : th) t.join();
-  for (int l = 1; l < L; ++l) {  // the helpers' counts are the member's
+  for (int l = 1; l < L; ++l) {  // the member's stream waits for the helpers' work; their counts are the member's
+    if (st[l] == GG_OK && st[0] == GG_OK) {
+      if (!lanes[l]->copy_done) GG_HIP(m, hipEventCreateWithFlags(&lanes[l]->copy_done, hipEventDisableTiming));
+      GG_HIP(m, hipEventRecord(lanes[l]->copy_done, lanes[l]->stream));
+      GG_HIP(m, hipStreamWaitEvent(m->stream, lanes[l]->copy_done, 0));
+    }
     for (int k = 0; k < GG_FALLBACK_COUNT; ++k) {
       m->fallbacks[k] += lanes[l]->fallbacks[k];
       lanes[l]->fallbacks[k] = 0;

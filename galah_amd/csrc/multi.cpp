@@ -133,6 +133,10 @@ gg_status replicate(gg_ctx* m, size_t mi, const std::vector<gg_ctx*>& ms, const 
       m->rep_live[sp.owner] = 1;
     }
     const gg_ctx* o = ms[sp.owner];
+    if (m->rep_live[sp.owner] == 1 && o->rows_ready) {  // (the owner's rows are final on its device)
+      GG_HIP(m, hipStreamWaitEvent(ps, o->rows_ready, 0));
+      m->rep_live[sp.owner] = 2;
+    }
     uint64_t* dsk = rows[mi].sk + (size_t)sp.row0 * s;
     const uint64_t* ssk = rows[sp.owner].sk + (size_t)sp.row0 * s;
     uint32_t* dl = rows[mi].len + sp.row0;
@@ -548,7 +552,10 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
                                hipMemcpyHostToDevice, m->stream));
     }
     GG_HIP(m, hipStreamSynchronize(m->stream));
-    if (gz_dev) return gz_member_ingest(m, claims, r.sk, r.len, copy_threads, owned[mi]);
+    if (gz_dev) {
+      const gg_status gs = gz_member_ingest(m, claims, r.sk, r.len, copy_threads, owned[mi]);
+      return gs != GG_OK ? gs : mark_rows_ready(m);
+    }
     PackStream& stream = *streamp;
     std::vector<gg_run> runs;
     std::vector<uint32_t> row_of;
@@ -666,7 +673,7 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
         }
       }
     }
-    return GG_OK;
+    return mark_rows_ready(m);
   };
   gg_status st = on_members(c, ms, [&](size_t mi, gg_ctx* m) -> gg_status {
     const gg_status r = body(mi, m);
@@ -720,6 +727,12 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
 
 // Direct access from device a to device b's memory: true when a == b (a
 // device always reaches its own memory) or when the peer link is enabled.
+// (GALAHGPU_TEST_NO_PEER=1, tests: every pair of distinct members reports
+// no peer access, so one GPU runs the host-staged branch of replicate.)
+bool test_no_peer() {
+  const char* e = getenv("GALAHGPU_TEST_NO_PEER");
+  return e && *e == '1';
+}
 bool enable_peer(int a, int b) {
   if (a == b) return true;
   int can = 0;
@@ -820,7 +833,8 @@ gg_ctx* gg_create_multi(int kmer_length, uint32_t sketch_size, uint64_t hash_see
   const size_t M = list.size();
   c->peer_direct.assign(M * M, 0);
   for (size_t a = 0; a < M; ++a)
-    for (size_t b = 0; b < M; ++b) c->peer_direct[a * M + b] = enable_peer(list[a], list[b]) ? 1 : 0;
+    for (size_t b = 0; b < M; ++b)
+      c->peer_direct[a * M + b] = (a == b || !test_no_peer()) && enable_peer(list[a], list[b]) ? 1 : 0;
   (void)hipSetDevice(list[0]);
   *status = GG_OK;
   return c;
@@ -1019,8 +1033,9 @@ gg_status gg_precluster_shards(gg_ctx* ctx, const gg_shard* shards, float min_an
     const gg_shard& sh = shards[mi];
     if (sh.n_genomes == 0) return GG_OK;
     // K1 writes the shard's rows at their global offset
-    return sketch_core(m, sh.d_words, sh.n_words, sh.runs, sh.n_runs, sh.n_genomes,
-                       rows[mi].sk + (size_t)off[mi] * m->s, rows[mi].len + off[mi], nullptr, m->stream);
+    const gg_status ks = sketch_core(m, sh.d_words, sh.n_words, sh.runs, sh.n_runs, sh.n_genomes,
+                                     rows[mi].sk + (size_t)off[mi] * m->s, rows[mi].len + off[mi], nullptr, m->stream);
+    return ks != GG_OK ? ks : mark_rows_ready(m);
   });
   if (st != GG_OK) return st;
   ctx->phase_ms[GG_PHASE_SKETCH] = ms_since(t0);

@@ -50,6 +50,27 @@ def test_precluster_files_same_for_1_2_3_devices(golden):
             assert "host-staged peer copies 0 (links without peer access 0)" in line
 
 
+@pytest.mark.parametrize("devs", [[0], [0, 0], [0, 0, 0], [0] * 5])
+def test_precluster_files_without_peer_access(golden, monkeypatch, devs):
+    """GALAHGPU_TEST_NO_PEER=1 makes every pair of distinct members report no
+    peer access (as two GPUs without an xGMI link would): the replication
+    takes its host-staged branch (counted in gg_fallbacks) and waits on the
+    owners' rows-ready events; pairs and ANI are unchanged."""
+    monkeypatch.setenv("GALAHGPU_TEST_NO_PEER", "1")
+    min_ani = ga.parse_percentage(90)
+    exp = expected_pairs_from_table(golden, min_ani)
+    M = len(devs)
+    with ga.Context(k=21, sketch_size=1000, devices=devs) as ctx:
+        pairs, ani = ctx.precluster_files(golden["paths"], min_ani)
+        assert as_tuples(pairs) == exp
+        for r, a in zip(pairs, ani):
+            assert a == np.float32(oracle.ani(int(r["common"]), int(r["total"])))
+        assert (ctx.peer_links() == np.eye(M, dtype=int)).all()
+        fb = ctx.fallbacks()
+        assert (fb["peer_staged"] > 0) == (M > 1), fb
+        assert "links without peer access %d" % (M * M - M if M > 1 else 0) in ctx.info_line()
+
+
 def test_sketch_and_pairs_host_buffers_multi(golden):
     pk = ga.pack_files(golden["paths"])
     for devs in LISTS[1:]:
