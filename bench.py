@@ -55,6 +55,8 @@ ISSUE_MODEL = os.path.join(ROOT, "profiles", "r04_k1_issue_model.json")
 # VALU issue share, LDS-array utilisation) of the bucketed inverted index:
 # scripts/k2_pmc.sh + scripts/k2_pmc_model.py
 K2_PMC = os.path.join(ROOT, "profiles", "r04_k2_pmc.json")
+# the device-inflate ingest kernels' counters at C2 (scripts/ingest_pmc.sh + ingest_pmc_model.py)
+INGEST_PMC = os.path.join(ROOT, "profiles", "r05_ingest_pmc.json")
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 from host_cpus import host_cpu_info  # noqa: E402
 
@@ -373,6 +375,70 @@ def cpu_baseline(sample_words, glen, sk_all, lens_all, k, s, min_ani, n_total, b
 # ---------------------------------------------------------------------------
 # ingest-inclusive leg: real gzip FASTA files through gg_precluster_files
 # ---------------------------------------------------------------------------
+def roofline_ingest(ks, wall_s, gz_bytes, text_bytes):
+    """The device-inflate ingest priced kernel by kernel:
+    HIP-event ms per call of each kernel class on the stream it ran on (one
+    call with one processing lane, so no kernel shares the GPU with
+    another), its algorithmic bytes against 8 TB/s HBM, and the PMC pass's
+    VALU issue share and HBM bytes (profiles/r05_ingest_pmc.json, the same
+    C2 workload).  Algorithmic bytes per call (G = gzip bytes, X = text
+    bytes, T = tokens the decode wrote):
+      upload  G (host -> device, over PCIe: priced against the HBM peak too)
+      search  G read once
+      decode  G read + 4 T (tokens written)
+      expand  4 T read + 5 X (val u32 + the text byte per text byte)
+      resolve 2 X (the text read and rewritten)
+      crc     X
+      parse   3.25 X (three passes over the text, X / 4 of packed words)"""
+    G, X = float(gz_bytes), float(text_bytes)
+    T = float(ks["decode"]["work"]) if ks.get("decode") else 0.0
+    alg = {"upload": G, "search": G, "decode": G + 4 * T, "expand": 4 * T + 5 * X, "resolve": 2 * X, "crc": X,
+           "parse": 3.25 * X}
+    pmc = {}
+    if os.path.exists(INGEST_PMC):
+        with open(INGEST_PMC) as f:
+            pk = json.load(f)["kernels"]
+        merge = {"decode": ("decode_staged", "decode_global")}
+        for name in alg:
+            parts = merge.get(name, (name,))
+            rows = [pk[p] for p in parts if p in pk]
+            if not rows:
+                continue
+            ms = sum(r["ms_per_call"] for r in rows)
+            hb = sum(r.get("hbm_bytes_per_call", 0.0) for r in rows)
+            valu = sum(r["valu_frac_guide"] * r["ms_per_call"] for r in rows) / ms if ms else 0.0
+            pmc[name] = {"ms_per_call": round(ms, 4), "valu_frac_guide": round(valu, 4),
+                         "hbm_bytes_per_call": round(hb), "hbm_frac": round(hb / (ms * 1e-3) / 8e12, 4) if ms else 0.0,
+                         "wait_frac": round(max(r["wait_frac"] for r in rows), 3)}
+    kern = {}
+    tot_ms = tot_alg = 0.0
+    for name, b in alg.items():
+        k = ks.get(name)
+        if not k or not k["launches"]:
+            continue
+        ms = k["ms"]
+        e = {"ms_per_call": round(ms, 4), "launches": k["launches"], "algorithmic_bytes": round(b),
+             "achieved_GBps": round(b / (ms * 1e-3) / 1e9, 2), "peak_GBps": 8000.0,
+             "frac": round(b / (ms * 1e-3) / 8e12, 5)}
+        if name in pmc:
+            e["pmc"] = pmc[name]
+        kern[name] = e
+        tot_ms += ms
+        tot_alg += b
+    dom = max(kern, key=lambda x: kern[x]["ms_per_call"]) if kern else None
+    traffic = sum(v.get("pmc", {}).get("hbm_bytes_per_call", 0) for v in kern.values()) or None
+    return {"bound": "hbm", "unit": "GB/s", "peak": 8000.0,
+            "achieved": round(tot_alg / (tot_ms * 1e-3) / 1e9, 2) if tot_ms else None,
+            "frac": round(tot_alg / (tot_ms * 1e-3) / 8e12, 5) if tot_ms else None, "traffic": traffic,
+            "kernels_ms_per_call": round(tot_ms, 3), "call_s_one_lane": round(wall_s, 4), "dominant": dom,
+            "kernels": kern,
+            "note": "achieved = the ingest kernels' algorithmic bytes per call (docstring of bench.py "
+                    "roofline_ingest) / their summed HIP-event time on their own streams, one call with one lane "
+                    "(GALAHGPU_GZ_LANES=1); the default two lanes overlap these kernels; pmc: "
+                    "profiles/r05_ingest_pmc.json (valu_frac_guide = VALU wave-instructions / (1024 SIMDs x "
+                    "cycles / 2), hbm_bytes = FETCH_SIZE x 2 + WRITE_SIZE)"}
+
+
 def files_leg(a, device, steps):
     """C2's genomes (1k x 3 Mbp, clusters of 10) written as gzip FASTA (80
     columns, level 6) to local disk OUTSIDE the timed region, then
@@ -440,6 +506,19 @@ def files_leg(a, device, steps):
                         for p, v in ctx.phase_times().items():
                             ph[p] += v
                     fb = ctx.fallbacks()["inflate_host"]
+                    if inflate == "device":  # one more call, timed kernel by kernel (one lane: no overlap)
+                        os.environ["GALAHGPU_GZ_LANES"] = "1"
+                        try:
+                            ctx.timing_enable(True)
+                            t1 = time.perf_counter()
+                            ctx.precluster_files(paths, thr)
+                            w1 = time.perf_counter() - t1
+                            kst = {name: ctx.timing_read(k) for name, k in ga.INGEST_KERNELS.items()}
+                            kst["k1"] = ctx.timing_read(ga.KERNEL_SKETCH)
+                            ctx.timing_enable(False)
+                        finally:
+                            os.environ.pop("GALAHGPU_GZ_LANES", None)
+                        ingest[:] = [kst, w1]
             finally:
                 os.environ.pop("GALAHGPU_INFLATE", None)
             t = float(np.median(times))
@@ -449,8 +528,12 @@ def files_leg(a, device, steps):
                     "inflate_host_batches": fb}, pairs
 
         # the default path for gzip files: inflated on the GPU (inflate.hip), the host threads only read
+        ingest = []
         dev, dp = timed("device")
         out.update(dev)
+        if ingest:
+            text_bytes = sum(len(b">genome_%d synthetic C2\n" % g) for g in range(n)) + n * (glen + glen // 80)
+            out["roofline_ingest"] = roofline_ingest(ingest[0], ingest[1], out["gz_bytes"], text_bytes)
         out["inflate"] = "device"
         t = dev["s_per_call_median"]
         # the same files gunzipped and packed on the host threads (GALAHGPU_INFLATE=host, round 3's path)

@@ -161,6 +161,12 @@ _sig("gg_info_line", _i32, [_vp, ctypes.c_char_p, ctypes.c_size_t])
 FALLBACKS = ("index_to_gate", "index_full_sort", "peer_staged", "sketch_retry", "inflate_host")  # gg_fallbacks order
 _sig("gg_timing_read", _i32, [_vp, _i32, ctypes.POINTER(_KStats)])
 KERNEL_SKETCH, KERNEL_FINALIZE, KERNEL_PAIRS, KERNEL_PAIRS_INDEX = 0, 1, 2, 3
+# the device-inflate ingest's kernels (gzip lists through precluster_files / sketch_files)
+(KERNEL_INFLATE_SEARCH, KERNEL_INFLATE_DECODE, KERNEL_INFLATE_EXPAND, KERNEL_INFLATE_RESOLVE, KERNEL_INFLATE_CRC,
+ KERNEL_PARSE, KERNEL_UPLOAD) = range(4, 11)
+INGEST_KERNELS = {"search": KERNEL_INFLATE_SEARCH, "decode": KERNEL_INFLATE_DECODE, "expand": KERNEL_INFLATE_EXPAND,
+                  "resolve": KERNEL_INFLATE_RESOLVE, "crc": KERNEL_INFLATE_CRC, "parse": KERNEL_PARSE,
+                  "upload": KERNEL_UPLOAD}
 
 
 def lib():

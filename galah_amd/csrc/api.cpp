@@ -102,8 +102,6 @@ hipError_t pinned(gg_ctx* c, size_t bytes, void** out) {
   return hipSuccess;
 }
 
-namespace {
-
 hipEvent_t take_event(gg_ctx* c) {
   if (!c->spare_events.empty()) {
     hipEvent_t e = c->spare_events.back();
@@ -115,22 +113,7 @@ hipEvent_t take_event(gg_ctx* c) {
   return e;
 }
 
-// Runs `launch` (which enqueues one kernel on st); when timing is enabled
-// brackets it with events recorded on the same stream.
-template <typename F>
-hipError_t timed_launch(gg_ctx* c, int kernel, uint64_t work, hipStream_t st, F&& launch) {
-  if (!c->timing) return launch();
-  hipEvent_t a = take_event(c), b = take_event(c);
-  if (!a || !b) return hipErrorOutOfMemory;
-  hipError_t e = hipEventRecord(a, st);
-  if (e != hipSuccess) return e;
-  e = launch();
-  if (e != hipSuccess) return e;
-  e = hipEventRecord(b, st);
-  if (e != hipSuccess) return e;
-  c->timed.push_back(gg_ctx::Timed{kernel, a, b, work});
-  return hipSuccess;
-}
+namespace {
 
 // Number of pairs (i < j < n) in tiles [tb, te).
 uint64_t pairs_in_tiles(uint32_t n, uint64_t tb, uint64_t te) {

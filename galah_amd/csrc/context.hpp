@@ -236,6 +236,25 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
 gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<uint64_t>& foff, uint32_t** d_words,
                           uint64_t* n_words, std::vector<gg_run>& runs);
 
+// A timing event of c (a spare one, else a new one; nullptr on failure).
+hipEvent_t take_event(gg_ctx* c);
+// Runs `launch` (which enqueues one kernel on st); when timing is enabled
+// brackets it with events recorded on the same stream (gg_timing_read).
+template <typename F>
+hipError_t timed_launch(gg_ctx* c, int kernel, uint64_t work, hipStream_t st, F&& launch) {
+  if (!c->timing) return launch();
+  hipEvent_t a = take_event(c), b = take_event(c);
+  if (!a || !b) return hipErrorOutOfMemory;
+  hipError_t e = hipEventRecord(a, st);
+  if (e != hipSuccess) return e;
+  e = launch();
+  if (e != hipSuccess) return e;
+  e = hipEventRecord(b, st);
+  if (e != hipSuccess) return e;
+  c->timed.push_back(gg_ctx::Timed{kernel, a, b, work});
+  return hipSuccess;
+}
+
 // Records m->rows_ready on m->stream (after the member's sketching).
 gg_status mark_rows_ready(gg_ctx* m);
 

@@ -313,13 +313,16 @@ hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st);
 // kernel on st (inflate.hip); both buffers hold a multiple of 16 bytes
 hipError_t launch_slot_upload(uint8_t* dst, const uint8_t* src_mapped, uint64_t bytes, hipStream_t st);
 hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st);
-// expand + resolve (text[0, text_len); val is read only where the expand wrote it) + CRC-32 per file
-// (file f's 4 KB segments are seg_first[f] .. seg_first[f + 1] - 1; crc
-// receives n_files CRCs, then each file's first byte)
+// the text of a batch: expand (every lane's tokens into text + val), then
+// resolve (text[0, text_len); val is read only where the expand wrote it)
+hipError_t launch_inflate_expand(const InflatePlace& a, hipStream_t st);
+hipError_t launch_inflate_resolve(const InflatePlace& a, uint64_t text_len, hipStream_t st);
+// CRC-32 per file (file f's 4 KB segments are seg_first[f] .. seg_first[f +
+// 1] - 1; crc receives n_files CRCs, then each file's first byte)
 constexpr uint32_t kInflateCrcSeg = 4096;
-hipError_t launch_inflate_place(const InflatePlace& a, uint64_t text_len, uint8_t* text, uint32_t n_files,
-                                const uint64_t* file_text, const uint64_t* file_len, const uint32_t* seg_first,
-                                uint32_t n_segs, uint32_t* seg_crc, uint32_t* crc, hipStream_t st);
+hipError_t launch_inflate_crc(const uint8_t* text, uint32_t n_files, const uint64_t* file_text, const uint64_t* file_len,
+                              const uint32_t* seg_first, uint32_t n_segs, uint32_t* seg_crc, uint32_t* crc,
+                              hipStream_t st);
 
 struct IndexBuild {
   const uint64_t* sketches;

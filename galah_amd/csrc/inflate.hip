@@ -1203,22 +1203,26 @@ hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_inflate_place(const InflatePlace& a, uint64_t text_len, uint8_t* text, uint32_t n_files,
-                                const uint64_t* file_text, const uint64_t* file_len, const uint32_t* seg_first,
-                                uint32_t n_segs, uint32_t* seg_crc, uint32_t* crc, hipStream_t st) {
+hipError_t launch_inflate_expand(const InflatePlace& a, hipStream_t st) {
   if (a.n_lanes) hipLaunchKernelGGL(inflate_expand_kernel, dim3(a.n_lanes), dim3(kExpandThreads), 0, st, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+hipError_t launch_inflate_resolve(const InflatePlace& a, uint64_t text_len, hipStream_t st) {
   const uint64_t groups = (text_len + 15) / 16;
   if (groups)
     hipLaunchKernelGGL(inflate_resolve_kernel, dim3((uint32_t)std::min<uint64_t>(65536, (groups + 255) / 256)),
                        dim3(256), 0, st, a.val, a.text, text_len, a.flags);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  return hipGetLastError();
+}
+
+hipError_t launch_inflate_crc(const uint8_t* text, uint32_t n_files, const uint64_t* file_text, const uint64_t* file_len,
+                              const uint32_t* seg_first, uint32_t n_segs, uint32_t* seg_crc, uint32_t* crc,
+                              hipStream_t st) {
   if (n_segs)
     hipLaunchKernelGGL(inflate_crc_seg_kernel, dim3((n_segs + kCrcThreads - 1) / kCrcThreads), dim3(kCrcThreads), 0,
                        st, text, file_text, file_len, seg_first, n_files, n_segs, seg_crc);
-  e = hipGetLastError();
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (n_files)
     hipLaunchKernelGGL(inflate_crc_fold_kernel, dim3(n_files), dim3(kFoldThreads), 0, st, text, file_text, file_len,

@@ -151,7 +151,9 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
       GG_HIP(m, hipMemsetAsync(d_sprof, 0, 8 * sizeof(uint64_t), st));
       s.prof = d_sprof;
     }
-    GG_HIP(m, launch_inflate_search(s, st));
+    uint64_t gz_in = 0;
+    for (uint32_t f = 0; f < nf; ++f) gz_in += files[f].gz ? files[f].data_len : 0;
+    GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_SEARCH, gz_in, st, [&] { return launch_inflate_search(s, st); }));
     if (d_sprof) {
       uint64_t pr[8];
       GG_HIP(m, hipStreamSynchronize(st));
@@ -264,7 +266,8 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
       GG_HIP(m, hipMemsetAsync(d_prof, 0, 8 * sizeof(uint64_t), st));
       d.prof = d_prof;
     }
-    GG_HIP(m, launch_inflate_decode(d, st));
+    const size_t timed_at = m->timed.size();
+    GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_DECODE, 0, st, [&] { return launch_inflate_decode(d, st); }));
     if (d_prof) {
       uint64_t pr[8];
       GG_HIP(m, hipStreamSynchronize(st));
@@ -279,6 +282,11 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     GG_HIP(m, hipStreamSynchronize(st));
     stamp("decode pass");
     const uint32_t* r32 = (const uint32_t*)(res.data() + 3 * (size_t)nl);
+    if (timed_at < m->timed.size()) {  // (timing: the work of a decode pass is the tokens its lanes wrote)
+      uint64_t toks_out = 0;
+      for (uint32_t k = 0; k < nl; ++k) toks_out += res[k];
+      m->timed[timed_at].work = toks_out;
+    }
     for (uint32_t k = 0; k < nl; ++k) {
       Lane& x = lanes[redo[k]];
       x.n_tok = x.done_tok + res[k];
@@ -397,7 +405,12 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
   GG_HIP(m, scratch_t(m, "gz_sfirst", nf + 1, &d_sfirst));
   GG_HIP(m, scratch_t(m, "gz_scrc", std::max(nseg, 1u), &d_scrc));
   GG_HIP(m, hipMemcpyAsync(d_sfirst, seg_first.data(), (nf + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-  GG_HIP(m, launch_inflate_place(p, text_len, *d_text, nf, d_ftext, d_flen, d_sfirst, nseg, d_scrc, d_crc, st));
+  GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_EXPAND, text_len, st, [&] { return launch_inflate_expand(p, st); }));
+  GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_RESOLVE, text_len, st,
+                         [&] { return launch_inflate_resolve(p, text_len, st); }));
+  GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_CRC, text_len, st, [&] {
+    return launch_inflate_crc(*d_text, nf, d_ftext, d_flen, d_sfirst, nseg, d_scrc, d_crc, st);
+  }));
   // plain files (not gzip) go into their place as they are
   for (uint32_t f = 0; f < nf; ++f)
     if (!files[f].gz && files[f].data_len)

@@ -104,14 +104,12 @@ uint64_t gz_batch_bytes() {
   return v;
 }
 uint64_t gz_batch_text() { return std::min<uint64_t>(3 * gz_batch_bytes(), 960ull << 20); }  // (text < 1 GiB)
-// processing lanes per device (GALAHGPU_GZ_LANES, 1..4; tuning only)
+// processing lanes per device (GALAHGPU_GZ_LANES, 1..4, read per call;
+// tuning and per-kernel timing without overlap: no result depends on it)
 int gz_lanes() {
-  static const int v = [] {
-    const char* e = getenv("GALAHGPU_GZ_LANES");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 ? std::min(x, 4) : 2;
-  }();
-  return v;
+  const char* e = getenv("GALAHGPU_GZ_LANES");
+  const int x = e ? atoi(e) : 0;
+  return x > 0 ? std::min(x, 4) : 2;
 }
 // reading threads per stager (GALAHGPU_GZ_COPY_THREADS; tuning only)
 int gz_stage_threads(int host_threads, int lanes) {
@@ -215,6 +213,7 @@ struct GzStaged {
   std::string err;
   double ms = 0;
   Clock::time_point t0;
+  hipEvent_t up_a = nullptr, up_b = nullptr;  // (timing: the upload kernel)
 };
 
 // One lane's stager: two slots (pinned host + device buffers and an upload
@@ -372,7 +371,15 @@ class GzStager {
     for (auto& x : th) x.join();
     // the batch to the device by a kernel reading the mapped slot (inflate.hip
     // launch_slot_upload): no DMA-engine queue for the lanes' small copies to wait behind
-    if (g.st == GG_OK && !g.file_err && g.at) hip(launch_slot_upload(sl.dev, sl.host_dev, g.at, sl.st), "slot upload");
+    if (g.st == GG_OK && !g.file_err && g.at) {
+      if (m_->timing && !g.up_a) {  // (events of the consuming lane's timing, gg_timing_read)
+        hip(hipEventCreate(&g.up_a), "hipEventCreate");
+        hip(hipEventCreate(&g.up_b), "hipEventCreate");
+      }
+      if (g.up_a) hip(hipEventRecord(g.up_a, sl.st), "hipEventRecord");
+      hip(launch_slot_upload(sl.dev, sl.host_dev, g.at, sl.st), "slot upload");
+      if (g.up_b) hip(hipEventRecord(g.up_b, sl.st), "hipEventRecord");
+    }
     g.ms = ms_since(g.t0);
     return !g.idx.empty() || g.st != GG_OK || g.file_err;
   }
@@ -393,6 +400,10 @@ gg_status inflate_staged_batch(gg_ctx* m, GzStager& pipe, GzStaged& g, GzClaims&
   const auto t0 = Clock::now();
   if (g.st != GG_OK) return fail(m, g.st, g.err);
   if (g.file_err) return fail(m, GG_ERR_IO, "a file did not read");  // (the call reports the file's own error)
+  if (g.up_a) {  // (the stager's upload, timed: the lane's events from here on)
+    m->timed.push_back(gg_ctx::Timed{GG_KERNEL_UPLOAD, g.up_a, g.up_b, g.at});
+    g.up_a = g.up_b = nullptr;
+  }
   // the stream waits for the batch's copies (queued on the slot's stream)
   if (!m->copy_done) GG_HIP(m, hipEventCreateWithFlags(&m->copy_done, hipEventDisableTiming));
   GG_HIP(m, hipEventRecord(m->copy_done, pipe.up_stream()));
@@ -514,6 +525,7 @@ gg_status gz_member_ingest(gg_ctx* m, GzClaims& cl, uint64_t* d_sk, uint32_t* d_
       return fail(m, GG_ERR_HIP, "helper stream creation failed");
     }
   }
+  for (int l = 1; l < L; ++l) lanes[l]->timing = m->timing;
   const int per = std::max(1, host_threads / L);
   const int stage_threads = gz_stage_threads(host_threads, L);
   std::mutex owned_mu;
@@ -539,6 +551,8 @@ gg_status gz_member_ingest(gg_ctx* m, GzClaims& cl, uint64_t* d_sk, uint32_t* d_
     }
     m->inflate_dev_batches += lanes[l]->inflate_dev_batches;
     lanes[l]->inflate_dev_batches = 0;
+    m->timed.insert(m->timed.end(), lanes[l]->timed.begin(), lanes[l]->timed.end());  // (the events are m's now)
+    lanes[l]->timed.clear();
   }
   for (int l = 0; l < L; ++l)
     if (st[l] != GG_OK) {

@@ -380,7 +380,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   std::vector<uint64_t> fbases(nf, 0), gofs(nf + 1, 0);
   uint64_t n_starts = 0;
   if (nb) {
-    GG_HIP(m, parse_batch_pass(1, p, st));
+    GG_HIP(m, timed_launch(m, GG_KERNEL_PARSE, foff[nf], st, [&] { return parse_batch_pass(1, p, st); }));
     GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_nl, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
     stamp("pass 1");
@@ -392,7 +392,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
     }
     GG_HIP(m, hipMemcpyAsync((void*)p.pre_nl, h.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     // pass 2 -> bases, run starts (as if no base before), first byte a base?, last non-dropped byte
-    GG_HIP(m, parse_batch_pass(2, p, st));
+    GG_HIP(m, timed_launch(m, GG_KERNEL_PARSE, 0, st, [&] { return parse_batch_pass(2, p, st); }));
     GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_bases, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipMemcpyAsync(h2.data(), p.blk_last, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipMemcpyAsync(hr.data(), p.blk_runs, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
@@ -441,7 +441,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   std::vector<uint64_t> hs(n_starts);
   if (nb) {
     if (*n_words) GG_HIP(m, hipMemsetAsync(*d_words, 0, *n_words * sizeof(uint32_t), st));
-    GG_HIP(m, parse_batch_pass(3, p, st));
+    GG_HIP(m, timed_launch(m, GG_KERNEL_PARSE, 0, st, [&] { return parse_batch_pass(3, p, st); }));
     if (n_starts) GG_HIP(m, hipMemcpyAsync(hs.data(), starts, n_starts * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
     stamp("pass 3");

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 5u
+#define GG_ABI_VERSION 6u
 
 typedef enum gg_status {
   GG_OK = 0,
@@ -315,9 +315,16 @@ void gg_free(void* p);
  * GG_KERNEL_SKETCH, genomes for GG_KERNEL_FINALIZE, evaluated pairs for
  * GG_KERNEL_PAIRS; GG_KERNEL_PAIRS_INDEX is the inverted-index pair kernel's
  * sort and run pass, whose pair pass counts under GG_KERNEL_PAIRS) since the
- * last gg_timing_enable. */
+ * last gg_timing_enable.  The device-inflate ingest of gg_precluster_files /
+ * gg_sketch_files (gzip lists) times its kernels too, every lane of every
+ * member: the block-start search (work: compressed bytes of the batch), the
+ * sub-span decode (tokens written), the expand and the resolve (text bytes),
+ * the CRC-32 (text bytes), the three parse passes (text bytes, counted on
+ * the first) and the PCIe upload of each staged batch (bytes). */
 enum { GG_KERNEL_SKETCH = 0, GG_KERNEL_FINALIZE = 1, GG_KERNEL_PAIRS = 2, GG_KERNEL_PAIRS_INDEX = 3,
-       GG_KERNEL_COUNT = 4 };
+       GG_KERNEL_INFLATE_SEARCH = 4, GG_KERNEL_INFLATE_DECODE = 5, GG_KERNEL_INFLATE_EXPAND = 6,
+       GG_KERNEL_INFLATE_RESOLVE = 7, GG_KERNEL_INFLATE_CRC = 8, GG_KERNEL_PARSE = 9, GG_KERNEL_UPLOAD = 10,
+       GG_KERNEL_COUNT = 11 };
 typedef struct gg_kernel_stats {
   double ms;
   uint64_t launches;
