@@ -268,15 +268,12 @@ struct InflateDecode {
   uint64_t* out_len;           // [n_lanes] bytes the lane's tokens stand for
   uint64_t* last_end;          // [n_lanes] bit after the lane's last block
   uint32_t* bfinal;            // [n_lanes] the lane decoded the stream's last block
-  // lanes [0, n_staged) take the staged kernel (the segment's compressed
-  // words copied into LDS first; every stream read of the decode is an LDS
-  // read): those whose words fit inflate_stage_words(); the rest read global
-  // memory
+  // lanes [0, n_staged) take the staged kernel (the compressed words copied
+  // into LDS window by window; every stream read of the decode is an LDS
+  // read), the rest read global memory
   uint32_t n_staged = 0;
 };
-// A segment (start .. end bits of its file) fits the staged decode when
-// these words hold it (the words its bits touch + the readers' look-ahead).
-uint32_t inflate_stage_words();
+// The words from start_bit to end_bit touch, + the readers' look-ahead.
 __host__ __device__ inline uint64_t inflate_segment_words(uint64_t start_bit, uint64_t end_bit) { return (end_bit + 31) / 32 - start_bit / 32 + 8; }
 struct InflatePlace {
   const uint32_t* tok;

@@ -90,7 +90,7 @@ __device__ __forceinline__ uint64_t quick64(const uint32_t (&A)[5], const uint8_
 // (block_header_ok, one candidate per lane) run when the list is full or
 // the chunk is done, so a step waits on no header walk; the first
 // candidate that passes is the chunk's start.
-__global__ __launch_bounds__(64 * kSearchWaves) void inflate_search_kernel(InflateSearch a) {
+__global__ __launch_bounds__(64 * kSearchWaves, 4) void inflate_search_kernel(InflateSearch a) {
   __shared__ uint64_t cand[kSearchWaves][kSearchCands];
   __shared__ uint32_t win[kSearchWaves][kWinWords];
   __shared__ ClLds cls[kSearchWaves][64];
@@ -555,8 +555,10 @@ __device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restri
 // the one that decoded end-of-block are the block; their tokens are copied
 // to the segment's tokens.
 //
-// Staged form (kStaged, the lanes [0, n_staged)): the segment's compressed
-// words are first copied into LDS by the whole wave (coalesced, one wait),
+// Staged form (kStaged, the lanes [0, n_staged)): at each block start the
+// compressed words from there are copied into LDS by the whole wave
+// (coalesced, one wait; at most kStageWords: a longer body is decoded in
+// windows, the next starting at the last lane's end with the same tables),
 // so the header walk, the sub-span decodes and their cursor refills read LDS
 // only.  Read from global memory, every cursor refill waited for its load
 // (the window rotation copies the loaded registers at once), a latency of
@@ -591,16 +593,22 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
   const uint64_t end = a.lane_end[seg];  // ~0: the file's last segment (ends with the BFINAL block)
   const bool final_seg = end == ~0ull;
   Bits in{gin};
-  uint64_t sbase = 0;  // (kStaged: the file bit position of stage[0])
-  if (kStaged) {  // words [w0, w0 + nw) of the file into LDS; `in` reads them at their file positions
-    const uint64_t s0 = a.lane_start[seg];
-    const uint64_t w0 = s0 >> 5;
-    sbase = w0 * 32;
-    const uint32_t nw = (uint32_t)inflate_segment_words(s0, final_seg ? limit : end);
+  const uint64_t seg_end = final_seg ? limit : end;
+  uint64_t sbase = 0;   // (kStaged: the file bit position of stage[0])
+  uint64_t slimit = 0;  // (kStaged: lanes decode up to here; their look-ahead stays in the stage)
+  // (kStaged) the file's words from bit b on into LDS, at most kStageWords
+  // and no further than the segment's words; `in` reads them at their file
+  // positions
+  auto restage = [&](uint64_t b) {
+    const uint64_t w0 = b >> 5;
+    const uint32_t nw = (uint32_t)min<uint64_t>(kStageWords, inflate_segment_words(b, seg_end));
+    __syncthreads();  // (every lane is done with the stage before)
     for (uint32_t i = j; i < nw; i += kSpanLanes) stage[i] = gin[w0 + i];
     __syncthreads();
     in.w = stage - w0;  // (only words [w0, w0 + nw) are read)
-  }
+    sbase = w0 * 32;
+    slimit = min(seg_end, sbase + (uint64_t)(nw - 8) * 32);
+  };
   uint32_t* out = a.tok + a.tok_off[seg];
   const uint64_t cap = a.tok_cap[seg];
   uint32_t* scr_all = a.scr + a.scr_off[seg];
@@ -625,6 +633,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
         tp = t;
       }
     };
+    if constexpr (kStaged) restage(pos);  // (the header and the body's first window)
     const int bt = wave_header(in, pos, tab, hcl, H, j);
     phase(0);
     const uint32_t bfinal = H.bfinal;
@@ -644,19 +653,27 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
         status = kDecFull;
         break;
       }
-      const uint8_t* src = (const uint8_t*)in.w + body0 / 8;
+      const uint8_t* src = (const uint8_t*)gin + body0 / 8;  // (global: a stored block may pass the stage)
       for (uint64_t i = j; i < stl; i += kSpanLanes) out[n_out + i] = src[i];
       n_out += stl;
       out_bytes += stl;
       pos = body0 + 8 * stl;
     } else {
-      const uint64_t span_end = final_seg ? limit : end;
+      const uint64_t span_end = seg_end;
+      // windows of the body: staged, what the LDS stage holds (a body that
+      // runs past it continues from the last lane's end, a symbol start,
+      // with the same tables); global, the whole span at once
+      uint64_t bstart = body0;
+      bool more = true, stop_blk = false;
+      while (more) {
+      more = false;
+      const uint64_t wend = kStaged ? slimit : span_end;
       uint64_t L;
       uint32_t nsub;
-      span_layout(body0, span_end, kSpanLanes, L, nsub);
+      span_layout(bstart, wend, kSpanLanes, L, nsub);
       const bool act = j < nsub;
-      const uint64_t S = body0 + j * L;
-      const uint64_t R = j + 1 == nsub ? span_end : S + L;
+      const uint64_t S = bstart + j * L;
+      const uint64_t R = j + 1 == nsub ? wend : S + L;
       const uint64_t capL = span_cap(L), ncks = span_cks(L);
       uint32_t* A = scr_all + j * span_words(L);  // first decode
       uint32_t* B = A + capL;                     // second decode
@@ -703,8 +720,9 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
           c_end = t;
           break;
         }
-        if (c >= nsub) {  // every span right, none ended the block: it runs past the segment
-          overrun = true;
+        if (c >= nsub) {  // every span right, none ended the block: it runs past the window
+          overrun = wend == span_end;  // (past the segment: not a block boundary; else the next window)
+          more = !overrun;
           c_end = nsub - 1;
           break;
         }
@@ -732,11 +750,13 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       if (overrun) {  // (the host decodes again from this block's start, the tokens before it kept)
         status = kDecOverrun;
         pos = blk0;
+        stop_blk = true;
         break;
       }
       if (st_end == kSpanBad) {
         status = kDecBad;
         pos = e_end;
+        stop_blk = true;
         break;
       }
       phase(2);
@@ -775,6 +795,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       const uint32_t total = __shfl(incl, 63);
       if (n_out + total > cap) {
         status = kDecFull;
+        stop_blk = true;
         break;
       }
       uint32_t* dst = out + n_out + (incl - valid);
@@ -788,7 +809,13 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       n_out += total;
       out_bytes += tb;
       pos = e_end;
-      __syncthreads();  // (the LDS tables and spans are rewritten for the next block)
+      __syncthreads();  // (the LDS tables and spans are rewritten for the next block or window)
+      if (more) {
+        bstart = e_end;
+        if constexpr (kStaged) restage(bstart);
+      }
+      }  // (windows)
+      if (stop_blk) break;
     }
     if (bfinal) {
       fin = 1;
@@ -1192,8 +1219,6 @@ hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st) {
                      dim3(64 * kSearchWaves), 0, st, a);
   return hipGetLastError();
 }
-
-uint32_t inflate_stage_words() { return kStageWords; }
 
 hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st) {
   if (a.n_staged)

@@ -213,12 +213,11 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
       if (lanes[l].alive && lanes[l].redo) redo.push_back(l);
     const uint32_t nl = (uint32_t)redo.size();
     if (nl == 0) break;
-    // the lanes whose segment fits the staged (LDS) decode first
-    auto fits = [&](uint32_t l) {
-      const Lane& x = lanes[l];
-      return inflate_segment_words(x.start, x.end == ~0ull ? fbits[x.file] : x.end) <= inflate_stage_words();
-    };
-    const uint32_t n_staged = (uint32_t)(std::stable_partition(redo.begin(), redo.end(), fits) - redo.begin());
+    // every lane takes the staged (LDS) decode, which stages a long segment
+    // in windows (GALAHGPU_DECODE_GLOBAL=1: the global-memory form, A/B only)
+    const char* gdec = getenv("GALAHGPU_DECODE_GLOBAL");
+    const bool global_only = gdec && *gdec == '1';
+    const uint32_t n_staged = global_only ? 0u : nl;
     if (pass >= kMaxRelaunch) return hand_back("block starts did not chain", 0);  // (ok = false)
     // the lanes to decode: 6 arrays of nl u64 (file, start, end, tok_off, cap, scr_off)
     std::vector<uint64_t> arg((size_t)nl * 6);

@@ -87,8 +87,13 @@ static void expand(const std::vector<uint32_t>& toks, std::vector<uint8_t>& out)
 // first decode) and concatenated (inflate.hip inflate_decode_kernel).
 // rounds counts second-decode rounds, redo_bits the bits they decoded.
 struct SpecStats {
-  size_t rounds = 0, redo_bits = 0, spans = 0, span_bits = 0;
+  size_t rounds = 0, redo_bits = 0, spans = 0, span_bits = 0, windows = 0;
 };
+// The staged decode's window (bits of LDS stage past its word-aligned base,
+// less the look-ahead): a block body longer than that is decoded in
+// windows, each from the last lane's end of the one before (0: no windows,
+// the global form).
+static uint64_t g_window = 0;
 static uint32_t spec_segment(const Bits& in, uint64_t s0, uint64_t end, uint64_t limit, LaneTables<ArrayStore>& tab,
                              ClArrays& cla, std::vector<uint32_t>& out, uint64_t& out_len, uint64_t& last_end, uint32_t& fin,
                              SpecStats& ss) {
@@ -116,9 +121,15 @@ static uint32_t spec_segment(const Bits& in, uint64_t s0, uint64_t end, uint64_t
       pos = q + 8ull * stl;
     } else {
       const uint64_t span_end = final_seg ? limit : end;
+      uint64_t bstart = q, wbase = pos;
+      bool more = true;
+      while (more) {
+      more = false;
+      const uint64_t wend = g_window ? std::min<uint64_t>(span_end, (wbase & ~31ull) + g_window) : span_end;
+      ++ss.windows;
       uint64_t L;
       uint32_t nsub;
-      span_layout(q, span_end, 64, L, nsub);
+      span_layout(bstart, wend, 64, L, nsub);
       struct Lane {
         uint64_t S, R, first = 0, Ea = 0, Eb = 0, ba = 0, bb = 0;
         uint32_t na = 0, nb = 0, sa = 0, sb = 0, nck = 0;
@@ -132,8 +143,8 @@ static uint32_t spec_segment(const Bits& in, uint64_t s0, uint64_t end, uint64_t
       std::vector<Lane> ln(nsub);
       for (uint32_t j = 0; j < nsub; ++j) {
         Lane& x = ln[j];
-        x.S = q + j * L;
-        x.R = j + 1 == nsub ? span_end : x.S + L;
+        x.S = bstart + j * L;
+        x.R = j + 1 == nsub ? wend : x.S + L;
         x.ck.assign(span_cks(L), 0);
         x.sa = decode_span(in, x.S, x.S, x.R, tab,
                            [&](uint32_t t) {
@@ -165,7 +176,8 @@ static uint32_t spec_segment(const Bits& in, uint64_t s0, uint64_t end, uint64_t
           break;
         }
         if (c >= nsub) {
-          overrun = true;
+          overrun = wend == span_end;
+          more = !overrun;
           c_end = nsub - 1;
           break;
         }
@@ -220,6 +232,8 @@ static uint32_t spec_segment(const Bits& in, uint64_t s0, uint64_t end, uint64_t
         }
       }
       pos = ln[c_end].E();
+      bstart = wbase = pos;
+      }  // (windows)
     }
     if (bf) {
       fin = 1;
@@ -235,9 +249,16 @@ int main(int argc, char** argv) {
   int failures = 0;
   uint32_t chunk = 4096;
   int first = 1;
-  if (argc > 2 && std::string(argv[1]) == "--chunk") {
-    chunk = (uint32_t)atoi(argv[2]);
-    first = 3;
+  for (;;) {
+    if (argc > first + 1 && std::string(argv[first]) == "--chunk") {
+      chunk = (uint32_t)atoi(argv[first + 1]);
+      first += 2;
+    } else if (argc > first + 1 && std::string(argv[first]) == "--window") {
+      g_window = (uint64_t)atoll(argv[first + 1]);
+      first += 2;
+    } else {
+      break;
+    }
   }
   for (int a = first; a < argc; ++a) {
     std::vector<uint8_t> gz, want;
@@ -379,9 +400,9 @@ int main(int argc, char** argv) {
       continue;
     }
     printf("{\"file\": \"%s\", \"bytes\": %zu, \"gz_bytes\": %zu, \"starts_found\": %zu, \"starts_dropped\": %zu, "
-           "\"lanes\": %zu, \"tokens\": %zu, \"max_chain\": %zu, \"redo_rounds\": %zu, \"spans\": %zu, \"span_bits\": %zu, \"redo_bits\": %zu}\n",
+           "\"lanes\": %zu, \"tokens\": %zu, \"max_chain\": %zu, \"redo_rounds\": %zu, \"spans\": %zu, \"span_bits\": %zu, \"redo_bits\": %zu, \"windows\": %zu}\n",
            argv[a], want.size(), gz.size(), found, dropped, starts.size(), toks.size(), max_chain, ss.rounds, ss.spans,
-           ss.span_bits, ss.redo_bits);
+           ss.span_bits, ss.redo_bits, ss.windows);
   }
   if (failures) {
     fprintf(stderr, "%d failure(s)\n", failures);

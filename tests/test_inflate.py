@@ -67,16 +67,22 @@ def core_binary():
     return BIN
 
 
-@pytest.mark.parametrize("chunk", [4096, 300])
-def test_core_chunked_decode_equals_zlib(core_binary, tmp_path, chunk):
+@pytest.mark.parametrize("chunk,window", [(4096, 0), (300, 0), (4096, 20000), (65536, 100000)])
+def test_core_chunked_decode_equals_zlib(core_binary, tmp_path, chunk, window):
+    """window > 0: the staged device decode's windows (a block body longer
+    than the LDS stage continues from the last sub-span's end); with 64 KB
+    chunks most segments hold several blocks."""
     paths = golden_gz() + synthetic_streams(str(tmp_path))
-    r = subprocess.run([core_binary, "--chunk", str(chunk)] + paths, capture_output=True, text=True, timeout=300)
+    r = subprocess.run([core_binary, "--chunk", str(chunk), "--window", str(window)] + paths, capture_output=True,
+                       text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     rows = [json.loads(x) for x in r.stdout.splitlines()]
     assert len(rows) == len(paths)
     # the search finds block starts in the multi-block streams
     big = [x for x in rows if x["file"].endswith("l6.fa.gz") or "abisko4" in x["file"]]
     assert big and all(x["starts_found"] > 1 for x in big)
+    if window:  # (bodies longer than a window were decoded in several)
+        assert sum(x["windows"] for x in rows) > sum(x["lanes"] for x in rows)
 
 
 # ---------------------------------------------------------------------------
@@ -136,6 +142,34 @@ def test_device_inflate_streams_and_handbacks(tmp_path, monkeypatch):
         dsk, dl, fb = sketch_files(ps, monkeypatch, "device")
         assert fb["inflate_host"] == 1, extra
         assert (dl == hl).all() and all((dsk[g][:dl[g]] == hsk[g][:hl[g]]).all() for g in range(len(ps)))
+
+
+@pytest.mark.gpu
+def test_device_inflate_blocks_longer_than_the_stage(tmp_path, monkeypatch):
+    """zlib memLevel 9 (as GNU gzip: 32k symbols per block, ~53 KB of
+    FASTA) makes block bodies longer than the staged decode's 30 KB LDS
+    window: they are decoded in windows.  Sketches equal the oracle's and
+    the host path's, no batch handed back."""
+    rng = np.random.default_rng(9)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    paths = []
+    for i in range(12):
+        seq = acgt[rng.integers(0, 4, 1500000)].tobytes()
+        text = b">big%d\n" % i + b"\n".join(seq[j:j + 60] for j in range(0, len(seq), 60)) + b"\n"
+        c = zlib.compressobj(9 if i % 2 else 6, zlib.DEFLATED, 31, 9)
+        p = tmp_path / ("big%02d.fna.gz" % i)
+        p.write_bytes(c.compress(text) + c.flush())
+        paths.append(str(p))
+    exp_sk, exp_len = oracle.sketch_files(paths, threads=8)
+    dsk, dl, fb = sketch_files(paths, monkeypatch, "device")
+    assert fb["inflate_host"] == 0
+    assert (dl == exp_len).all()
+    for g in range(len(paths)):
+        assert (dsk[g][:dl[g]] == exp_sk[g][:dl[g]]).all(), paths[g]
+    # the global-memory decode (A/B knob) agrees
+    monkeypatch.setenv("GALAHGPU_DECODE_GLOBAL", "1")
+    gsk, gl, fb = sketch_files(paths, monkeypatch, "device")
+    assert fb["inflate_host"] == 0 and (gl == dl).all() and (gsk == dsk).all()
 
 
 @pytest.mark.gpu
