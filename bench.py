@@ -155,8 +155,13 @@ def k2_pmc(config):
 
 # K2 kernels timed under GG_KERNEL_PAIRS / GG_KERNEL_PAIRS_INDEX (the passing
 # pairs' device sort is not: it is output handling, ~0.1 ms at C3)
-K2_TIMED = ("index_scan", "bucket_hist", "bucket_base", "index_fill", "index_sort", "bucket_bounds", "index_bucket",
-            "index_pairs")
+K2_TIMED = ("index_scan", "bucket_hist", "bucket_base", "index_fill", "index_sort", "bucket_bounds", "split_keys",
+            "split_scan", "split_scatter", "superbin_count", "superbin_place", "index_bucket", "index_pairs")
+
+
+def index_split_on():
+    """The split build (default) or GALAHGPU_INDEX_SPLIT=0's fill + 16-bit sort."""
+    return os.environ.get("GALAHGPU_INDEX_SPLIT", "1") != "0"
 
 
 def k2_algorithmic_bytes(d_sk, d_len, n, s):
@@ -178,13 +183,26 @@ def k2_algorithmic_bytes(d_sk, d_len, n, s):
     m = 2 if n <= 65536 else 4
     per = {
         "index_scan": 4.0 * n,                        # row lengths
-        "bucket_hist": 8.0 * E,                       # each hash once
-        "index_fill": 8.0 * E + 6.0 * S,              # hash read; 16-bit bucket key + 32-bit entry written per slot
-        "sort_16bit_2pass": 2.0 * S + 2 * 12.0 * S,   # key histogram; 2 passes reading and writing 6 B per slot
-        "bucket_bounds": 2.0 * S,                     # sorted keys
+        "bucket_hist": 8.0 * (E if E < (1 << 26) else E / 8),  # each hash once (past 2^26 entries: 1 line in 8)
+    }
+    if index_split_on():
+        per.update({
+            "split_keys": 8.0 * E + 2.0 * S,          # hash read; 16-bit bucket id written per slot
+            "split_scan": 2 * 4.0 * 256 * n,           # per-row super-bin counts read, offsets written
+            "split_scatter": 2.0 * E + 5.0 * E,        # bucket ids read; low key byte + 32-bit entry written
+            "superbin_count": 1.0 * E,                 # key bytes
+            "superbin_place": 5.0 * E + 4.0 * E,       # key bytes + entries read, entries written
+        })
+    else:
+        per.update({
+            "index_fill": 8.0 * E + 6.0 * S,          # hash read; 16-bit bucket key + 32-bit entry written per slot
+            "sort_16bit_2pass": 2.0 * S + 2 * 12.0 * S,  # key histogram; 2 passes reading and writing 6 B per slot
+            "bucket_bounds": 2.0 * S,                 # sorted keys
+        })
+    per.update({
         "index_bucket": (4.0 + 8.0 + m + 8.0) * E,    # entry, its hash, member id and runinfo written
         "index_pairs": 8.0 * E + m * g2,              # runinfo of every entry; g members of each of its runs
-    }
+    })
     return {"bytes": sum(per.values()), "per_kernel": per, "entries": E, "slots": S, "shared_runs": runs,
             "sum_g2": g2}
 
@@ -201,8 +219,10 @@ def roofline_k2(model, kst_pr, config):
            "algorithmic_bytes_per_kernel": {k: round(v) for k, v in model["per_kernel"].items()},
            "entries": model["entries"], "slots": model["slots"], "shared_runs": model["shared_runs"],
            "sum_g2": round(model["sum_g2"]),
-           "kernel": "K2: bucketed inverted index (index_scan, bucket_hist, bucket_base, index_fill, 16-bit onesweep "
-                     "sort, bucket_bounds, index_bucket) + index_pairs_kernel",
+           "kernel": ("K2: bucketed inverted index (index_scan, bucket_hist, bucket_base, split_keys, scan, "
+                      "split_scatter, superbin_count/place, index_bucket) + index_pairs_kernel" if index_split_on() else
+                      "K2: bucketed inverted index (index_scan, bucket_hist, bucket_base, index_fill, 16-bit onesweep "
+                      "sort, bucket_bounds, index_bucket) + index_pairs_kernel"),
            "note": "achieved = algorithmic bytes (per kernel above, DESIGN §4) / K2's HIP-event time per step (index "
                    "build + pairs kernel, on the stream they run on); traffic = HBM bytes of the same kernels from "
                    "the PMC pass (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md), per step"}

@@ -158,7 +158,7 @@ _sig("gg_pair_paths", _i32, [_vp, _vp])
 _sig("gg_fallbacks", _i32, [_vp, _vp])
 _sig("gg_peer_links", _i32, [_vp, _vp])
 _sig("gg_info_line", _i32, [_vp, ctypes.c_char_p, ctypes.c_size_t])
-FALLBACKS = ("index_to_gate", "index_full_sort", "peer_staged", "sketch_retry", "inflate_host")  # gg_fallbacks order
+FALLBACKS = ("index_to_gate", "index_full_sort", "peer_staged", "sketch_retry", "inflate_host", "sketch_set")  # gg_fallbacks order
 _sig("gg_timing_read", _i32, [_vp, _i32, ctypes.POINTER(_KStats)])
 KERNEL_SKETCH, KERNEL_FINALIZE, KERNEL_PAIRS, KERNEL_PAIRS_INDEX = 0, 1, 2, 3
 # the device-inflate ingest's kernels (gzip lists through precluster_files / sketch_files)
@@ -525,7 +525,7 @@ class Context:
 
     def fallbacks(self):
         """Slow paths taken since the context was created (gg_fallbacks):
-        {"index_to_gate", "index_full_sort", "peer_staged", "sketch_retry", "inflate_host"}."""
+        {"index_to_gate", "index_full_sort", "peer_staged", "sketch_retry", "inflate_host", "sketch_set"}."""
         out = np.zeros(len(FALLBACKS), np.uint64)
         st = _L.gg_fallbacks(self._c, _ptr(out))
         if st != GG_OK:

@@ -482,6 +482,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
           if (status0[slot] == kSketchOk) continue;
           if (status0[slot] == kSketchRetrySet) {  // the same tau, in set mode
             set_mode[slot] = 1;
+            ++c->fallbacks[GG_FALLBACK_SKETCH_SET];
             next.push_back(slot);
             continue;
           }
@@ -581,6 +582,7 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
         if (status[slot] == kSketchOk) continue;
         if (status[slot] == kSketchRetrySet) {  // the same tau, in set mode
           set_mode[slot] = 1;
+          ++c->fallbacks[GG_FALLBACK_SKETCH_SET];
           next.push_back(slot);
           continue;
         }
@@ -845,9 +847,18 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
     // back to back (every row slot is a sort item, so the sort's size is
     // known up front; the pairs kernel emits nothing if the build failed)
     const uint32_t nbb = index_bucket_bound(total);
-    b.sort_tmp_bytes = index_bucket_sort_tmp_bytes(total);
+    // split build (default; GALAHGPU_INDEX_SPLIT=0: the fill and the 16-bit
+    // sort), whose super-bin sort writes the bounds of all 2^16 bucket ids
+    const char* se = getenv("GALAHGPU_INDEX_SPLIT");
+    const bool split = !(se && *se == '0');
+    if (split) {
+      GG_HIP(c, scratch_t(c, "idx_split_cnt", (size_t)256 * n + 1, &b.split_cnt));
+      GG_HIP(c, scratch_t(c, "idx_split_off", (size_t)256 * n + 1, &b.split_off));
+      GG_HIP(c, scratch_t(c, "idx_split_hist", (size_t)256 * 16 * 256, &b.split_hist));
+    }
+    b.sort_tmp_bytes = split ? index_split_tmp_bytes(n) : index_bucket_sort_tmp_bytes(total);
     GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
-    GG_HIP(c, scratch_t(c, "idx_bstart", (size_t)nbb + 1, &b.bstart));
+    GG_HIP(c, scratch_t(c, "idx_bstart", split ? (size_t)65537 : (size_t)nbb + 1, &b.bstart));
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_fill(b, st); }));
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st, [&] { return index_build_buckets(b, total, nbb, st); }));
     gg_status ps = launch_pairs(true);
@@ -1416,11 +1427,13 @@ gg_status gg_info_line(const gg_ctx* ctx, char* buf, size_t cap) {
   snprintf(line, sizeof line,
            "galahgpu: %zu device(s) [%s]; sketch %.1f ms, replicate %.2f ms, pairs %.2f ms, merge %.2f ms; "
            "fallbacks: index->gate %llu, index full sort %llu, host-staged peer copies %llu (links without peer "
-           "access %llu), sketch retry passes %llu, host-inflated batches %llu (device-inflated %llu)",
+           "access %llu), sketch retry passes %llu (set-mode genomes %llu), host-inflated batches %llu "
+           "(device-inflated %llu)",
            M, ords.c_str(), ctx->phase_ms[GG_PHASE_SKETCH], ctx->phase_ms[GG_PHASE_REPLICATE],
            ctx->phase_ms[GG_PHASE_PAIRS], ctx->phase_ms[GG_PHASE_MERGE], (unsigned long long)fb[0],
            (unsigned long long)fb[1], (unsigned long long)fb[2], (unsigned long long)staged_links,
-           (unsigned long long)fb[3], (unsigned long long)fb[4], (unsigned long long)dev_batches);
+           (unsigned long long)fb[3], (unsigned long long)fb[5], (unsigned long long)fb[4],
+           (unsigned long long)dev_batches);
   const size_t n = std::min(cap - 1, strlen(line));
   memcpy(buf, line, n);
   buf[n] = 0;

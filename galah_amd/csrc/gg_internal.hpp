@@ -358,6 +358,15 @@ struct IndexBuild {
   uint32_t* hist = nullptr;
   uint32_t* bbase = nullptr;
   uint32_t* bstart = nullptr;
+  // Split build (split_cnt != null; bucketed, every row): instead of the
+  // fill and the 16-bit sort, the entries are dealt to 256 super-bins (bucket
+  // >> 8) row by row -- a row is sorted, so its entries of one super-bin are
+  // contiguous -- at offsets from a scan of the per-row counts (split_cnt,
+  // split_off: [256 * n + 1], super-bin major), and each super-bin's
+  // entries are ordered by the low 8 bits of their bucket.
+  uint32_t* split_cnt = nullptr;
+  uint32_t* split_off = nullptr;
+  uint32_t* split_hist = nullptr;  // [256 * 16 * 256]: per super-bin slice, its counts per bucket
 };
 struct IndexLaunch {
   const uint64_t* sketches;
@@ -399,6 +408,8 @@ uint32_t index_bucket_bound(uint64_t entries);
 // the bucketed build's
 size_t index_sort_tmp_bytes(uint64_t total, uint32_t end_bit);
 size_t index_bucket_sort_tmp_bytes(uint64_t total);
+// temporary bytes of the split build's scan over 256 * n + 1 counts
+size_t index_split_tmp_bytes(uint32_t n);
 constexpr uint32_t kIndexCoarse = 4096;  // coarse bins of the bucketed build
 hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t st);
 bool index_ents16(uint32_t n);

@@ -309,10 +309,20 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     // not a block boundary -- the lane takes the next lane's range and token
     // region (they follow its own) and is decoded again, alone, from the
     // start of the block that ran past (last_end), its earlier blocks' tokens
-    // kept (and its scratch, which the next lane's follows)
+    // kept (and its scratch, which the next lane's follows).  A failed lane
+    // right after a lane set to decode again waits for that lane's next pass:
+    // its start may be a false one the lane before will run past and absorb
+    // (two false starts in a row), and is only confirmed when that lane ends
+    // on it.
+    bool prev_redo = false;
+    uint32_t prev_file = ~0u;
     for (uint32_t l = 0; l < (uint32_t)lanes.size(); ++l) {
       Lane& x = lanes[l];
-      if (!x.alive || x.redo) continue;
+      if (!x.alive) continue;
+      const bool after_redo = prev_redo && prev_file == x.file;
+      prev_file = x.file;
+      prev_redo = x.redo;
+      if (x.redo) continue;
       uint32_t nx = l + 1;
       while (nx < lanes.size() && !lanes[nx].alive) ++nx;
       const bool has_next = nx < lanes.size() && lanes[nx].file == x.file;
@@ -325,7 +335,8 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
         x.cap = y.tok_off + y.cap - x.tok_off;
         x.redo = true;
         y.alive = false;
-      } else if (x.status != inflate::kDecOk) {  // malformed / full / a second member: host path
+        prev_redo = true;
+      } else if (x.status != inflate::kDecOk && !after_redo) {  // malformed / full / a second member: host path
         return hand_back(x.status == inflate::kDecFull ? "token capacity"
                          : x.status == inflate::kDecFinalEarly ? "stream ended early (several members?)"
                                                                : "malformed stream", x.file);

@@ -165,6 +165,23 @@ __global__ __launch_bounds__(256) void index_fill_kernel(const uint64_t* __restr
   }
 }
 
+// Adds the lanes' values to the LDS counts h for a wave whose active lanes
+// (`in`, a prefix of the wave) hold non-decreasing values: the first lane of
+// each run of equal values adds the run's length x weight (one atomic per
+// run).
+__device__ __forceinline__ void wave_runs_add(uint32_t* h, uint32_t v, bool in, uint32_t weight = 1) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t prev = __shfl_up(v, 1);
+  const bool head = in && (lane == 0 || prev != v);
+  const uint64_t heads = __ballot(head);
+  const uint32_t n_in = (uint32_t)__popcll(__ballot(in));
+  if (head) {
+    const uint64_t after = (heads >> lane) >> 1;
+    const uint32_t next = after ? lane + 1u + (uint32_t)__builtin_ctzll(after) : 64u;
+    atomicAdd(&h[v], (min(next, n_in) - lane) * weight);
+  }
+}
+
 // Coarse-bin histogram of every sketch entry (one LDS histogram per
 // workgroup over a contiguous slice of rows, merged with one atomic per
 // non-empty bin).
@@ -172,7 +189,7 @@ __global__ __launch_bounds__(256) void bucket_hist_kernel(const uint64_t* __rest
                                                           const uint32_t* __restrict__ lens, uint32_t n,
                                                           uint32_t stride,
                                                           const unsigned long long* __restrict__ info,
-                                                          uint32_t* __restrict__ hist) {
+                                                          uint32_t* __restrict__ hist, uint32_t may_sample) {
   __shared__ uint32_t lh[kCoarse];
   for (uint32_t x = threadIdx.x; x < kCoarse; x += 256) lh[x] = 0u;
   __syncthreads();
@@ -180,28 +197,40 @@ __global__ __launch_bounds__(256) void bucket_hist_kernel(const uint64_t* __rest
   const uint32_t i0 = (uint32_t)((uint64_t)n * blockIdx.x / gridDim.x);
   const uint32_t i1 = (uint32_t)((uint64_t)n * (blockIdx.x + 1) / gridDim.x);
   auto bin = [&](uint64_t h) { return ((uint32_t)(h >> ks.sh) << ks.norm) >> (32 - kCoarseBits); };
-  // A row is sorted, so its bins never decrease: each thread takes a
-  // contiguous piece of the row and adds one count per run of equal bins.
-  // (Consecutive entries on consecutive lanes put the lanes of a wave on a
-  // few neighbouring bins: C5's s = 10000 rows hold ~2.4 entries per bin,
-  // and the same-address LDS atomics serialised, 21.5 conflict cycles per
-  // LDS instruction.)
+  // A row is sorted, so its bins never decrease: the lanes of a wave read 64
+  // consecutive entries (coalesced) and only the first lane of each run of
+  // equal bins adds the run's length (C5's s = 10000 rows hold ~2.4 entries
+  // per bin: one atomic per entry put the lanes of a wave on a few
+  // neighbouring bins, 21.5 conflict cycles per LDS instruction; a contiguous
+  // piece per thread instead spread every load over 64 lines and read the
+  // sketches ~6x over, 0.25 -> 0.76 ms)
+  // Past 2^26 entries the histogram is sampled: one 16-entry line (128 B) of
+  // every 8 of a row, its offset varying with the row, each entry counted 8
+  // times.  The counts only shape the buckets (any bucket_of is exact), and
+  // a coarse bin then holds >= ~2k sampled entries at C5's skew, so a bucket
+  // comes out within a few % of `per` (the capacity is 1.8x).
+  const bool sample = may_sample && info[0] >= (1ull << 26);
   for (uint32_t i = i0; i < i1; ++i) {
     const uint32_t len = lens[i];
     const uint64_t* row = sk + (uint64_t)i * stride;
-    const uint32_t per = (len + 255) / 256;
-    const uint32_t k0 = min(len, threadIdx.x * per), k1 = min(len, k0 + per);
-    uint32_t cur = ~0u, cnt = 0;
-    for (uint32_t k = k0; k < k1; ++k) {
-      const uint32_t b = bin(row[k]);
-      if (b != cur) {
-        if (cnt) atomicAdd(&lh[cur], cnt);
-        cur = b;
-        cnt = 0;
+    if (sample) {
+      const uint32_t lines = (len + 15) / 16, first = i & 7;
+      const uint32_t q_end = lines > first ? (lines - first + 7) / 8 * 16 : 0;
+      for (uint32_t q0 = 0; q0 < q_end; q0 += 256) {
+        const uint32_t q = q0 + threadIdx.x;
+        const uint32_t k = (first + (q >> 4) * 8) * 16 + (q & 15);
+        const bool in = q < q_end && k < len;
+        const uint32_t b = in ? bin(row[k]) : ~0u;
+        wave_runs_add(lh, b, in, 8);
       }
-      ++cnt;
+      continue;
     }
-    if (cnt) atomicAdd(&lh[cur], cnt);
+    for (uint32_t k0 = 0; k0 < len; k0 += 256) {
+      const uint32_t k = k0 + threadIdx.x;
+      const bool in = k < len;
+      const uint32_t b = in ? bin(row[k]) : ~0u;
+      wave_runs_add(lh, b, in);
+    }
   }
   __syncthreads();
   for (uint32_t x = threadIdx.x; x < kCoarse; x += 256)
@@ -216,14 +245,29 @@ __global__ __launch_bounds__(kBaseThreads) void bucket_base_kernel(const uint32_
                                                                    const unsigned long long* __restrict__ info,
                                                                    uint32_t* __restrict__ bbase) {
   __shared__ uint32_t wsum[kBaseThreads / 64];
+  __shared__ unsigned long long wtot[kBaseThreads / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
-  const unsigned long long total = info[0];
-  const uint32_t per = (uint32_t)max(1024ull, (total + 59999ull) / 60000ull);
   constexpr uint32_t q = kCoarse / kBaseThreads;
+  // per from the histogram's own total (a sampled histogram's differs from
+  // the entries a little): sum ceil(c / per) <= 60000 + 4096 buckets either way
+  uint32_t hc[q];
+  unsigned long long t = 0;
+#pragma unroll
+  for (uint32_t x = 0; x < q; ++x) {
+    hc[x] = hist[tid * q + x];
+    t += hc[x];
+  }
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+  if (lane == 0) wtot[tid >> 6] = t;
+  __syncthreads();
+  unsigned long long total = 0;
+  for (uint32_t w = 0; w < kBaseThreads / 64; ++w) total += wtot[w];
+  (void)info;
+  const uint32_t per = (uint32_t)max(1024ull, (total + 59999ull) / 60000ull);
   uint32_t ns[q], sum = 0;
 #pragma unroll
   for (uint32_t x = 0; x < q; ++x) {
-    ns[x] = (hist[tid * q + x] + per - 1u) / per;
+    ns[x] = max(1u, (hc[x] + per - 1u) / per);  // (a bin the sample missed still gets its own bucket)
     sum += ns[x];
   }
   uint32_t inc = sum;
@@ -241,6 +285,262 @@ __global__ __launch_bounds__(kBaseThreads) void bucket_base_kernel(const uint32_
     run += ns[x];
   }
   if (tid == kBaseThreads - 1) bbase[kCoarse] = run;
+}
+
+// Split build (bucketed, every row): the sort of the bucket ids is replaced
+// by two placements that use what the sort did not know -- a row is sorted,
+// so bucket ids never decrease along it and its entries of one super-bin
+// (bucket >> 8, at most 256 of them) are one contiguous piece:
+//   split_keys     one workgroup per row: bucket ids (16 bits, row-major
+//                  slots as index_fill writes them) and the row's count per
+//                  super-bin -> cnt[D * n + i];
+//   (scan)         off = exclusive sum of cnt (super-bin major, row minor):
+//                  super-bin D's entries from off[D * n], row i's at
+//                  off[D * n + i];
+//   split_scatter  one workgroup per row: each entry to off[D * n + i] plus
+//                  its place in the row's piece of D, as its 8 low bucket
+//                  bits (keys8) and its entry value (vals);
+//   superbin_count, superbin_place  an LDS counting sort of each super-bin's
+//                  entries by the low bits (the bucket), giving the buckets'
+//                  bounds (bstart) and the entries in bucket order.
+// The entries move 3 times at 5 B instead of a fill and two radix passes at
+// 6 B each (no digit look-back, no bounds pass).
+constexpr uint32_t kSuper = 256;  // super-bins: bucket >> 8 (buckets < 2^16)
+
+__device__ __forceinline__ uint32_t row_of_block(uint32_t n) {
+  // XCD-aware: the workgroups of XCD x (blockIdx % kXcds) take the x-th
+  // contiguous range of rows, so the counts and pieces of neighbouring rows
+  // (adjacent in every super-bin) are written through the same L2
+  const uint32_t per_xcd = (n + kXcds - 1) / kXcds;
+  return (blockIdx.x % kXcds) * per_xcd + blockIdx.x / kXcds;
+}
+
+__global__ __launch_bounds__(256) void split_keys_kernel(const uint64_t* __restrict__ sk,
+                                                         const uint32_t* __restrict__ lens, uint32_t n,
+                                                         uint32_t stride,
+                                                         const unsigned long long* __restrict__ info,
+                                                         const uint32_t* __restrict__ bbase,
+                                                         uint16_t* __restrict__ keys, uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t lc[kSuper];
+  const uint32_t i = row_of_block(n);
+  if (i >= n) return;
+  const uint32_t tid = threadIdx.x;
+  lc[tid] = 0u;
+  if (i == 0 && tid == 0) cnt[(uint64_t)kSuper * n] = 0u;  // (the scan's last item: off[256 n] = entries)
+  __syncthreads();
+  const KeyShape ks = key_shape(info[1]);
+  const uint32_t len = lens[i];
+  const uint64_t* row = sk + (uint64_t)i * stride;
+  uint16_t* krow = keys + (uint64_t)i * stride;
+  for (uint32_t k0 = 0; k0 < stride; k0 += 256) {
+    const uint32_t k = k0 + tid;
+    const bool in = k < len;
+    const uint32_t b = in ? bucket_of(row[k], ks, bbase) : kBucketPad;
+    if (k < stride) krow[k] = (uint16_t)b;
+    if (k0 < len) wave_runs_add(lc, b >> 8, in);  // (uniform: k0 < len)
+  }
+  __syncthreads();
+  cnt[(uint64_t)tid * n + i] = lc[tid];
+}
+
+__global__ __launch_bounds__(256) void split_scatter_kernel(const uint16_t* __restrict__ keys,
+                                                            const uint32_t* __restrict__ lens, uint32_t n,
+                                                            uint32_t stride, uint32_t kbits,
+                                                            const uint32_t* __restrict__ cnt,
+                                                            const uint32_t* __restrict__ off,
+                                                            uint8_t* __restrict__ keys8,
+                                                            uint32_t* __restrict__ vals) {
+  __shared__ uint32_t base[kSuper];
+  __shared__ uint32_t wsum[256 / 64];
+  const uint32_t i = row_of_block(n);
+  if (i >= n) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  // base[D] = off[D n + i] - (the row's entries before its piece of D)
+  const uint32_t c = cnt[(uint64_t)tid * n + i];
+  uint32_t inc = c;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[tid >> 6] = inc;
+  __syncthreads();
+  uint32_t before = inc - c;
+  for (uint32_t w = 0; w < (tid >> 6); ++w) before += wsum[w];
+  base[tid] = off[(uint64_t)tid * n + i] - before;
+  __syncthreads();
+  const uint32_t len = lens[i];
+  const uint16_t* krow = keys + (uint64_t)i * stride;
+  for (uint32_t k = tid; k < len; k += 256) {
+    const uint32_t b = krow[k];
+    const uint32_t p = base[b >> 8] + k;
+    keys8[p] = (uint8_t)b;
+    vals[p] = (i << kbits) | k;
+  }
+}
+
+// The super-bin sort: super-bin D's entries [off[D n], off[(D + 1) n]) are
+// cut into kSuperParts equal slices, one 256-thread workgroup each (a
+// workgroup per super-bin left the chip at one workgroup per CU: 0.57 ms at
+// C5).  A slice is read in groups of 16 entries (one 16-byte load of keys8,
+// four of vals; groups aligned to 16 entries, the slice ends masked).
+//   superbin_count  the slice's counts per low key byte -> shist[D][part][256]
+//   superbin_place  bucket x of super-bin D starts at off[D n] + the counts of
+//                   buckets < x over all slices (bstart; part 0 writes it,
+//                   the last workgroup also bstart[65536] = entries); the
+//                   slice's entries of bucket x follow those of earlier
+//                   slices (order inside a bucket is free: index_bucket
+//                   groups by hash)
+constexpr uint32_t kSuperParts = 16;
+
+__device__ __forceinline__ void super_slice(const uint32_t* __restrict__ off, uint32_t n, uint32_t D, uint32_t part,
+                                            uint32_t& a, uint32_t& e) {
+  const uint32_t s0 = off[(uint64_t)D * n], s1 = off[(uint64_t)(D + 1) * n];
+  a = s0 + (uint32_t)((uint64_t)(s1 - s0) * part / kSuperParts);
+  e = s0 + (uint32_t)((uint64_t)(s1 - s0) * (part + 1) / kSuperParts);
+}
+
+// XCD-aware: the kSuperParts slices of a super-bin run on one XCD (blockIdx
+// % kXcds), so the bucket-ordered lines of its output are written through
+// one L2 (slices dealt round-robin over the XCDs wrote each line from up to
+// 8 L2s)
+__device__ __forceinline__ void super_block(uint32_t& D, uint32_t& part) {
+  constexpr uint32_t per_xcd = kSuper / kXcds;
+  const uint32_t j = blockIdx.x / kXcds;
+  D = (blockIdx.x % kXcds) * per_xcd + j / kSuperParts;
+  part = j % kSuperParts;
+}
+
+__device__ __forceinline__ uint32_t key_byte(const uint32_t (&w)[4], uint32_t e) {
+  return (w[e >> 2] >> (8 * (e & 3))) & 0xFFu;
+}
+
+__global__ __launch_bounds__(256) void superbin_count_kernel(const uint8_t* __restrict__ keys8,
+                                                             const uint32_t* __restrict__ off, uint32_t n,
+                                                             uint32_t* __restrict__ shist) {
+  __shared__ uint32_t h[kSuper];
+  const uint32_t tid = threadIdx.x;
+  uint32_t D, part, a, e;
+  super_block(D, part);
+  super_slice(off, n, D, part, a, e);
+  h[tid] = 0u;
+  __syncthreads();
+  for (uint64_t g = a / 16 + tid; g < (e + 15ull) / 16; g += 256) {
+    const uint4 kw = *(const uint4*)(keys8 + g * 16);
+    const uint32_t w[4] = {kw.x, kw.y, kw.z, kw.w};
+#pragma unroll
+    for (uint32_t x = 0; x < 16; ++x) {
+      const uint64_t p = g * 16 + x;
+      if (p >= a && p < e) atomicAdd(&h[key_byte(w, x)], 1u);
+    }
+  }
+  __syncthreads();
+  shist[((uint64_t)D * kSuperParts + part) * kSuper + tid] = h[tid];
+}
+
+// superbin_place stages a chunk of up to kPlaceChunk entries in LDS in bucket
+// order (an LDS counting sort of the chunk), then writes each bucket's piece
+// as one contiguous run: ~48 entries per bucket per chunk at C5.  (Placing
+// each entry straight at its bucket's cursor was one 4-byte store per entry
+// to a scattered line: 0.63-0.67 ms at C5.)
+constexpr uint32_t kPlaceThreads = 512;
+constexpr uint32_t kPlaceChunk = 12288;  // (65 KB of LDS: two workgroups per CU)
+
+// exclusive scan of v over threads 0..255 (waves 0-3, uniform), into the
+// running total of waves before; wsum holds the 4 wave totals after a barrier
+__device__ __forceinline__ uint32_t scan256_wave(uint32_t v, uint32_t* wsum) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  uint32_t inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= (uint32_t)o) inc += y;
+  }
+  if (lane == 63) wsum[tid >> 6] = inc;
+  return inc - v;
+}
+
+__global__ __launch_bounds__(kPlaceThreads) void superbin_place_kernel(const uint8_t* __restrict__ keys8,
+                                                                       const uint32_t* __restrict__ vals,
+                                                                       const uint32_t* __restrict__ off, uint32_t n,
+                                                                       const uint32_t* __restrict__ shist,
+                                                                       uint32_t* __restrict__ bstart,
+                                                                       uint32_t* __restrict__ sorted) {
+  __shared__ uint32_t cur[kSuper], lcnt[kSuper], lpos[kSuper], lstart[kSuper], wsum[kSuper / 64];
+  __shared__ uint32_t stage[kPlaceChunk];
+  __shared__ uint8_t sbk[kPlaceChunk];
+  const uint32_t tid = threadIdx.x;
+  const bool bt = tid < kSuper;  // (threads 0-255: one bucket each)
+  uint32_t D, part, a, e;
+  super_block(D, part);
+  super_slice(off, n, D, part, a, e);
+  // bucket tid: its count over all slices and over the slices before this one
+  uint32_t tot = 0, before = 0, ex = 0;
+  if (bt) {
+    const uint32_t* hd = shist + (uint64_t)D * kSuperParts * kSuper + tid;
+#pragma unroll
+    for (uint32_t q = 0; q < kSuperParts; ++q) {
+      const uint32_t c = hd[q * kSuper];
+      tot += c;
+      before += q < part ? c : 0u;
+    }
+    ex = scan256_wave(tot, wsum);
+  }
+  __syncthreads();
+  if (bt) {
+    uint32_t start = off[(uint64_t)D * n] + ex;
+    for (uint32_t w = 0; w < (tid >> 6); ++w) start += wsum[w];
+    if (part == 0) bstart[D * kSuper + tid] = start;
+    if (D == kSuper - 1 && part == kSuperParts - 1 && tid == 0) bstart[(uint64_t)kSuper * kSuper] = e;
+    cur[tid] = start + before;
+  }
+  for (uint32_t c0 = a; c0 < e; c0 += kPlaceChunk) {
+    const uint32_t c1 = min(e, c0 + kPlaceChunk);
+    if (bt) lcnt[tid] = 0u;
+    __syncthreads();
+    for (uint64_t g = c0 / 16 + tid; g < (c1 + 15ull) / 16; g += kPlaceThreads) {
+      const uint4 kw = *(const uint4*)(keys8 + g * 16);
+      const uint32_t w[4] = {kw.x, kw.y, kw.z, kw.w};
+#pragma unroll
+      for (uint32_t x = 0; x < 16; ++x) {
+        const uint64_t p = g * 16 + x;
+        if (p >= c0 && p < c1) atomicAdd(&lcnt[key_byte(w, x)], 1u);
+      }
+    }
+    __syncthreads();
+    uint32_t lex = 0;
+    if (bt) lex = scan256_wave(lcnt[tid], wsum);
+    __syncthreads();
+    if (bt) {
+      for (uint32_t w = 0; w < (tid >> 6); ++w) lex += wsum[w];
+      lstart[tid] = lex;
+      lpos[tid] = lex;
+    }
+    __syncthreads();
+    for (uint64_t g = c0 / 16 + tid; g < (c1 + 15ull) / 16; g += kPlaceThreads) {
+      const uint4 kw = *(const uint4*)(keys8 + g * 16);
+      const uint4* vp = (const uint4*)(vals + g * 16);
+      const uint4 v0 = vp[0], v1 = vp[1], v2 = vp[2], v3 = vp[3];
+      const uint32_t w[4] = {kw.x, kw.y, kw.z, kw.w};
+      const uint32_t v[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                              v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+#pragma unroll
+      for (uint32_t x = 0; x < 16; ++x) {
+        const uint64_t p = g * 16 + x;
+        if (p >= c0 && p < c1) {
+          const uint32_t bk = key_byte(w, x);
+          const uint32_t l = atomicAdd(&lpos[bk], 1u);
+          stage[l] = v[x];
+          sbk[l] = (uint8_t)bk;
+        }
+      }
+    }
+    __syncthreads();
+    for (uint32_t l = tid; l < c1 - c0; l += kPlaceThreads) {
+      const uint32_t bk = sbk[l];
+      sorted[cur[bk] + (l - lstart[bk])] = stage[l];
+    }
+    __syncthreads();
+    if (bt) cur[tid] += lcnt[tid];
+  }
 }
 
 // Row-range index.  A blocked Bloom filter of the hashes of rows [r0, r1):
@@ -498,10 +798,19 @@ __global__ __launch_bounds__(256) void index_mixed_kernel(const uint32_t* __rest
 // Bucketed build, after the sort by bucket (16-bit keys, entry values):
 // bstart[b] = first sorted entry of bucket b (bstart[nb] = total), written
 // where the bucket changes (one coalesced pass over the keys).
+// runinfo of an entry in a run of g >= 2 equal hashes: the run's first
+// member in ents (bits 0-31), g (bits 32-44), and, when the run's members
+// are in row order (kRunSorted), the entry's own rank in it (bits 45-57)
+constexpr uint32_t kRunGMask = 0x1FFFu;
+constexpr uint32_t kRunRankShift = 45;
+constexpr uint64_t kRunSorted = 1ull << 58;
+constexpr uint32_t kRowSortedRun = 32;  // longer runs of the bucketed build keep their arrival order
 constexpr uint32_t kBucketCap = 3072;    // entries of one bucket grouped in LDS
 constexpr uint32_t kBucketSlots = 4096;  // its LDS hash table (load <= 0.75)
 constexpr int kBucketThreads = 256;
 constexpr uint32_t kBucketPer = kBucketCap / kBucketThreads;
+static_assert(kSuper % kXcds == 0, "super-bins per XCD");
+static_assert(kBucketSlots * sizeof(uint64_t) >= kBucketCap * sizeof(uint32_t), "row-order pass: entries in tkey's space");
 static_assert(kBucketCap % kBucketThreads == 0 && kBucketSlots % kBucketThreads == 0 && kBucketCap < 4096,
               "bucket table: group start and size packed as 12 + 12 bits");
 
@@ -657,6 +966,20 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
     if (tid == kBucketThreads - 1) tcnt[kBucketSlots] |= run << 12;
   }
   __syncthreads();
+  // A group of g <= kRowSortedRun is stored in row order: the entries are
+  // laid out in LDS by their arrival rank (in tkey's space, free now), each
+  // counts the members of lower row (a hash is in a row at most once), and
+  // its runinfo carries that rank, so the pairs kernel reads only the
+  // members after it -- the partners j > i (sum g (g - 1) / 2 member reads
+  // instead of sum g^2).  Longer groups keep the arrival order (rank flag 0:
+  // every member is read and filtered, as the full build's runs are).
+  uint32_t* grp = reinterpret_cast<uint32_t*>(tkey);
+#pragma unroll
+  for (uint32_t r = 0; r < kBucketPer; ++r) {
+    const uint32_t q = tid + r * kBucketThreads;
+    if (q < n) grp[(tcnt[slot[r]] >> 12) + rank[r]] = ent[r];
+  }
+  __syncthreads();
 #pragma unroll
   for (uint32_t r = 0; r < kBucketPer; ++r) {
     const uint32_t q = tid + r * kBucketThreads;
@@ -664,14 +987,23 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
       const uint32_t t = tcnt[slot[r]];
       const uint32_t start = t >> 12, g = t & 0xFFFu;
       const uint32_t e = ent[r];
-      if (ents16) ((uint16_t*)ents)[lo + start + rank[r]] = (uint16_t)(e >> kbits);
-      else ents[lo + start + rank[r]] = e;
+      uint32_t rk = rank[r];
+      uint64_t sorted_flag = 0;
+      if (g >= 2 && g <= kRowSortedRun) {
+        const uint32_t row = e >> kbits;
+        rk = 0;
+        for (uint32_t x = 0; x < g; ++x) rk += (grp[start + x] >> kbits) < row ? 1u : 0u;
+        sorted_flag = kRunSorted;
+      }
+      if (ents16) ((uint16_t*)ents)[lo + start + rk] = (uint16_t)(e >> kbits);
+      else ents[lo + start + rk] = e;
       if (g > max_run) {
         atomicOr(&flags[0], 1u);
         continue;
       }
       runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] =
-          g >= 2 ? ((uint64_t)(lo + start) | ((uint64_t)g << 32)) : 0ull;
+          g >= 2 ? ((uint64_t)(lo + start) | ((uint64_t)g << 32) | ((uint64_t)rk << kRunRankShift) | sorted_flag)
+                 : 0ull;
     }
   }
 }
@@ -741,16 +1073,18 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
       if (over) break;
       const uint64_t info = info_next;
       info_next = k + kRowThreads < la ? ri[k + kRowThreads] : 0ull;
-      const uint32_t g = (uint32_t)(info >> 32);
+      const uint32_t g = (uint32_t)(info >> 32) & kRunGMask;
       if (g < 2) continue;
-      const uint32_t st = (uint32_t)info;
+      // a run in row order: only the members after row i's own (j > i)
+      const uint32_t st = (uint32_t)info, end = st + g;
+      const uint32_t q_first = (info & kRunSorted) ? st + 1u + ((uint32_t)(info >> kRunRankShift) & kRunGMask) : st;
       bool stop = false;
-      for (uint32_t q0 = st; q0 < st + g && !stop; q0 += kMemberLoads) {
+      for (uint32_t q0 = q_first; q0 < end && !stop; q0 += kMemberLoads) {
         uint32_t jv[kMemberLoads];
 #pragma unroll
         for (uint32_t u = 0; u < kMemberLoads; ++u) {
           const uint32_t q = q0 + u;
-          jv[u] = q < st + g ? (E16 ? (uint32_t)((const uint16_t*)a.vals)[q] : a.vals[q] >> a.kbits) : jhi;
+          jv[u] = q < end ? (E16 ? (uint32_t)((const uint16_t*)a.vals)[q] : a.vals[q] >> a.kbits) : jhi;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kMemberLoads; ++u) {
@@ -815,6 +1149,12 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
 
 }  // namespace
 
+// GALAHGPU_INDEX_HIST_SAMPLE=0: the coarse histogram over every entry at any size
+static bool hist_sampling() {
+  const char* e = getenv("GALAHGPU_INDEX_HIST_SAMPLE");
+  return !(e && *e == '0');
+}
+
 hipError_t index_fill(const IndexBuild& b, hipStream_t st) {
   hipError_t e = hipMemsetAsync(b.flags, 0, 4 * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
@@ -827,7 +1167,7 @@ hipError_t index_fill(const IndexBuild& b, hipStream_t st) {
     e = hipMemsetAsync(b.hist, 0, kCoarse * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(bucket_hist_kernel, dim3(std::max(1u, std::min<uint32_t>(b.n, 1024))), dim3(256), 0, st,
-                       b.sketches, b.lens, b.n, b.stride, info, b.hist);
+                       b.sketches, b.lens, b.n, b.stride, info, b.hist, hist_sampling() ? 1u : 0u);
     hipLaunchKernelGGL(bucket_base_kernel, dim3(1), dim3(kBaseThreads), 0, st, b.hist, info, b.bbase);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -883,8 +1223,46 @@ hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_
   return hipGetLastError();
 }
 
+static hipError_t index_sort_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_bound, hipStream_t st);
+
 hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_bound, hipStream_t st) {
   if (total == 0 || nb_bound == 0) return hipSuccess;
+  const uint32_t* nbuckets_d = b.bbase + kCoarse;
+  uint32_t* vout = (uint32_t*)b.vals_out;
+  if (b.split_cnt && !b.bloom) {  // split build: two placements instead of the fill and the sort
+    const dim3 rows((b.n + kXcds - 1) / kXcds * kXcds);
+    hipLaunchKernelGGL(split_keys_kernel, rows, dim3(256), 0, st, b.sketches, b.lens, b.n, b.stride,
+                       (const unsigned long long*)b.info, b.bbase, (uint16_t*)b.keys_in, b.split_cnt);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t bytes = b.sort_tmp_bytes;
+    e = hipcub::DeviceScan::ExclusiveSum(b.sort_tmp, bytes, b.split_cnt, b.split_off, (int)(kSuper * b.n + 1), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(split_scatter_kernel, rows, dim3(256), 0, st, (const uint16_t*)b.keys_in, b.lens, b.n,
+                       b.stride, b.kbits, b.split_cnt, b.split_off, (uint8_t*)b.keys_out, (uint32_t*)b.vals_in);
+    hipLaunchKernelGGL(superbin_count_kernel, dim3(kSuper * kSuperParts), dim3(256), 0, st,
+                       (const uint8_t*)b.keys_out, b.split_off, b.n, b.split_hist);
+    hipLaunchKernelGGL(superbin_place_kernel, dim3(kSuper * kSuperParts), dim3(kPlaceThreads), 0, st,
+                       (const uint8_t*)b.keys_out, (const uint32_t*)b.vals_in, b.split_off, b.n, b.split_hist,
+                       b.bstart, vout);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  } else {
+    hipError_t e = index_sort_buckets(b, total, nb_bound, st);
+    if (e != hipSuccess) return e;
+  }
+  // the entries land in keys_in (free after the sort), as with the run pass
+  const uint32_t per_xcd = (nb_bound + kXcds - 1) / kXcds;
+  hipLaunchKernelGGL(index_bucket_kernel, dim3(per_xcd * kXcds), dim3(kBucketThreads), 0, st, vout, b.bstart,
+                     nbuckets_d, total, b.sketches, b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in,
+                     index_ents16(b.n) ? 1u : 0u, b.flags);
+  return hipGetLastError();
+}
+
+// The bucketed build's fill and 16-bit sort (the row-range index, whose
+// kept entries are compacted, or GALAHGPU_INDEX_SPLIT=0), then the bucket
+// bounds.
+static hipError_t index_sort_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_bound, hipStream_t st) {
   const uint32_t* nbuckets_d = b.bbase + kCoarse;
   if (!b.bloom)
     hipLaunchKernelGGL(index_fill_kernel<true>, dim3(std::min<uint32_t>(b.n, 16384)), dim3(256), 0, st, b.sketches,
@@ -908,14 +1286,14 @@ hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(bucket_bounds_kernel, dim3((uint32_t)std::min<uint64_t>(16384, total / 2048 + 1)), dim3(256), 0,
                      st, (const uint16_t*)b.keys_out, total, nbuckets_d, b.bstart);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  // the entries land in keys_in (free after the sort), as with the run pass
-  const uint32_t per_xcd = (nb_bound + kXcds - 1) / kXcds;
-  hipLaunchKernelGGL(index_bucket_kernel, dim3(per_xcd * kXcds), dim3(kBucketThreads), 0, st, vout, b.bstart,
-                     nbuckets_d, total, b.sketches, b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in,
-                     index_ents16(b.n) ? 1u : 0u, b.flags);
   return hipGetLastError();
+}
+
+size_t index_split_tmp_bytes(uint32_t n) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                         (int)(kSuper * n + 1));
+  return bytes;
 }
 
 uint32_t index_bucket_bound(uint64_t entries) {

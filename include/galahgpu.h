@@ -371,14 +371,19 @@ gg_status gg_pair_paths(const gg_ctx* ctx, uint64_t* paths);
  *                                (GALAHGPU_INFLATE=device) handed back to the
  *                                host threads (several members per file,
  *                                FASTQ, a stream it could not chain, a CRC
- *                                mismatch) */
+ *                                mismatch)
+ *   GG_FALLBACK_SKETCH_SET       genomes whose candidate list outgrew its
+ *                                region and were re-run in set mode (one
+ *                                insert per distinct candidate; a subset of
+ *                                the passes GG_FALLBACK_SKETCH_RETRY counts) */
 enum {
   GG_FALLBACK_INDEX_TO_GATE = 0,
   GG_FALLBACK_INDEX_FULL_SORT = 1,
   GG_FALLBACK_PEER_STAGED = 2,
   GG_FALLBACK_SKETCH_RETRY = 3,
   GG_FALLBACK_INFLATE_HOST = 4,
-  GG_FALLBACK_COUNT = 5
+  GG_FALLBACK_SKETCH_SET = 5,
+  GG_FALLBACK_COUNT = 6
 };
 gg_status gg_fallbacks(const gg_ctx* ctx, uint64_t* counts /* [GG_FALLBACK_COUNT] */);
 /* links[a * M + b] (M = gg_device_count) for members a and b: 1 when member

@@ -10,7 +10,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 out=$1; shift
 mkdir -p "$out"
-rx='index_|bucket_|onesweep|pair_keys|pair_gather|sort|merge'
+rx='index_|bucket_|split_|superbin_|onesweep|pair_keys|pair_gather|sort|merge|scan'
 sets=(
   "GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_WAVES SQ_BUSY_CYCLES SQ_INSTS_LDS_LOAD_BANDWIDTH SQ_INSTS_VMEM_RD"
   "GRBM_GUI_ACTIVE FETCH_SIZE"

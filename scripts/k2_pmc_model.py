@@ -30,7 +30,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N_SIMD, N_CU = 1024, 256
 HBM_PEAK = 8.0e12
-NAMES = ("index_scan", "bucket_hist", "bucket_base", "index_fill_range", "index_fill", "bucket_bounds",
+NAMES = ("index_scan", "bucket_hist", "bucket_base", "index_fill_range", "index_fill", "bucket_bounds", "split_keys",
+         "split_scatter", "superbin_count", "superbin_place",
          "index_bucket", "index_pairs", "index_runs", "index_mixed", "pair_keys", "pair_gather", "bloom_build")
 
 
@@ -43,6 +44,8 @@ def short(name):
             return "index_sort"  # the bucketed build's 16-bit key sort (histogram, scan, 2 passes)
         if "onesweep" in name:
             return "index_sort_full"  # the full build's 32-bit sort (fallback)
+        if "scan" in name:
+            return "split_scan"  # the split build's scan of the per-row super-bin counts
         return "pair_sort"  # the passing pairs' sort (merge-sort path below 2^20 items)
     return "not_k2: " + name[:40]  # torch kernels of bench.py's own analysis (torch.unique)
 

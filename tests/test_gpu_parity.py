@@ -121,6 +121,29 @@ def test_repeated_kmers_dedup_in_candidate_list():
         assert lens[g] == len(exp) == 1000 and (sk[g][:lens[g]] == exp).all(), g
 
 
+@pytest.mark.parametrize("max_batch", ["0", "2"])
+def test_tandem_repeats_switch_to_set_mode(monkeypatch, max_batch):
+    """Tandem repeats (a 20-60 kb stretch 8-40 times over): every distinct
+    candidate is appended once per copy, so once tau admits s distinct values
+    the append-mode list outgrows its region and the finalize re-runs the
+    genome at the same tau in set mode (kSketchRetrySet: one atomicCAS insert
+    per distinct value, finch's insert-if-new).  The sketches equal the
+    oracle's, through one batch and through batches of 2 genomes
+    (GALAHGPU_K1_MAX_BATCH), next to genomes that need no retry."""
+    rng = np.random.default_rng(13)
+    rnd = lambda n: np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)].tobytes()
+    genomes = [[rnd(20000) * 10], [rnd(120000)], [rnd(5000) * 40], [rnd(60000) * 8, rnd(3000)], [rnd(90000)]]
+    monkeypatch.setenv("GALAHGPU_K1_MAX_BATCH", max_batch)
+    with ga.Context(k=21, sketch_size=1000) as ctx:
+        sk, lens = ctx.sketch(ga.pack_records(genomes))
+        fb = ctx.fallbacks()
+        assert fb["sketch_set"] >= 3 and fb["sketch_retry"] > 0, fb
+        assert "set-mode genomes %d" % fb["sketch_set"] in ctx.info_line()
+    for g, recs in enumerate(genomes):
+        exp = oracle.sketch_records(recs)
+        assert lens[g] == len(exp) == 1000 and (sk[g][:lens[g]] == exp).all(), g
+
+
 def test_other_k_and_s():
     rng = np.random.default_rng(5)
     recs = [[np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 20000)].tobytes()] for _ in range(3)]
