@@ -54,7 +54,7 @@ ISSUE_MODEL = os.path.join(ROOT, "profiles", "r04_k1_issue_model.json")
 # K2's per-kernel PMC summary (HBM bytes from FETCH_SIZE x 2 and WRITE_SIZE,
 # VALU issue share, LDS-array utilisation) of the bucketed inverted index:
 # scripts/k2_pmc.sh + scripts/k2_pmc_model.py
-K2_PMC = os.path.join(ROOT, "profiles", "r04_k2_pmc.json")
+K2_PMC = os.path.join(ROOT, "profiles", "r05_k2_pmc.json")
 # the device-inflate ingest kernels' counters at C2 (scripts/ingest_pmc.sh + ingest_pmc_model.py)
 INGEST_PMC = os.path.join(ROOT, "profiles", "r05_ingest_pmc.json")
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
@@ -148,7 +148,7 @@ def k2_pmc(config):
     keep = ("dispatches", "ms", "hbm_bytes", "hbm_GBps", "hbm_frac", "valu_frac_guide", "lds_util", "l2_hit",
             "bound", "bound_frac")
     ks = {k: {x: e[x] for x in keep if x in e} for k, e in c["kernels"].items()}
-    return {"source": "profiles/r04_k2_pmc.json (%s, one step; raw: %s)" % (config, c.get("source")), "kernels": ks,
+    return {"source": "profiles/r05_k2_pmc.json (%s, one step; raw: %s)" % (config, c.get("source")), "kernels": ks,
             "peaks": "VALU: 2 cycles per wave64 instruction per SIMD (MI355X_MICROARCH.md); LDS: array busy cycles "
                      "per CU; HBM: 8 TB/s, bytes = FETCH_SIZE x 2 + WRITE_SIZE"}
 
@@ -179,6 +179,11 @@ def k2_algorithmic_bytes(d_sk, d_len, n, s):
     cnt = cnt[cnt >= 2].to(torch.float64)
     g2 = float((cnt * cnt).sum())
     runs = int(cnt.numel())
+    # member reads of the pairs kernel: a run of g <= 32 is stored in row
+    # order and each member reads only the members after it (g (g - 1) / 2
+    # per run); a longer run is read whole by every member (g^2)
+    short = cnt <= 32
+    members = float((cnt[short] * (cnt[short] - 1) / 2).sum() + (cnt[~short] * cnt[~short]).sum())
     del mask
     m = 2 if n <= 65536 else 4
     per = {
@@ -201,10 +206,10 @@ def k2_algorithmic_bytes(d_sk, d_len, n, s):
         })
     per.update({
         "index_bucket": (4.0 + 8.0 + m + 8.0) * E,    # entry, its hash, member id and runinfo written
-        "index_pairs": 8.0 * E + m * g2,              # runinfo of every entry; g members of each of its runs
+        "index_pairs": 8.0 * E + m * members,         # runinfo of every entry; the members after it in its run
     })
     return {"bytes": sum(per.values()), "per_kernel": per, "entries": E, "slots": S, "shared_runs": runs,
-            "sum_g2": g2}
+            "sum_g2": g2, "member_reads": members}
 
 
 def roofline_k2(model, kst_pr, config):
@@ -218,7 +223,7 @@ def roofline_k2(model, kst_pr, config):
            "algorithmic_bytes": round(model["bytes"]),
            "algorithmic_bytes_per_kernel": {k: round(v) for k, v in model["per_kernel"].items()},
            "entries": model["entries"], "slots": model["slots"], "shared_runs": model["shared_runs"],
-           "sum_g2": round(model["sum_g2"]),
+           "sum_g2": round(model["sum_g2"]), "member_reads": round(model["member_reads"]),
            "kernel": ("K2: bucketed inverted index (index_scan, bucket_hist, bucket_base, split_keys, scan, "
                       "split_scatter, superbin_count/place, index_bucket) + index_pairs_kernel" if index_split_on() else
                       "K2: bucketed inverted index (index_scan, bucket_hist, bucket_base, index_fill, 16-bit onesweep "

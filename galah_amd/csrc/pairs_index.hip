@@ -379,7 +379,7 @@ __global__ __launch_bounds__(256) void split_scatter_kernel(const uint16_t* __re
 }
 
 // The super-bin sort: super-bin D's entries [off[D n], off[(D + 1) n]) are
-// cut into kSuperParts equal slices, one 256-thread workgroup each (a
+// cut into up to kSuperParts equal slices, one workgroup each (a
 // workgroup per super-bin left the chip at one workgroup per CU: 0.57 ms at
 // C5).  A slice is read in groups of 16 entries (one 16-byte load of keys8,
 // four of vals; groups aligned to 16 entries, the slice ends masked).
@@ -390,24 +390,24 @@ __global__ __launch_bounds__(256) void split_scatter_kernel(const uint16_t* __re
 //                   slice's entries of bucket x follow those of earlier
 //                   slices (order inside a bucket is free: index_bucket
 //                   groups by hash)
-constexpr uint32_t kSuperParts = 16;
+constexpr uint32_t kSuperParts = 16;  // slices per super-bin at most (fewer for small inputs)
 
 __device__ __forceinline__ void super_slice(const uint32_t* __restrict__ off, uint32_t n, uint32_t D, uint32_t part,
-                                            uint32_t& a, uint32_t& e) {
+                                            uint32_t parts, uint32_t& a, uint32_t& e) {
   const uint32_t s0 = off[(uint64_t)D * n], s1 = off[(uint64_t)(D + 1) * n];
-  a = s0 + (uint32_t)((uint64_t)(s1 - s0) * part / kSuperParts);
-  e = s0 + (uint32_t)((uint64_t)(s1 - s0) * (part + 1) / kSuperParts);
+  a = s0 + (uint32_t)((uint64_t)(s1 - s0) * part / parts);
+  e = s0 + (uint32_t)((uint64_t)(s1 - s0) * (part + 1) / parts);
 }
 
-// XCD-aware: the kSuperParts slices of a super-bin run on one XCD (blockIdx
+// XCD-aware: the slices of a super-bin run on one XCD (blockIdx
 // % kXcds), so the bucket-ordered lines of its output are written through
 // one L2 (slices dealt round-robin over the XCDs wrote each line from up to
 // 8 L2s)
-__device__ __forceinline__ void super_block(uint32_t& D, uint32_t& part) {
+__device__ __forceinline__ void super_block(uint32_t parts, uint32_t& D, uint32_t& part) {
   constexpr uint32_t per_xcd = kSuper / kXcds;
   const uint32_t j = blockIdx.x / kXcds;
-  D = (blockIdx.x % kXcds) * per_xcd + j / kSuperParts;
-  part = j % kSuperParts;
+  D = (blockIdx.x % kXcds) * per_xcd + j / parts;
+  part = j % parts;
 }
 
 __device__ __forceinline__ uint32_t key_byte(const uint32_t (&w)[4], uint32_t e) {
@@ -416,12 +416,12 @@ __device__ __forceinline__ uint32_t key_byte(const uint32_t (&w)[4], uint32_t e)
 
 __global__ __launch_bounds__(256) void superbin_count_kernel(const uint8_t* __restrict__ keys8,
                                                              const uint32_t* __restrict__ off, uint32_t n,
-                                                             uint32_t* __restrict__ shist) {
+                                                             uint32_t parts, uint32_t* __restrict__ shist) {
   __shared__ uint32_t h[kSuper];
   const uint32_t tid = threadIdx.x;
   uint32_t D, part, a, e;
-  super_block(D, part);
-  super_slice(off, n, D, part, a, e);
+  super_block(parts, D, part);
+  super_slice(off, n, D, part, parts, a, e);
   h[tid] = 0u;
   __syncthreads();
   for (uint64_t g = a / 16 + tid; g < (e + 15ull) / 16; g += 256) {
@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256) void superbin_count_kernel(const uint8_t* __re
     }
   }
   __syncthreads();
-  shist[((uint64_t)D * kSuperParts + part) * kSuper + tid] = h[tid];
+  shist[((uint64_t)D * parts + part) * kSuper + tid] = h[tid];
 }
 
 // superbin_place stages a chunk of up to kPlaceChunk entries in LDS in bucket
@@ -461,6 +461,7 @@ __device__ __forceinline__ uint32_t scan256_wave(uint32_t v, uint32_t* wsum) {
 __global__ __launch_bounds__(kPlaceThreads) void superbin_place_kernel(const uint8_t* __restrict__ keys8,
                                                                        const uint32_t* __restrict__ vals,
                                                                        const uint32_t* __restrict__ off, uint32_t n,
+                                                                       uint32_t parts,
                                                                        const uint32_t* __restrict__ shist,
                                                                        uint32_t* __restrict__ bstart,
                                                                        uint32_t* __restrict__ sorted) {
@@ -470,14 +471,13 @@ __global__ __launch_bounds__(kPlaceThreads) void superbin_place_kernel(const uin
   const uint32_t tid = threadIdx.x;
   const bool bt = tid < kSuper;  // (threads 0-255: one bucket each)
   uint32_t D, part, a, e;
-  super_block(D, part);
-  super_slice(off, n, D, part, a, e);
+  super_block(parts, D, part);
+  super_slice(off, n, D, part, parts, a, e);
   // bucket tid: its count over all slices and over the slices before this one
   uint32_t tot = 0, before = 0, ex = 0;
   if (bt) {
-    const uint32_t* hd = shist + (uint64_t)D * kSuperParts * kSuper + tid;
-#pragma unroll
-    for (uint32_t q = 0; q < kSuperParts; ++q) {
+    const uint32_t* hd = shist + (uint64_t)D * parts * kSuper + tid;
+    for (uint32_t q = 0; q < parts; ++q) {
       const uint32_t c = hd[q * kSuper];
       tot += c;
       before += q < part ? c : 0u;
@@ -489,7 +489,7 @@ __global__ __launch_bounds__(kPlaceThreads) void superbin_place_kernel(const uin
     uint32_t start = off[(uint64_t)D * n] + ex;
     for (uint32_t w = 0; w < (tid >> 6); ++w) start += wsum[w];
     if (part == 0) bstart[D * kSuper + tid] = start;
-    if (D == kSuper - 1 && part == kSuperParts - 1 && tid == 0) bstart[(uint64_t)kSuper * kSuper] = e;
+    if (D == kSuper - 1 && part == parts - 1 && tid == 0) bstart[(uint64_t)kSuper * kSuper] = e;
     cur[tid] = start + before;
   }
   for (uint32_t c0 = a; c0 < e; c0 += kPlaceChunk) {
@@ -807,11 +807,9 @@ constexpr uint64_t kRunSorted = 1ull << 58;
 constexpr uint32_t kRowSortedRun = 32;  // longer runs of the bucketed build keep their arrival order
 constexpr uint32_t kBucketCap = 3072;    // entries of one bucket grouped in LDS
 constexpr uint32_t kBucketSlots = 4096;  // its LDS hash table (load <= 0.75)
-constexpr int kBucketThreads = 256;
-constexpr uint32_t kBucketPer = kBucketCap / kBucketThreads;
 static_assert(kSuper % kXcds == 0, "super-bins per XCD");
 static_assert(kBucketSlots * sizeof(uint64_t) >= kBucketCap * sizeof(uint32_t), "row-order pass: entries in tkey's space");
-static_assert(kBucketCap % kBucketThreads == 0 && kBucketSlots % kBucketThreads == 0 && kBucketCap < 4096,
+static_assert(kBucketCap < 4096,
               "bucket table: group start and size packed as 12 + 12 bits");
 
 __global__ __launch_bounds__(256) void bucket_bounds_kernel(const uint16_t* __restrict__ keys, uint64_t total,
@@ -857,6 +855,7 @@ __global__ __launch_bounds__(256) void bucket_bounds_kernel(const uint16_t* __re
 // its runinfo slot (group start and size g >= 2, or 0) as index_runs_kernel
 // does.  A bucket over kBucketCap entries sets flags[3] (the host rebuilds
 // with the full sort).
+template <int kBucketThreads>
 __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
     const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ nbuckets_p,
     uint64_t total, const uint64_t* __restrict__ sk, uint32_t stride, uint32_t kbits,
@@ -864,6 +863,8 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
     uint32_t* __restrict__ flags) {
   __shared__ uint64_t tkey[kBucketSlots];
   __shared__ uint32_t tcnt[kBucketSlots + 1];  // group size; after the scan start << 12 | size
+  constexpr uint32_t kBucketPer = kBucketCap / kBucketThreads;
+  static_assert(kBucketCap % kBucketThreads == 0 && kBucketSlots % kBucketThreads == 0, "bucket table");
   __shared__ uint32_t wsum[kBucketThreads / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t kmask = (1u << kbits) - 1u;
@@ -1240,10 +1241,15 @@ hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(split_scatter_kernel, rows, dim3(256), 0, st, (const uint16_t*)b.keys_in, b.lens, b.n,
                        b.stride, b.kbits, b.split_cnt, b.split_off, (uint8_t*)b.keys_out, (uint32_t*)b.vals_in);
-    hipLaunchKernelGGL(superbin_count_kernel, dim3(kSuper * kSuperParts), dim3(256), 0, st,
-                       (const uint8_t*)b.keys_out, b.split_off, b.n, b.split_hist);
-    hipLaunchKernelGGL(superbin_place_kernel, dim3(kSuper * kSuperParts), dim3(kPlaceThreads), 0, st,
-                       (const uint8_t*)b.keys_out, (const uint32_t*)b.vals_in, b.split_off, b.n, b.split_hist,
+    // slices per super-bin: ~1.5 LDS chunks each (C5: 16; C3's 39k-entry
+    // super-bins: 2 -- 16 slices of 2.4k entries took 0.12 ms there, mostly
+    // per-workgroup latency)
+    const uint32_t parts = (uint32_t)std::max<uint64_t>(
+        1, std::min<uint64_t>(kSuperParts, total / ((uint64_t)kSuper * 3 * kPlaceChunk / 2)));
+    hipLaunchKernelGGL(superbin_count_kernel, dim3(kSuper * parts), dim3(256), 0, st, (const uint8_t*)b.keys_out,
+                       b.split_off, b.n, parts, b.split_hist);
+    hipLaunchKernelGGL(superbin_place_kernel, dim3(kSuper * parts), dim3(kPlaceThreads), 0, st,
+                       (const uint8_t*)b.keys_out, (const uint32_t*)b.vals_in, b.split_off, b.n, parts, b.split_hist,
                        b.bstart, vout);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1253,9 +1259,17 @@ hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_
   }
   // the entries land in keys_in (free after the sort), as with the run pass
   const uint32_t per_xcd = (nb_bound + kXcds - 1) / kXcds;
-  hipLaunchKernelGGL(index_bucket_kernel, dim3(per_xcd * kXcds), dim3(kBucketThreads), 0, st, vout, b.bstart,
-                     nbuckets_d, total, b.sketches, b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in,
-                     index_ents16(b.n) ? 1u : 0u, b.flags);
+  // 1024 threads per bucket (GALAHGPU_BUCKET_THREADS=256|512: A/B; C5 index_bucket
+  // 1.76 ms at 256, 1.74 at 512, 1.63 at 1024)
+  const char* bt = getenv("GALAHGPU_BUCKET_THREADS");
+  const int threads = bt && *bt ? atoi(bt) : 1024;
+  auto go = [&](auto kern, int t) {
+    hipLaunchKernelGGL(kern, dim3(per_xcd * kXcds), dim3(t), 0, st, vout, b.bstart, nbuckets_d, total, b.sketches,
+                       b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in, index_ents16(b.n) ? 1u : 0u, b.flags);
+  };
+  if (threads == 256) go(index_bucket_kernel<256>, 256);
+  else if (threads == 512) go(index_bucket_kernel<512>, 512);
+  else go(index_bucket_kernel<1024>, 1024);
   return hipGetLastError();
 }
 

@@ -1,5 +1,5 @@
 """Per-kernel PMC summary of K2 (the bucketed inverted index and the passing
-pairs' device sort) over one bench step -> profiles/r04_k2_pmc.json.
+pairs' device sort) over one bench step -> profiles/r05_k2_pmc.json.
 
 Input: the directory scripts/k2_pmc.sh wrote for one config, one rocprofv3
 run per pass over `bench.py --steps 1 --warmup 0`: p1 SQ instruction and LDS
@@ -44,8 +44,10 @@ def short(name):
             return "index_sort"  # the bucketed build's 16-bit key sort (histogram, scan, 2 passes)
         if "onesweep" in name:
             return "index_sort_full"  # the full build's 32-bit sort (fallback)
+        if "scan" in name and "unsigned int" in name:
+            return "split_scan"  # the split build's scan of the per-row super-bin counts (u32)
         if "scan" in name:
-            return "split_scan"  # the split build's scan of the per-row super-bin counts
+            return "not_k2: u64 scan (K1 run index)"
         return "pair_sort"  # the passing pairs' sort (merge-sort path below 2^20 items)
     return "not_k2: " + name[:40]  # torch kernels of bench.py's own analysis (torch.unique)
 
@@ -106,7 +108,7 @@ def summarise(per):
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--out")]
-    out_path = os.path.join(ROOT, "profiles", "r04_k2_pmc.json")
+    out_path = os.path.join(ROOT, "profiles", "r05_k2_pmc.json")
     for a in sys.argv[1:]:
         if a.startswith("--out="):
             out_path = a.split("=", 1)[1]
