@@ -833,7 +833,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
 }
 
 // One workgroup per segment, its output built in order in steps of up to
-// 1024 tokens / kExpandBytes bytes.  The segment's last 32 KB of output stay
+// kExpandThreads tokens / kExpandBytes bytes.  The segment's last 32 KB of output stay
 // in an LDS ring (u16 per byte: a literal, or a back-reference to before
 // the segment as its distance from the segment's start), so every
 // back-reference inside the segment is an LDS read: a step's bytes are
@@ -843,8 +843,19 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
 // pointer jumping, and the step goes to val (coalesced) and to the ring.
 // So pointers left in val reach only into earlier segments and the resolve
 // chains are short.
-constexpr int kExpandThreads = 1024;
-constexpr uint32_t kExpandBytes = 8192;
+// 512 threads and steps of <= 4000 bytes: 80 KB of LDS, two workgroups per
+// CU, one's barriers overlapping the other's work (1024 threads and 8 KB
+// steps, one per CU: 2.20 ms per C2 batch; this: 1.81; 1024 threads with
+// 4000-byte steps: 2.34).  (A/B builds: scripts/ab_lib.sh with
+// -DGG_EXPAND_THREADS=... -DGG_EXPAND_BYTES=...)
+#ifndef GG_EXPAND_THREADS
+#define GG_EXPAND_THREADS 512
+#endif
+#ifndef GG_EXPAND_BYTES
+#define GG_EXPAND_BYTES 4000
+#endif
+constexpr int kExpandThreads = GG_EXPAND_THREADS;
+constexpr uint32_t kExpandBytes = GG_EXPAND_BYTES;
 constexpr uint32_t kRing = 32768;          // the DEFLATE window
 constexpr uint32_t kIntra = 0x40000000u;   // (batch text < 2^30 bytes: pointers leave bit 30 clear)
 constexpr uint16_t kRingPtr = 0x8000u;     // ring entry: pointer to o0 - 1 - (entry & 0x7FFF)
