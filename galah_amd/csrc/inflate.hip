@@ -566,9 +566,15 @@ __device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restri
 #ifndef GG_DECODE_MIN_WAVES
 #define GG_DECODE_MIN_WAVES 1
 #endif
-// (30 KB + the static tables ~10 KB: four waves per CU; a zlib -6 block of
-// FASTA is 24-27 KB)
-constexpr uint32_t kStageWords = 30 * 1024 / 4;
+// (10 KB + the static tables ~10 KB: eight waves per CU, two per SIMD as the
+// 174 VGPRs allow; a zlib -6 block of FASTA, 24-27 KB, takes three windows.
+// C2 files per call: 30 KB stages (one wave per SIMD) 0.063-0.064 s, 18 KB
+// 0.063-0.064, 14 KB 0.061-0.063, 10 KB 0.060-0.061.  A/B builds:
+// scripts/ab_lib.sh ... -DGG_STAGE_KB=14)
+#ifndef GG_STAGE_KB
+#define GG_STAGE_KB 10
+#endif
+constexpr uint32_t kStageWords = GG_STAGE_KB * 1024 / 4;
 template <bool kStaged>
 __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decode_kernel(InflateDecode a) {
   extern __shared__ uint32_t stage[];  // (kStaged: kStageWords words)
@@ -617,6 +623,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
   uint32_t status = kDecOk, fin = 0;
   for (;;) {
     const uint64_t blk0 = pos;  // (this block's start)
+    const uint64_t n_out0 = n_out, out_bytes0 = out_bytes;  // (the tokens and bytes before it)
     if (pos == end) {
       status = kDecOk;
       break;
@@ -748,8 +755,13 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       const uint64_t e_end = sE[c_end];
       const uint32_t st_end = sSt[c_end];
       if (overrun) {  // (the host decodes again from this block's start, the tokens before it kept)
+        // a block decoded in windows has its earlier windows' tokens counted
+        // already: they are dropped with the block (kept, the host's redo
+        // from blk0 appended them a second time)
         status = kDecOverrun;
         pos = blk0;
+        n_out = n_out0;
+        out_bytes = out_bytes0;
         stop_blk = true;
         break;
       }
