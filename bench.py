@@ -682,6 +682,15 @@ def run_lib(a, world, rank):
             cpu = cpu_baseline(sample, a.genome_len, d_sk.cpu().numpy().view(np.uint64),
                                d_len.cpu().numpy().view(np.uint32), a.k, s, min_ani, N, a.cpu_budget_s)
         del d_sk, d_len
+        # the headline workload's context and inputs are released before the
+        # files leg, which is a separate call as galah makes it in a fresh
+        # process (with the C3 context and its ~10 GB of inputs still held, the
+        # same calls measured 0.073 s against 0.061-0.065 in a fresh process:
+        # scripts/files_data_ab.py, gpurun_out r6e/r6f)
+        ctx.close()
+        ctx = None
+        del shards, keep, d_words, runs
+        torch.cuda.empty_cache()
         files = None
         want_files = a.files if a.files is not None else (a.config == "c3")
         if world == 1 and M == 1 and want_files:
@@ -712,7 +721,6 @@ def run_lib(a, world, rank):
             "downstream": downstream,
             "files": files,
         }
-        ctx.close()
     if world > 1:
         dist.destroy_process_group()
     return line
