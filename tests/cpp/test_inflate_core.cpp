@@ -372,16 +372,36 @@ int main(int argc, char** argv) {
     if (starts.empty()) continue;
     // place: every byte a literal (bit 31) or a pointer to an earlier byte
     std::vector<uint32_t> val;
-    for (size_t b = 0; b < part.size(); ++b)
+    // (stats: bytes copied by matches, and the bytes the device's expand
+    // leaves to the resolve pass -- a copy whose source, followed inside its
+    // segment, lies before the segment -- and the 16-byte groups holding one)
+    std::vector<uint8_t> marker;
+    size_t match_bytes = 0;
+    for (size_t b = 0; b < part.size(); ++b) {
+      const size_t o0 = val.size();
       for (uint32_t t : part[b]) {
         if (!tok_is_match(t)) {
           val.push_back(0x80000000u | t);
+          marker.push_back(0);
         } else {
           const uint32_t len = tok_len(t), dist = tok_dist(t);
           const size_t at = val.size();
-          for (uint32_t i = 0; i < len; ++i) val.push_back((uint32_t)(at + i - dist));
+          for (uint32_t i = 0; i < len; ++i) {
+            const size_t src = at + i - dist;
+            val.push_back((uint32_t)src);
+            marker.push_back(src < o0 || marker[src] ? 1 : 0);
+          }
+          match_bytes += len;
         }
       }
+    }
+    size_t marker_bytes = 0, marker_groups = 0;
+    for (size_t g = 0; g * 16 < marker.size(); ++g) {
+      size_t m = 0;
+      for (size_t i = g * 16; i < std::min(marker.size(), g * 16 + 16); ++i) m += marker[i];
+      marker_bytes += m;
+      marker_groups += m ? 1 : 0;
+    }
     std::vector<uint8_t> got2(val.size());
     size_t max_chain = 0;
     for (size_t i = 0; i < val.size(); ++i) {
@@ -400,9 +420,10 @@ int main(int argc, char** argv) {
       continue;
     }
     printf("{\"file\": \"%s\", \"bytes\": %zu, \"gz_bytes\": %zu, \"starts_found\": %zu, \"starts_dropped\": %zu, "
-           "\"lanes\": %zu, \"tokens\": %zu, \"max_chain\": %zu, \"redo_rounds\": %zu, \"spans\": %zu, \"span_bits\": %zu, \"redo_bits\": %zu, \"windows\": %zu}\n",
+           "\"lanes\": %zu, \"tokens\": %zu, \"max_chain\": %zu, \"redo_rounds\": %zu, \"spans\": %zu, \"span_bits\": %zu, \"redo_bits\": %zu, \"windows\": %zu, "
+           "\"match_bytes\": %zu, \"marker_bytes\": %zu, \"marker_groups\": %zu}\n",
            argv[a], want.size(), gz.size(), found, dropped, starts.size(), toks.size(), max_chain, ss.rounds, ss.spans,
-           ss.span_bits, ss.redo_bits, ss.windows);
+           ss.span_bits, ss.redo_bits, ss.windows, match_bytes, marker_bytes, marker_groups);
   }
   if (failures) {
     fprintf(stderr, "%d failure(s)\n", failures);
