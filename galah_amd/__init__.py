@@ -757,10 +757,16 @@ def distances(genome_fasta_paths, min_ani, num_kmers, kmer_length, sketch_cache_
     sketch_cache_dir (not in galah) reuses sketches of
     unchanged genome files from earlier runs; the result is the same."""
     log = logging.getLogger("galah")
+    # At debug level the reference logs every compared pair
+    # (src/finch.rs:65-68): the call then asks for every pair (min_ani 0: the
+    # gate kernel emits all N (N - 1) / 2), logs each with its f64 distance and
+    # keeps those at or above min_ani, as the reference's loop does.
+    every = log.isEnabledFor(logging.DEBUG)
+    paths = list(genome_fasta_paths)
     try:
         ctx = _context(int(kmer_length), int(num_kmers))
         log.info("Sketching MinHash representations of each genome with finch ..")  # src/finch.rs:46
-        pairs, ani = ctx.precluster_files(list(genome_fasta_paths), float(np.float32(min_ani)),
+        pairs, ani = ctx.precluster_files(paths, 0.0 if every else float(np.float32(min_ani)),
                                           cache_dir=sketch_cache_dir)
     except GalahGpuError as e:
         # src/finch.rs:50
@@ -768,9 +774,45 @@ def distances(genome_fasta_paths, min_ani, num_kmers, kmer_length, sketch_cache_
     log.info("Finished sketching genomes")  # src/finch.rs:48
     log.info(ctx.info_line())  # device count, phase times, fallbacks (gg_info_line)
     cache = SortedPairGenomeDistanceCache()
+    if every:
+        thr = float(np.float32(min_ani))
+        for p in pairs:
+            i, j = int(p["i"]), int(p["j"])
+            d = ani_f64(int(p["common"]), int(p["total"]), int(kmer_length))
+            log.debug("Comparing %s and %s, distance %s", paths[i], paths[j], rust_f64(d))
+            if d >= thr:
+                cache.insert((i, j), np.float32(d))
+        return cache
     for p, a in zip(pairs, ani):
         cache.insert((int(p["i"]), int(p["j"])), np.float32(a))
     return cache
+
+
+def rust_f64(x):
+    """Rust's `{}` of an f64: the shortest round-trip digits, no exponent, no
+    trailing ".0" (1.0 -> "1", 0.0 -> "0")."""
+    x = float(x)
+    if x != x:
+        return "NaN"
+    if x in (float("inf"), float("-inf")):
+        return "inf" if x > 0 else "-inf"
+    r = repr(x)
+    if "e" in r or "E" in r:
+        m, e = r.lower().split("e")
+        neg = m.startswith("-")
+        m = m.lstrip("-")
+        digits = m.replace(".", "")
+        point = (m.index(".") if "." in m else len(m)) + int(e)
+        if point <= 0:
+            r = "0." + "0" * (-point) + digits
+        elif point >= len(digits):
+            r = digits + "0" * (point - len(digits))
+        else:
+            r = digits[:point] + "." + digits[point:]
+        r = ("-" if neg else "") + r
+    if r.endswith(".0"):
+        r = r[:-2]
+    return r
 
 
 class FinchPreclusterer(PreclusterDistanceFinder):

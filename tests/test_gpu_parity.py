@@ -63,6 +63,27 @@ def test_finch_rs_hello_world(golden, caplog):
     assert d2 == ga.SortedPairGenomeDistanceCache()
 
 
+def test_debug_logs_every_compared_pair(golden, caplog):
+    """src/finch.rs:65-68: at debug level every pair i < j is logged with its
+    f64 distance (Rust's `{}` formatting); the cache is the INFO-level one."""
+    paths = golden["paths"]
+    n = len(paths)
+    with caplog.at_level("INFO", logger="galah"):
+        d_info = ga.distances(paths, np.float32(0.9), 1000, 21)
+    caplog.clear()
+    with caplog.at_level("DEBUG", logger="galah"):
+        d_dbg = ga.distances(paths, np.float32(0.9), 1000, 21)
+    assert d_dbg == d_info and len(d_info.internal) == 161
+    lines = [r.getMessage() for r in caplog.records if r.name == "galah" and r.levelname == "DEBUG"]
+    assert len(lines) == n * (n - 1) // 2
+    table = {(int(i), int(j)): (int(c), int(t)) for (i, j, c, t, _a) in golden["pairs"]}
+    assert len(table) == len(lines)
+    want = [(i, j) for i in range(n) for j in range(i + 1, n)]  # (the reference's loop order)
+    for line, (i, j) in zip(lines, want):
+        c, t = table[(i, j)]
+        assert line == "Comparing %s and %s, distance %s" % (paths[i], paths[j], ga.rust_f64(oracle.ani(c, t))), line
+
+
 def test_precluster_files_matches_oracle(gpu_ctx, golden):
     min_ani = ga.parse_percentage(90)
     pairs, ani = gpu_ctx.precluster_files(golden["paths"], min_ani)
