@@ -697,8 +697,14 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
           }
           return true;
         };
-        if constexpr (kStaged) sa = decode_span_lds(stage, sbase, S, S, R, tab, sink, ck1, na, ba, Ea);
-        else sa = decode_span(in, S, S, R, tab, sink, ck1, na, ba, Ea);
+        // (a lane after the first starts kWarmBits early, so that its decode
+        // has most likely fallen into step with the true symbols by S and its
+        // first checkpoint agrees with the lane before: fewer second decodes,
+        // whose longest kept the whole wave waiting; its tokens before the
+        // first checkpoint are dropped as before)
+        const uint64_t S0 = j == 0 ? S : (S - bstart > kWarmBits ? S - kWarmBits : bstart);
+        if constexpr (kStaged) sa = decode_span_lds(stage, sbase, S0, S, R, tab, sink, ck1, na, ba, Ea);
+        else sa = decode_span(in, S0, S, R, tab, sink, ck1, na, ba, Ea);
         sink.flush();
       }
       phase(1);

@@ -958,9 +958,13 @@ GG_HD void span_layout(uint64_t body0, uint64_t span_end, uint32_t max_lanes, ui
 }
 
 // Per lane of a segment's decode: two token areas (the first decode, the
-// second) of span_cap(L) tokens each -- a decode of [S, R + 48) emits at
-// most one token per bit -- and span_cks(L) checkpoints (u64).
-GG_HD uint64_t span_cap(uint64_t L) { return (L + kCkBits + 3) / 4 * 4; }
+// second) of span_cap(L) tokens each -- a decode of [S - kWarmBits, R + 48)
+// emits at most one token per bit -- and span_cks(L) checkpoints (u64).
+#ifndef GG_DECODE_WARM_BITS  // (A/B builds: scripts/ab_lib.sh ... -DGG_DECODE_WARM_BITS=0)
+#define GG_DECODE_WARM_BITS 256
+#endif
+constexpr uint64_t kWarmBits = GG_DECODE_WARM_BITS;  // a lane's first decode starts this far before its span
+GG_HD uint64_t span_cap(uint64_t L) { return (L + kWarmBits + kCkBits + 3) / 4 * 4; }
 GG_HD uint64_t span_cks(uint64_t L) { return (L / kCkBits + 4) & ~1ull; }  // (even: areas stay 16-byte aligned)
 GG_HD uint64_t span_words(uint64_t L) { return 2 * span_cap(L) + 2 * span_cks(L); }  // (u32 words, even)
 // Scratch words the device decode of a segment of seg_bits bits needs (L
