@@ -13,6 +13,7 @@
 #pragma once
 
 #include <algorithm>
+#include <charconv>
 #include <cstdint>
 #include <cstdio>
 #include <functional>
@@ -101,9 +102,25 @@ inline void info(const std::string& line) {
   if (info_sink()) info_sink()(line);
 }
 
+// galah's debug! log: unset (the default level, info) logs nothing; set, it
+// receives src/finch.rs:65-68's line for every compared pair.
+inline std::function<void(const std::string&)>& debug_sink() {
+  static std::function<void(const std::string&)> sink;
+  return sink;
+}
+
+// Rust's `{}` of an f64: the shortest digits that read back the same value,
+// fixed notation (1.0 -> "1", 1e-7 -> "0.0000001")
+inline std::string rust_f64(double x) {
+  char buf[400];
+  const auto r = std::to_chars(buf, buf + sizeof buf, x, std::chars_format::fixed);
+  return std::string(buf, r.ptr);
+}
+
 namespace detail {
 // sketch + all pairs + threshold on an existing context; takes ownership of ctx
-inline SortedPairGenomeDistanceCache distances_on(gg_ctx* ctx, const std::vector<std::string>& paths, float min_ani) {
+inline SortedPairGenomeDistanceCache distances_on(gg_ctx* ctx, const std::vector<std::string>& paths, float min_ani,
+                                                  int kmer_length) {
   if (!ctx)
     throw std::runtime_error(std::string("Failed to sketch genomes with finch: ") + gg_thread_last_error());
   gg_set_host_threads(ctx, current_num_threads());
@@ -113,7 +130,11 @@ inline SortedPairGenomeDistanceCache distances_on(gg_ctx* ctx, const std::vector
   float* ani = nullptr;
   uint64_t n = 0;
   info("Sketching MinHash representations of each genome with finch ..");  // src/finch.rs:46
-  const gg_status st = gg_precluster_files(ctx, c_paths.data(), (uint32_t)c_paths.size(), min_ani, &pairs, &ani, &n);
+  // at debug level every pair is asked for (min_ani 0: the gate kernel emits
+  // all of them), logged with its f64 distance and kept if >= min_ani
+  const bool every = (bool)debug_sink();
+  const gg_status st = gg_precluster_files(ctx, c_paths.data(), (uint32_t)c_paths.size(), every ? 0.0f : min_ani,
+                                           &pairs, &ani, &n);
   if (st != GG_OK) {
     std::string msg = gg_last_error(ctx);
     gg_destroy(ctx);
@@ -123,7 +144,15 @@ inline SortedPairGenomeDistanceCache distances_on(gg_ctx* ctx, const std::vector
   char line[1024];
   if (gg_info_line(ctx, line, sizeof line) == GG_OK) info(line);
   SortedPairGenomeDistanceCache cache;
-  for (uint64_t i = 0; i < n; ++i) cache.insert({pairs[i].i, pairs[i].j}, ani[i]);  // src/finch.rs:70
+  for (uint64_t i = 0; i < n; ++i) {
+    if (every) {  // src/finch.rs:65-71
+      const double d = gg_ani_f64(pairs[i].common, pairs[i].total, kmer_length);
+      debug_sink()("Comparing " + paths[pairs[i].i] + " and " + paths[pairs[i].j] + ", distance " + rust_f64(d));
+      if (d >= (double)min_ani) cache.insert({pairs[i].i, pairs[i].j}, (float)d);
+    } else {
+      cache.insert({pairs[i].i, pairs[i].j}, ani[i]);  // src/finch.rs:70
+    }
+  }
   gg_free(pairs);
   gg_free(ani);
   gg_destroy(ctx);
@@ -137,14 +166,15 @@ inline SortedPairGenomeDistanceCache distances_on(gg_ctx* ctx, const std::vector
 inline SortedPairGenomeDistanceCache finch_distances(const std::vector<std::string>& paths, float min_ani,
                                                      size_t num_kmers, uint8_t kmer_length) {
   gg_status st = GG_OK;
-  return detail::distances_on(gg_create_multi(kmer_length, (uint32_t)num_kmers, 0, nullptr, 0, &st), paths, min_ani);
+  return detail::distances_on(gg_create_multi(kmer_length, (uint32_t)num_kmers, 0, nullptr, 0, &st), paths, min_ani,
+                              kmer_length);
 }
 
 // The same on one HIP device (ordinal; -1 = the current device).
 inline SortedPairGenomeDistanceCache finch_distances(const std::vector<std::string>& paths, float min_ani,
                                                      size_t num_kmers, uint8_t kmer_length, int device) {
   gg_status st = GG_OK;
-  return detail::distances_on(gg_create(kmer_length, (uint32_t)num_kmers, 0, device, &st), paths, min_ani);
+  return detail::distances_on(gg_create(kmer_length, (uint32_t)num_kmers, 0, device, &st), paths, min_ani, kmer_length);
 }
 
 // The same on a list of HIP ordinals (repeats allowed: several members on one GPU).
@@ -154,7 +184,7 @@ inline SortedPairGenomeDistanceCache finch_distances_on(const std::vector<int>& 
   gg_status st = GG_OK;
   return detail::distances_on(
       gg_create_multi(kmer_length, (uint32_t)num_kmers, 0, devices.data(), (uint32_t)devices.size(), &st), paths,
-      min_ani);
+      min_ani, kmer_length);
 }
 
 // src/finch.rs:4-24

@@ -72,6 +72,17 @@ static void test_hello_world(const std::string& dir) {
   galah::SortedPairGenomeDistanceCache e1;
   e1.insert({0, 1}, 0.9808188f);
   CHECK(d1 == e1);
+  // debug level (src/finch.rs:65-68): the compared pair logged with its f64
+  // distance, the same cache
+  std::vector<std::string> dbg;
+  galah::debug_sink() = [&](const std::string& line) { dbg.push_back(line); };
+  auto d3 = p.distances(paths);
+  galah::debug_sink() = nullptr;
+  CHECK(d3 == e1);
+  CHECK(dbg.size() == 1 && dbg[0] == "Comparing " + paths[0] + " and " + paths[1] + ", distance " +
+                                         galah::rust_f64(gg_ani_f64(502, 1000, 21)));
+  CHECK(galah::rust_f64(1.0) == "1" && galah::rust_f64(0.0) == "0" && galah::rust_f64(1e-7) == "0.0000001" &&
+        galah::rust_f64(0.5) == "0.5");
   auto d2 = galah::finch_distances(paths, 0.99f, 1000, 21);
   CHECK(d2.size() == 0);
   // one device by ordinal, and two members of device 0
