@@ -272,6 +272,7 @@ struct InflateDecode {
   // into LDS window by window; every stream read of the decode is an LDS
   // read), the rest read global memory
   uint32_t n_staged = 0;
+  uint32_t stage_words = 0;  // LDS stage of the staged kernel (0: its default; GALAHGPU_TEST_STAGE_KB)
 };
 // The words from start_bit to end_bit touch, + the readers' look-ahead.
 __host__ __device__ inline uint64_t inflate_segment_words(uint64_t start_bit, uint64_t end_bit) { return (end_bit + 31) / 32 - start_bit / 32 + 8; }

@@ -607,7 +607,8 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
   // positions
   auto restage = [&](uint64_t b) {
     const uint64_t w0 = b >> 5;
-    const uint32_t nw = (uint32_t)min<uint64_t>(kStageWords, inflate_segment_words(b, seg_end));
+    const uint32_t nw = (uint32_t)min<uint64_t>(a.stage_words ? a.stage_words : kStageWords,
+                                                  inflate_segment_words(b, seg_end));
     __syncthreads();  // (every lane is done with the stage before)
     for (uint32_t i = j; i < nw; i += kSpanLanes) stage[i] = gin[w0 + i];
     __syncthreads();
@@ -1251,7 +1252,8 @@ hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st) {
 
 hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st) {
   if (a.n_staged)
-    hipLaunchKernelGGL(inflate_decode_kernel<true>, dim3(a.n_staged), dim3(kSpanLanes), kStageWords * 4, st, a);
+    hipLaunchKernelGGL(inflate_decode_kernel<true>, dim3(a.n_staged), dim3(kSpanLanes),
+                       (a.stage_words ? a.stage_words : kStageWords) * 4, st, a);
   if (a.n_lanes > a.n_staged)
     hipLaunchKernelGGL(inflate_decode_kernel<false>, dim3(a.n_lanes - a.n_staged), dim3(kSpanLanes), 0, st, a);
   return hipGetLastError();

@@ -184,6 +184,21 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     for (uint32_t c = first_chunk[f]; c < first_chunk[f + 1]; ++c)
       if (start[c] != ~0ull && start[c] > starts[f].back()) starts[f].push_back(start[c]);
   }
+  // GALAHGPU_TEST_FAKE_STARTS=1 (tests): a false start midway (odd bit)
+  // between every two starts found, not a block boundary but a lane of its
+  // own, so that every lane before one runs past it and absorbs it
+  {
+    const char* fe = getenv("GALAHGPU_TEST_FAKE_STARTS");
+    if (fe && *fe == '1')
+      for (auto& v : starts) {
+        std::vector<uint64_t> w;
+        for (size_t i = 0; i < v.size(); ++i) {
+          w.push_back(v[i]);
+          if (i + 1 < v.size() && v[i + 1] - v[i] > 4096) w.push_back(((v[i] + v[i + 1]) / 2) | 1u);
+        }
+        v.swap(w);
+      }
+  }
   if (inflate_debug()) {
     size_t ns = 0;
     for (const auto& v : starts) ns += v.size();
@@ -259,6 +274,11 @@ gg_status inflate_batch(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, const
     d.lane_end = d_arg + 2 * (size_t)nl;
     d.n_lanes = nl;
     d.n_staged = n_staged;
+    {  // GALAHGPU_TEST_STAGE_KB (tests): a smaller LDS stage, so blocks take several windows
+      const char* se = getenv("GALAHGPU_TEST_STAGE_KB");
+      const int kb = se && *se ? atoi(se) : 0;
+      d.stage_words = kb >= 1 && kb <= 30 ? (uint32_t)kb * 256u : 0u;
+    }
     d.tok = d_tok;
     d.tok_off = d_arg + 3 * (size_t)nl;
     d.tok_cap = d_arg + 4 * (size_t)nl;

@@ -173,6 +173,34 @@ def test_device_inflate_blocks_longer_than_the_stage(tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("stage_kb", ["0", "2"])
+def test_device_inflate_false_starts_absorbed(tmp_path, monkeypatch, stage_kb):
+    """A false block start (GALAHGPU_TEST_FAKE_STARTS: one midway between
+    every two starts the search found) is passed by the lane before, which
+    decodes again from the start of the block that ran past it and absorbs
+    the false lane; with a 2 KB LDS stage (GALAHGPU_TEST_STAGE_KB) every block
+    takes many windows, and the block that overran must not count its earlier
+    windows' tokens twice (that sent C2 batches back to the host on ISIZE).
+    No batch handed back, sketches equal the host path's."""
+    rng = np.random.default_rng(21)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    paths = []
+    for i in range(8):
+        seq = acgt[rng.integers(0, 4, 700000)].tobytes()
+        text = b">f%d\n" % i + b"\n".join(seq[j:j + 80] for j in range(0, len(seq), 80)) + b"\n"
+        p = tmp_path / ("f%02d.fna.gz" % i)
+        p.write_bytes(gzip.compress(text, 6))
+        paths.append(str(p))
+    hsk, hl, _ = sketch_files(paths, monkeypatch, "host")
+    monkeypatch.setenv("GALAHGPU_TEST_FAKE_STARTS", "1")
+    monkeypatch.setenv("GALAHGPU_TEST_STAGE_KB", stage_kb)
+    monkeypatch.setenv("GALAHGPU_GZ_CHUNK_KB", "16")  # (more chunks: more starts, more false ones)
+    dsk, dl, fb = sketch_files(paths, monkeypatch, "device")
+    assert fb["inflate_host"] == 0
+    assert (dl == hl).all() and all((dsk[g][:dl[g]] == hsk[g][:hl[g]]).all() for g in range(len(paths)))
+
+
+@pytest.mark.gpu
 def test_device_inflate_corrupt_and_empty_fail_as_host(tmp_path, monkeypatch):
     rng = np.random.default_rng(4)
     seq = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 200000)].tobytes()
