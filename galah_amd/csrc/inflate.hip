@@ -531,18 +531,30 @@ __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_
   return st;
 }
 
-// n tokens from a lane's scratch to the segment's tokens, 8 loads in flight
-// (a plain loop waited on each load in turn).
+// n tokens from a lane's scratch to the segment's tokens, kCopyBatch loads
+// in flight (a plain loop waited on each load in turn; with 8 in flight a
+// window's ~85 tokens per lane still took ~11 waits: 16% of the decode)
+#ifndef GG_COPY_BATCH  // (A/B builds: -DGG_COPY_BATCH=8)
+#define GG_COPY_BATCH 32
+#endif
+constexpr uint32_t kCopyBatch = GG_COPY_BATCH;
 __device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint32_t n) {
   uint32_t i = 0;
-  for (; i + 8 <= n; i += 8) {
-    uint32_t v[8];
+  for (; i + kCopyBatch <= n; i += kCopyBatch) {
+    uint32_t v[kCopyBatch];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = src[i + k];
+    for (uint32_t k = 0; k < kCopyBatch; ++k) v[k] = src[i + k];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) dst[i + k] = v[k];
+    for (uint32_t k = 0; k < kCopyBatch; ++k) dst[i + k] = v[k];
   }
-  for (; i < n; ++i) dst[i] = src[i];
+  // the rest: all loads first, then the stores
+  uint32_t v[kCopyBatch];
+#pragma unroll
+  for (uint32_t k = 0; k < kCopyBatch; ++k)
+    if (i + k < n) v[k] = src[i + k];
+#pragma unroll
+  for (uint32_t k = 0; k < kCopyBatch; ++k)
+    if (i + k < n) dst[i + k] = v[k];
 }
 
 // One wave per segment (a found block start up to the next one).  Per block:
