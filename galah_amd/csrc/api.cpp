@@ -1434,8 +1434,15 @@ gg_status gg_info_line(const gg_ctx* ctx, char* buf, size_t cap) {
            (unsigned long long)fb[1], (unsigned long long)fb[2], (unsigned long long)staged_links,
            (unsigned long long)fb[3], (unsigned long long)fb[5], (unsigned long long)fb[4],
            (unsigned long long)dev_batches);
-  const size_t n = std::min(cap - 1, strlen(line));
-  memcpy(buf, line, n);
+  std::string out = line;
+  if (ctx->devs.size() > 1) {  // the device-inflated batches of each member
+    out += " [";
+    for (size_t i = 0; i < ctx->devs.size(); ++i)
+      out += (i ? "," : "") + std::to_string(ctx->devs[i]->inflate_dev_batches);
+    out += "]";
+  }
+  const size_t n = std::min(cap - 1, out.size());
+  memcpy(buf, out.data(), n);
   buf[n] = 0;
   return GG_OK;
 }

@@ -91,6 +91,13 @@ bool debug() {  // GALAHGPU_INFLATE_DEBUG=1: a timeline of the batches on stderr
 // of text (the inflate's parallel units are the streams' blocks, ~30 per
 // 3 Mbp genome: a batch needs hundreds of files to fill the GPU)
 constexpr uint32_t kBatchGenomesGz = 4096;
+// (GALAHGPU_GZ_BATCH_FILES, 1..4096, read per call: fewer files per batch, so
+// a test's few small files make many batches; no result depends on it)
+uint32_t gz_batch_files() {
+  const char* e = getenv("GALAHGPU_GZ_BATCH_FILES");
+  const long x = e ? atol(e) : 0;
+  return x > 0 ? (uint32_t)std::min<long>(x, kBatchGenomesGz) : kBatchGenomesGz;
+}
 // (GALAHGPU_GZ_BATCH_MB sets the gzip bytes per batch, the text cap follows
 // at 3x, at most 960 MiB: tuning only, no result depends on it.  Device
 // memory per lane: ~100 B per gzip byte of scratch (tokens and sub-span
@@ -296,6 +303,7 @@ class GzStager {
     std::mutex bm;
     bool full = false;
     uint64_t gz_bytes = 0, text_est = 0;
+    const uint32_t max_files = gz_batch_files();
     const bool stamp = cl_.cache_dir != nullptr;
     auto worker = [&] {
       (void)hipSetDevice(m_->device);
@@ -326,7 +334,7 @@ class GzStager {
           p = (g.at + doff + 3) / 4 * 4 - doff;  // (deflate data on a 4-byte boundary)
           const uint64_t end = p + len + 16 + kInflatePad;
           const bool fits = end <= sl.host_cap && end <= sl.dev_cap;
-          if (!g.idx.empty() && (!fits || g.idx.size() >= kBatchGenomesGz)) {
+          if (!g.idx.empty() && (!fits || g.idx.size() >= max_files)) {
             full = true;
             cl_.give_back(i);
             return;

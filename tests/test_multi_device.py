@@ -220,6 +220,37 @@ def test_many_small_files_stream_in_batches(tmp_path):
                 assert (sk[g][lens[g]:] == 0).all()
 
 
+def test_gzip_list_spread_over_members_in_many_batches(tmp_path, monkeypatch):
+    """A gzip list of many more files than one device-inflate batch holds
+    (GALAHGPU_GZ_BATCH_FILES=4): files are claimed one at a time across the
+    members' lanes, every member inflates batches on its device, none goes
+    to the host, and the sketches equal the oracle's for 1 and 3 members."""
+    import gzip
+    monkeypatch.setenv("GALAHGPU_GZ_BATCH_FILES", "4")
+    rng = np.random.default_rng(11)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    paths = []
+    for i in range(96):
+        seq = acgt[rng.integers(0, 4, int(rng.integers(20000, 80000)))].tobytes()
+        p = tmp_path / ("g%03d.fna.gz" % i)
+        p.write_bytes(gzip.compress(b">r\n" + b"\n".join(seq[x:x + 80] for x in range(0, len(seq), 80)) + b"\n"))
+        paths.append(str(p))
+    exp_sk, exp_len = oracle.sketch_files(paths, threads=8)
+    for devs in ([0], [0, 0, 0]):
+        with ga.Context(k=21, sketch_size=1000, devices=devs) as ctx:
+            sk, lens, _ = ctx.sketch_files(paths)
+            assert (lens == exp_len).all()
+            for g in range(len(paths)):
+                assert (sk[g][:lens[g]] == exp_sk[g][:lens[g]]).all()
+            assert ctx.fallbacks()["inflate_host"] == 0
+            line = ctx.info_line()
+            batches = int(line.split("device-inflated ")[1].split(")")[0])
+            assert batches >= len(paths) // 4, line
+            if len(devs) > 1:  # every member inflated some of them
+                per = [int(x) for x in line.rsplit("[", 1)[1].rstrip("]").split(",")]
+                assert len(per) == len(devs) and sum(per) == batches and min(per) > 0, line
+
+
 @pytest.mark.parametrize("min_ani", [0.5, 0.9])
 def test_row_range_index_partners_across_members(min_ani):
     """Inverted-index K2 split over 2, 3 and 5 members, each indexing only the
