@@ -964,50 +964,25 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
       const uint64_t tn = t0 + nt + tid;  // the next step's token (in flight during this step's LDS work)
       tk_next = tn < n ? tok[tn] : 0u;
     }
-    // kIntra pointers followed inside the step: each thread chases its own
-    // bytes' chains (positions tid + kExpandThreads k) all at once, reading
-    // the current value of each target -- a target's owner may have moved it
-    // on already, so chains shorten as in pointer jumping -- with no barrier
-    // between hops (every pointer goes to an earlier byte, so every chain
-    // ends on a value the token pass wrote: a literal or a pointer out of
-    // the step).  The values stay in registers for the write-out.
-    constexpr uint32_t kPer = (kExpandBytes + kExpandThreads - 1) / kExpandThreads;
-    volatile uint32_t* vv = v;
-    uint32_t xv[kPer];
-    uint32_t pend = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {
-      const uint32_t i = tid + k * kExpandThreads;
-      xv[k] = i < nb ? vv[i] : 0x80000000u;
-      if ((xv[k] & 0xC0000000u) == kIntra) pend |= 1u << k;
-    }
-    for (uint32_t hop = 0; pend; ++hop) {
-      if (hop >= kExpandBytes) {  // (cannot happen: a chain has fewer hops than the step has bytes)
-        atomicOr(a.flags, 2u);
-        break;
-      }
-      uint32_t y[kPer];
-#pragma unroll
-      for (uint32_t k = 0; k < kPer; ++k) y[k] = (pend >> k) & 1u ? vv[xv[k] & 0x3FFFFFFFu] : 0u;
-#pragma unroll
-      for (uint32_t k = 0; k < kPer; ++k)
-        if ((pend >> k) & 1u) {
-          xv[k] = y[k];
-          vv[tid + k * kExpandThreads] = y[k];
-          if ((y[k] & 0xC0000000u) != kIntra) pend &= ~(1u << k);
+    for (;;) {  // kIntra pointers followed inside the step (each points to an earlier byte)
+      bool more = false;
+      for (uint32_t i = tid; i < nb; i += kExpandThreads) {
+        const uint32_t x = v[i];
+        if ((x & 0xC0000000u) == kIntra) {
+          const uint32_t y = v[x & 0x3FFFFFFFu];
+          v[i] = y;
+          more |= (y & 0xC0000000u) == kIntra;
         }
+      }
+      if (!__syncthreads_or(more)) break;
     }
     const uint32_t nw = base + nb <= lim ? nb : base < lim ? (uint32_t)(lim - base) : 0u;
-#pragma unroll
-    for (uint32_t k = 0; k < kPer; ++k) {
-      const uint32_t i = tid + k * kExpandThreads;
-      if (i < nw) {
-        const uint32_t x = xv[k];
-        a.val[base + i] = x;
-        a.text[base + i] = x >> 31 ? (uint8_t)x : kTextPtr;  // (kTextPtr: the resolve pass follows val there)
-        ring[(uint32_t)(base + i) & (kRing - 1)] =
-            x >> 31 ? (uint16_t)(x & 0xFFu) : (uint16_t)(kRingPtr | (uint32_t)(o0 - 1 - x));
-      }
+    for (uint32_t i = tid; i < nw; i += kExpandThreads) {
+      const uint32_t x = v[i];
+      a.val[base + i] = x;
+      a.text[base + i] = x >> 31 ? (uint8_t)x : kTextPtr;  // (kTextPtr: the resolve pass follows val there)
+      ring[(uint32_t)(base + i) & (kRing - 1)] =
+          x >> 31 ? (uint16_t)(x & 0xFFu) : (uint16_t)(kRingPtr | (uint32_t)(o0 - 1 - x));
     }
     __syncthreads();
     base += nb;
