@@ -275,6 +275,12 @@ struct GzClaims {
   uint32_t cursor = 0;
   std::vector<uint32_t> back;  // claimed, given back
   uint32_t batches = 0;        // batches begun (the first ones are cut smaller)
+  // the tail of the list cut into equal batches, a multiple of the stagers
+  // (members x lanes), so that they finish together instead of the last
+  // lane running a full batch alone
+  uint32_t stagers = 1;
+  uint64_t seen_files = 0, seen_bytes = 0;  // files staged so far, their bytes
+  uint32_t tail_cap = 0;                    // files per batch from the tail on (0: not there yet)
   bool stop = false;           // no more claims: a failure
   // the failing file with the lowest index (a file that did not read, or
   // did not decode or parse on the host): the call's error, as a serial
@@ -287,6 +293,8 @@ struct GzClaims {
   void file_error(uint32_t i, gg_status st, const std::string& msg);
   void halt();
 };
+// Inflate lanes per device (GALAHGPU_GZ_LANES, default 2).
+int gz_lane_count();
 // Member m's share of the list: inflated, parsed and sketched on m's device
 // by several lanes at once, rows into d_sk / d_len (m's [n x s] arrays);
 // the rows sketched are appended to owned.  host_threads: the host threads

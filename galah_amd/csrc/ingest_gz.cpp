@@ -36,6 +36,8 @@
 #include <new>
 #include <thread>
 
+#include <cmath>
+
 #include "context.hpp"
 
 namespace gg {
@@ -261,6 +263,7 @@ class GzStager {
     g = GzStaged{};
     g.t0 = Clock::now();
     int ramp;
+    uint32_t max_files = gz_batch_files();
     {
       std::lock_guard<std::mutex> lk(cl_.mu);
       if (cl_.stop || (cl_.cursor >= cl_.n && cl_.back.empty())) return false;
@@ -268,6 +271,20 @@ class GzStager {
       // while the full-size ones are staged
       ramp = cl_.batches < 3 ? 3 - (int)cl_.batches : 0;
       ++cl_.batches;
+      // the tail: once the files left fit fewer full batches than one per
+      // stager and one more, they go in k equal batches, k the stagers'
+      // smallest multiple that holds them at full size
+      if (!ramp && !cl_.tail_cap && cl_.seen_files && !(getenv("GALAHGPU_GZ_NO_TAIL") && *getenv("GALAHGPU_GZ_NO_TAIL") == '1')) {
+        const uint64_t left = (uint64_t)(cl_.n - cl_.cursor) + cl_.back.size();
+        const double full = std::max(1.0, (double)gz_batch_bytes() * cl_.seen_files / std::max<uint64_t>(1, cl_.seen_bytes));
+        const uint64_t S = std::max<uint32_t>(1, cl_.stagers);
+        if ((double)left < (double)(S + 1) * full) {
+          const uint64_t need = (uint64_t)std::ceil((double)left / full);
+          const uint64_t k = (std::max<uint64_t>(need, 1) + S - 1) / S * S;
+          cl_.tail_cap = (uint32_t)std::max<uint64_t>(1, (left + k - 1) / k);
+        }
+      }
+      if (cl_.tail_cap) max_files = std::min(max_files, cl_.tail_cap);
     }
     const uint64_t cut_gz = gz_batch_bytes() >> ramp, cut_text = gz_batch_text() >> ramp;
     gg_ctx::GzSlot& sl = m_->gz_slot[si];
@@ -303,7 +320,6 @@ class GzStager {
     std::mutex bm;
     bool full = false;
     uint64_t gz_bytes = 0, text_est = 0;
-    const uint32_t max_files = gz_batch_files();
     const bool stamp = cl_.cache_dir != nullptr;
     auto worker = [&] {
       (void)hipSetDevice(m_->device);
@@ -345,6 +361,11 @@ class GzStager {
           }
           g.at = p + len;
           gz_bytes += pr.gz ? pr.size : 0;
+          {
+            std::lock_guard<std::mutex> lc(cl_.mu);
+            ++cl_.seen_files;
+            cl_.seen_bytes += pr.size;
+          }
           text_est += pr.member ? pr.isize : len;
           if (gz_bytes >= cut_gz || text_est >= cut_text) full = true;
           InflateFile f;
@@ -521,6 +542,8 @@ gg_status run_lane(gg_ctx* x, GzClaims& cl, uint64_t* d_sk, uint32_t* d_len, int
 }
 
 }  // namespace
+
+int gz_lane_count() { return gz_lanes(); }
 
 gg_status gz_member_ingest(gg_ctx* m, GzClaims& cl, uint64_t* d_sk, uint32_t* d_len, int host_threads,
                            std::vector<uint32_t>& owned) {

@@ -531,6 +531,7 @@ gg_status sketch_files_members(gg_ctx* c, const std::vector<gg_ctx*>& ms, const 
   claims.row_of = miss_at.data();
   claims.n = nm;
   claims.cache_dir = cache_dir;
+  claims.stagers = (uint32_t)(M * gz_lane_count());
   std::mutex cursor_mu;
   uint32_t cursor = 0;
   bool stop = false;        // a member failed: the others take no more batches
