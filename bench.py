@@ -695,7 +695,7 @@ def run_lib(a, world, rank):
         want_files = a.files if a.files is not None else (a.config == "c3")
         if world == 1 and M == 1 and want_files:
             try:
-                files = files_leg(a, devs[0], 3)
+                files = files_leg(a, devs[0], 5)
             except Exception as e:  # the headline stands without it
                 files = {"error": "%s: %s" % (type(e).__name__, e)}
         line = {
