@@ -89,6 +89,11 @@ def parse():
                          "gg_precluster_files); on by default for the one-GPU C3 headline")
     ap.add_argument("--no-files", dest="files", action="store_false")
     ap.add_argument("--files-genomes", type=int, default=1000, help="genomes in the files leg (C2: 1000)")
+    ap.add_argument("--c4", dest="c4_leg", action="store_true", default=None,
+                    help="add the north-star leg (C4: 100k x 3 Mbp, s=1000 on one GPU, 3 steps); on by default for "
+                         "the one-GPU C3 headline")
+    ap.add_argument("--no-c4", dest="c4_leg", action="store_false")
+    ap.add_argument("--c4-steps", type=int, default=3)
     ap.add_argument("--cpu-budget-s", type=float, default=24.0)
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="dist mode: gloo stages collectives through host memory (ranks sharing one GPU)")
@@ -400,7 +405,25 @@ def cpu_baseline(sample_words, glen, sk_all, lens_all, k, s, min_ani, n_total, b
 # ---------------------------------------------------------------------------
 # ingest-inclusive leg: real gzip FASTA files through gg_precluster_files
 # ---------------------------------------------------------------------------
-def roofline_ingest(ks, wall_s, gz_bytes, text_bytes):
+def pcie_h2d_gbps(device, nbytes=1 << 30, reps=5):
+    """The host-to-device PCIe rate of this box: a pinned host buffer copied
+    to device memory by the DMA engine (torch), best of `reps` (the upload
+    kernel that moves the ingest's staged batches reads mapped pinned memory
+    over the same link, so this is its ceiling, not the 8 TB/s of HBM)."""
+    src = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+    dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda:%d" % device)
+    best = 0.0
+    for _ in range(reps):
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize(device)
+        best = max(best, nbytes / (time.perf_counter() - t0) / 1e9)
+    del src, dst
+    return best
+
+
+def roofline_ingest(ks, wall_s, gz_bytes, text_bytes, pcie_gbps=None):
     """The device-inflate ingest priced kernel by kernel:
     HIP-event ms per call of each kernel class on the stream it ran on (one
     call with one processing lane, so no kernel shares the GPU with
@@ -408,7 +431,9 @@ def roofline_ingest(ks, wall_s, gz_bytes, text_bytes):
     VALU issue share and HBM bytes (profiles/r05_ingest_pmc.json, the same
     C2 workload).  Algorithmic bytes per call (G = gzip bytes, X = text
     bytes, T = tokens the decode wrote):
-      upload  G (host -> device, over PCIe: priced against the HBM peak too)
+      upload  G (host -> device over PCIe: priced against the box's measured
+              PCIe H2D rate, pcie_h2d_gbps, not HBM; not a candidate for
+              the dominant HBM kernel)
       search  G read once
       decode  G read + 4 T (tokens written)
       expand  4 T read + 5 X (val u32 + the text byte per text byte)
@@ -442,37 +467,65 @@ def roofline_ingest(ks, wall_s, gz_bytes, text_bytes):
         if not k or not k["launches"]:
             continue
         ms = k["ms"]
+        peak = pcie_gbps if (name == "upload" and pcie_gbps) else 8000.0
         e = {"ms_per_call": round(ms, 4), "launches": k["launches"], "algorithmic_bytes": round(b),
-             "achieved_GBps": round(b / (ms * 1e-3) / 1e9, 2), "peak_GBps": 8000.0,
-             "frac": round(b / (ms * 1e-3) / 8e12, 5)}
+             "achieved_GBps": round(b / (ms * 1e-3) / 1e9, 2), "peak_GBps": round(peak, 2),
+             "frac": round(b / (ms * 1e-3) / 1e9 / peak, 5), "bound": "pcie" if name == "upload" else "hbm"}
         if name in pmc:
             e["pmc"] = pmc[name]
         kern[name] = e
         tot_ms += ms
         tot_alg += b
-    dom = max(kern, key=lambda x: kern[x]["ms_per_call"]) if kern else None
-    traffic = sum(v.get("pmc", {}).get("hbm_bytes_per_call", 0) for v in kern.values()) or None
+    # the HBM-side kernels (upload reads host memory over PCIe: its own line)
+    dev = {x: v for x, v in kern.items() if x != "upload"}
+    dom = max(dev, key=lambda x: dev[x]["ms_per_call"]) if dev else None
+    d_ms = sum(v["ms_per_call"] for v in dev.values())
+    d_alg = sum(v["algorithmic_bytes"] for v in dev.values())
+    traffic = sum(v.get("pmc", {}).get("hbm_bytes_per_call", 0) for v in dev.values()) or None
     return {"bound": "hbm", "unit": "GB/s", "peak": 8000.0,
-            "achieved": round(tot_alg / (tot_ms * 1e-3) / 1e9, 2) if tot_ms else None,
-            "frac": round(tot_alg / (tot_ms * 1e-3) / 8e12, 5) if tot_ms else None, "traffic": traffic,
-            "kernels_ms_per_call": round(tot_ms, 3), "call_s_one_lane": round(wall_s, 4), "dominant": dom,
+            "achieved": round(d_alg / (d_ms * 1e-3) / 1e9, 2) if d_ms else None,
+            "frac": round(d_alg / (d_ms * 1e-3) / 8e12, 5) if d_ms else None, "traffic": traffic,
+            "algorithmic_bytes": round(d_alg), "traffic_over_algorithmic": round(traffic / d_alg, 3) if (traffic and d_alg) else None,
+            "kernels_ms_per_call": round(tot_ms, 3), "device_kernels_ms_per_call": round(d_ms, 3),
+            "call_s_one_lane": round(wall_s, 4), "dominant": dom,
+            "upload": kern.get("upload"), "pcie_h2d_GBps": round(pcie_gbps, 2) if pcie_gbps else None,
             "kernels": kern,
-            "note": "achieved = the ingest kernels' algorithmic bytes per call (docstring of bench.py "
-                    "roofline_ingest) / their summed HIP-event time on their own streams, one call with one lane "
-                    "(GALAHGPU_GZ_LANES=1); the default two lanes overlap these kernels; pmc: "
+            "note": "achieved = the device-memory ingest kernels' algorithmic bytes per call (docstring of "
+                    "bench.py roofline_ingest) / their summed HIP-event time on their own streams, one call with "
+                    "one lane (GALAHGPU_GZ_LANES=1); the default two lanes overlap these kernels; upload (host "
+                    "memory over PCIe) is priced against pcie_h2d_GBps, the box's pinned H2D DMA rate; pmc: "
                     "profiles/r05_ingest_pmc.json (valu_frac_guide = VALU wave-instructions / (1024 SIMDs x "
                     "cycles / 2), hbm_bytes = FETCH_SIZE x 2 + WRITE_SIZE)"}
 
 
+def bgzf_bytes(data, level=6, block=65280):
+    """bgzip's output for data (BGZF, SAM/BAM specification 4.1): deflate
+    members of <= 64 KB of input, each header carrying its size in the 'BC'
+    extra subfield, then the empty end-of-file member."""
+    import zlib
+    out = []
+    for i in range(0, max(len(data), 1), block):
+        chunk = data[i:i + block]
+        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+        body = c.compress(chunk) + c.flush()
+        hdr = bytes([0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 66, 67, 2, 0]) + (len(body) + 25).to_bytes(2, "little")
+        out.append(hdr + body + zlib.crc32(chunk).to_bytes(4, "little") + len(chunk).to_bytes(4, "little"))
+    out.append(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+    return b"".join(out)
+
+
 def files_leg(a, device, steps):
-    """C2's genomes (1k x 3 Mbp, clusters of 10) written as gzip FASTA (80
-    columns, level 6) to local disk OUTSIDE the timed region, then
-    gg_precluster_files over the paths (what galah's distances() calls:
-    src/finch.rs:47-73) timed end to end: read + gunzip + parse + 2-bit pack
-    on the host threads, H2D, K1, K2, merge.  Files are in the page cache
-    (written just before).  Beside it: pure read + libdeflate gunzip of the
-    same files on the same threads (scripts/gunzip_probe), the floor any
-    host ingest of these files sits on."""
+    """C2's genomes (1k x 3 Mbp, clusters of 10) written as FASTA files (80
+    columns) to local disk OUTSIDE the timed region -- gzip (zlib level 6,
+    one member), bgzip (BGZF, level 6) and plain -- then gg_precluster_files
+    over each list (what galah's distances() calls: src/finch.rs:47-73) timed
+    end to end.  gzip: the default device inflate, and the host inflate
+    beside it; bgzip: the default device inflate (members from the headers);
+    plain: the default (host threads read and pack) and the device parse
+    (GALAHGPU_INFLATE=device).  Files are in the page cache (written just
+    before).  Beside them: pure read + libdeflate gunzip of the gzip files
+    on the same threads (scripts/gunzip_probe) and a pure read of the plain
+    files, the floors any host ingest sits on."""
     import concurrent.futures as cf
     import shutil
     import tempfile
@@ -482,6 +535,7 @@ def files_leg(a, device, steps):
     out = {"workload": "C2: %d synthetic genomes x %d bp as gzip FASTA (80 columns, zlib level 6), "
                        "k=21, s=1000, min_ani=%s" % (n, glen, float(ga.parse_percentage(a.min_ani))),
            "host_threads": T}
+    plain_out = {}
     d = tempfile.mkdtemp(prefix="gg_files_", dir=os.environ.get("TMPDIR") or "/tmp")
     try:
         t0 = time.perf_counter()
@@ -494,6 +548,8 @@ def files_leg(a, device, steps):
         acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
         shifts = (np.uint32(30) - 2 * np.arange(16, dtype=np.uint32))[None, :]
         nl = np.full((glen // 80, 1), ord("\n"), np.uint8)
+        for f in ("gz", "bgzf", "plain"):
+            os.makedirs(os.path.join(d, f))
 
         def write(g):
             w = words[g * glen // 16:(g + 1) * glen // 16]
@@ -501,42 +557,55 @@ def files_leg(a, device, steps):
             body = np.concatenate([seq[: glen // 80 * 80].reshape(-1, 80), nl], axis=1).tobytes()
             text = b">genome_%d synthetic C2\n" % g + body + (bytes(seq[glen // 80 * 80:]) + b"\n" if glen % 80 else b"")
             c = zlib.compressobj(6, zlib.DEFLATED, 31)
-            p = os.path.join(d, "g%05d.fna.gz" % g)
-            with open(p, "wb") as f:
-                f.write(c.compress(text) + c.flush())
-            return p
+            ps = {f: os.path.join(d, f, "g%05d.fna" % g + ("" if f == "plain" else ".gz")) for f in ("gz", "bgzf", "plain")}
+            with open(ps["gz"], "wb") as fh:
+                fh.write(c.compress(text) + c.flush())
+            with open(ps["bgzf"], "wb") as fh:
+                fh.write(bgzf_bytes(text))
+            with open(ps["plain"], "wb") as fh:
+                fh.write(text)
+            return ps
 
         with cf.ThreadPoolExecutor(T) as ex:
-            paths = list(ex.map(write, range(n)))
+            written = list(ex.map(write, range(n)))
         del words
+        lists = {f: [w[f] for w in written] for f in ("gz", "bgzf", "plain")}
+        paths = lists["gz"]
         out["write_s"] = round(time.perf_counter() - t0, 2)
         out["gz_bytes"] = int(sum(os.path.getsize(p) for p in paths))
-        print("[bench] files leg: wrote %d gzip FASTA files (%.2f GB) in %.1f s" % (n, out["gz_bytes"] / 1e9,
-              out["write_s"]), file=sys.stderr, flush=True)
+        print("[bench] files leg: wrote %d gzip, bgzip and plain FASTA files (%.2f GB gzip) in %.1f s"
+              % (n, out["gz_bytes"] / 1e9, out["write_s"]), file=sys.stderr, flush=True)
         thr = ga.parse_percentage(a.min_ani)
         bases = n * glen
+        ingest = []
 
-        def timed(inflate):
-            """gg_precluster_files over the paths, GALAHGPU_INFLATE=inflate."""
-            os.environ["GALAHGPU_INFLATE"] = inflate
+        def timed(plist, inflate, kernel_timing=False):
+            """gg_precluster_files over plist, GALAHGPU_INFLATE=inflate (None: the default)."""
+            if inflate:
+                os.environ["GALAHGPU_INFLATE"] = inflate
             try:
                 with ga.Context(k=21, sketch_size=1000, seed=0, device=device, host_threads=T) as ctx:
-                    ctx.precluster_files(paths, thr)  # warm-up: one untimed call (device buffers sized for the batches)
+                    ctx.precluster_files(plist, thr)  # warm-up: one untimed call (device buffers sized for the batches)
                     times, found, ph = [], 0, {p: 0.0 for p in ga.PHASES}
                     for _ in range(max(1, steps)):
                         t1 = time.perf_counter()
-                        pairs, _ani = ctx.precluster_files(paths, thr)
+                        pairs, _ani = ctx.precluster_files(plist, thr)
                         times.append(time.perf_counter() - t1)
                         found = len(pairs)
                         for p, v in ctx.phase_times().items():
                             ph[p] += v
+                    ctx.timing_enable(True)  # (one more call, untimed: K1's HIP-event time per call)
+                    ctx.precluster_files(plist, thr)
+                    k1 = ctx.timing_read(ga.KERNEL_SKETCH)
+                    ctx.timing_enable(False)
                     fb = ctx.fallbacks()["inflate_host"]
-                    if inflate == "device":  # one more call, timed kernel by kernel (one lane: no overlap)
+                    info = ctx.info_line()
+                    if kernel_timing:  # one more call, timed kernel by kernel (one lane: no overlap)
                         os.environ["GALAHGPU_GZ_LANES"] = "1"
                         try:
                             ctx.timing_enable(True)
                             t1 = time.perf_counter()
-                            ctx.precluster_files(paths, thr)
+                            ctx.precluster_files(plist, thr)
                             w1 = time.perf_counter() - t1
                             kst = {name: ctx.timing_read(k) for name, k in ga.INGEST_KERNELS.items()}
                             kst["k1"] = ctx.timing_read(ga.KERNEL_SKETCH)
@@ -547,25 +616,35 @@ def files_leg(a, device, steps):
             finally:
                 os.environ.pop("GALAHGPU_INFLATE", None)
             t = float(np.median(times))
-            return {"steps": len(times), "s_per_call_median": round(t, 4), "s_per_call": [round(x, 4) for x in times],
+            return {"steps": len(times), "s_per_call_median": round(t, 4), "s_per_call_max": round(max(times), 4),
+                    "max_over_median": round(max(times) / t, 3), "s_per_call": [round(x, 4) for x in times],
                     "gbases_per_s": round(bases / t / 1e9, 3), "genome_pairs_per_s": round(n * (n - 1) / 2 / t, 1),
                     "pairs_found": int(found), "phase_ms": {p: round(v / len(times), 2) for p, v in ph.items()},
-                    "inflate_host_batches": fb}, pairs
+                    "k1_ms_per_call": round(k1["ms"], 3),
+                    "inflate_host_batches": fb, "info_line": info}, pairs
 
         # the default path for gzip files: inflated on the GPU (inflate.hip), the host threads only read
-        ingest = []
-        dev, dp = timed("device")
+        dev, dp = timed(paths, "device", kernel_timing=True)
         out.update(dev)
         if ingest:
             text_bytes = sum(len(b">genome_%d synthetic C2\n" % g) for g in range(n)) + n * (glen + glen // 80)
-            out["roofline_ingest"] = roofline_ingest(ingest[0], ingest[1], out["gz_bytes"], text_bytes)
+            try:
+                pcie = pcie_h2d_gbps(device)
+            except Exception:
+                pcie = None
+            out["roofline_ingest"] = roofline_ingest(ingest[0], ingest[1], out["gz_bytes"], text_bytes, pcie)
         out["inflate"] = "device"
         t = dev["s_per_call_median"]
         # the same files gunzipped and packed on the host threads (GALAHGPU_INFLATE=host, round 3's path)
-        host, hp = timed("host")
+        host, hp = timed(paths, "host")
         out["host_inflate"] = host
         out["same_pairs_as_host_inflate"] = bool(np.array_equal(hp, dp))
         out["device_over_host_inflate"] = round(host["s_per_call_median"] / t, 3)
+        # bgzip (BGZF members from their headers), the default path
+        bg, bp = timed(lists["bgzf"], None)
+        bg["bgzf_bytes"] = int(sum(os.path.getsize(p) for p in lists["bgzf"]))
+        bg["same_pairs_as_gzip"] = bool(np.array_equal(bp, dp))
+        out["bgzip"] = bg
         probe = os.path.join(ROOT, "scripts", "gunzip_probe")
         if os.path.exists(probe):
             r = subprocess.run([probe, str(T)] + paths, capture_output=True, text=True, timeout=300)
@@ -580,10 +659,45 @@ def files_leg(a, device, steps):
                        "distances() starts from these paths (src/finch.rs:47); top level: the default for gzip "
                        "files, gzip bytes to the GPU, inflated and parsed there (inflate.hip, parse.hip), the host "
                        "threads only read; host_inflate: gunzip + parse + pack on the host threads "
-                       "(GALAHGPU_INFLATE=host); pure_decode: read + libdeflate gunzip alone on the same threads" % T)
+                       "(GALAHGPU_INFLATE=host); bgzip: the same genomes as BGZF files (device inflate, one unit "
+                       "per member); pure_decode: read + libdeflate gunzip alone on the same threads" % T)
+        # plain FASTA (the reference's own fixtures: tests/data/*.fna): the
+        # default (read + parse + 2-bit pack on the host threads, packed words
+        # to the device) and the device parse (text to the device)
+        pl = lists["plain"]
+        text_total = int(sum(os.path.getsize(p) for p in pl))
+
+        def pure_read():
+            def rd(p):
+                with open(p, "rb", buffering=0) as fh:
+                    return len(fh.read())
+            t1 = time.perf_counter()
+            with cf.ThreadPoolExecutor(T) as ex:
+                got = sum(ex.map(rd, pl))
+            return time.perf_counter() - t1, got
+
+        pure_read()  # (warm)
+        rs = min(pure_read()[0] for _ in range(3))
+        dflt, p0 = timed(pl, None)
+        devp, p1 = timed(pl, "device")
+        plain_out = {"workload": out["workload"].replace("as gzip FASTA (80 columns, zlib level 6)",
+                                                           "as plain FASTA (80 columns)"),
+                     "text_bytes": text_total, "host_threads": T,
+                     "default": dflt, "device_parse": devp,
+                     "gbases_per_s": dflt["gbases_per_s"],
+                     "pure_read_s": round(rs, 4), "pure_read_GBps": round(text_total / rs / 1e9, 2),
+                     "same_pairs_as_gzip": bool(np.array_equal(p0, dp) and np.array_equal(p1, dp)),
+                     "split_ms": {"pure_read_floor": round(rs * 1e3, 2),
+                                  "sketch_phase": dflt["phase_ms"]["sketch"], "k1_kernel": dflt["k1_ms_per_call"],
+                                  "pairs_phase": dflt["phase_ms"]["pairs"], "merge_phase": dflt["phase_ms"]["merge"]},
+                     "note": "default: the host threads read, parse and 2-bit pack (pack.cpp), packed words go to "
+                             "the device, K1 + K2 there; device_parse (GALAHGPU_INFLATE=device): the text goes to the "
+                             "device and parse.hip packs it; split_ms: the pure read of the same files on the same "
+                             "threads (page cache), the sketch phase (read + pack + upload + K1, overlapped), K1's "
+                             "HIP-event time, K2 + D2H, merge"}
     finally:
         shutil.rmtree(d, ignore_errors=True)
-    return out
+    return out, plain_out
 
 
 # ---------------------------------------------------------------------------
@@ -592,6 +706,75 @@ def workload_note(a, N, total_bases, min_ani, s):
          if a.config == "c5" else ("%s: %d synthetic genomes x %d bp" % (a.config.upper(), N, a.genome_len)))
     return w + ", clusters of %d, sub rate U(0,%.2f), k=%d, s=%d, min_ani=%s" % (a.cluster, a.max_sub, a.k, s,
                                                                                  min_ani)
+
+
+def c4_leg(a, device):
+    """The north-star workload on one GPU (BASELINE.json configs[3]: 100k
+    synthetic 3 Mbp genomes, s=1000, min_ani f32(0.95); src/finch.rs:53-73
+    over all 5e9 pairs): one warm-up and a.c4_steps timed steps of the same
+    gg_precluster_shards call as the headline, inputs resident in HBM (75 GB
+    of packed words), K1 / K2 HIP-event times and both rooflines.  The
+    node's 8-GPU curve extends this N=1 point."""
+    import copy
+    b = copy.copy(a)
+    b.config, b.genomes = "c4", 100000
+    N, s = b.genomes, 1000
+    min_ani = ga.parse_percentage(b.min_ani)
+    t0 = time.perf_counter()
+    ctx = ga.Context(k=b.k, sketch_size=s, seed=0, device=device)
+    try:
+        d_words, runs, bases = make_shard(ctx, b, 0, N, device)
+        d_runs = ga.device_runs(runs, "cuda:%d" % device)
+        shards = [(d_words, d_runs, N)]
+        torch.cuda.synchronize(device)
+        synth_s = time.perf_counter() - t0
+        ctx.precluster_shards(shards, min_ani)  # warm-up
+        ctx.timing_enable(True)
+        torch.cuda.synchronize(device)
+        times, ph = [], {p: 0.0 for p in ga.PHASES}
+        found = 0
+        for _ in range(max(1, b.c4_steps)):
+            t1 = time.perf_counter()
+            pairs, _ani = ctx.precluster_shards(shards, min_ani)
+            torch.cuda.synchronize(device)
+            times.append(time.perf_counter() - t1)
+            found = len(pairs)
+            for p, v in ctx.phase_times().items():
+                ph[p] += v
+        kst = {name: ctx.timing_read(kid) for name, kid in
+               (("sketch", ga.KERNEL_SKETCH), ("finalize", ga.KERNEL_FINALIZE), ("pairs", ga.KERNEL_PAIRS),
+                ("index", ga.KERNEL_PAIRS_INDEX))}
+        kst["pairs"]["ms"] += kst["index"]["ms"]
+        ctx.timing_enable(False)
+        steps = len(times)
+        roof = roofline(kst["sketch"], kst["pairs"], s, "C4 on one GPU")
+        d_sk = torch.zeros((N, s), dtype=torch.int64, device="cuda:%d" % device)
+        d_len = torch.zeros(N, dtype=torch.int32, device="cuda:%d" % device)
+        ctx.sketch_device(d_words, d_runs, N, d_sk, d_len)
+        torch.cuda.synchronize(device)
+        kp = dict(kst["pairs"])
+        kp["launches_sets"] = kst["pairs"]["launches"]
+        roof_k2 = roofline_k2(k2_algorithmic_bytes(d_sk, d_len, N, s), kp, None)
+        paths = ctx.pair_paths()
+        fb = ctx.fallbacks()
+        del d_sk, d_len, shards, d_words, d_runs
+    finally:
+        ctx.close()
+        torch.cuda.empty_cache()
+    ms = float(np.mean(times)) * 1e3
+    npairs = N * (N - 1) // 2
+    return {"workload": workload_note(b, N, bases, min_ani, s), "genomes": N, "steps": steps, "warmup": 1,
+            "ms_per_step": round(ms, 3), "ms_per_step_all": [round(x * 1e3, 3) for x in times],
+            "genome_pairs_per_s": round(npairs / (ms * 1e-3), 1), "pairs_found": found,
+            "sketch_gbases_per_s": round(bases / (ph["sketch"] / steps * 1e-3) / 1e9, 3),
+            "phase_ms": {p: round(v / steps, 3) for p, v in ph.items()},
+            "kernel_ms_per_step": {"k1": round(kst["sketch"]["ms"] / steps, 3),
+                                   "finalize": round(kst["finalize"]["ms"] / steps, 3),
+                                   "k2": round(kst["pairs"]["ms"] / steps, 3)},
+            "roofline": roof, "roofline_k2": roof_k2, "pair_paths": paths,
+            "fallbacks": fb, "synth_s": round(synth_s, 2),
+            "note": "the north-star scale (100k genomes, s=1000) on ONE MI355X, inputs resident in HBM; "
+                    "BASELINE's target is >= 1e9 genome-pairs/s node-wide"}
 
 
 def run_lib(a, world, rank):
@@ -691,13 +874,19 @@ def run_lib(a, world, rank):
         ctx = None
         del shards, keep, d_words, runs
         torch.cuda.empty_cache()
-        files = None
+        files = files_plain = c4 = None
         want_files = a.files if a.files is not None else (a.config == "c3")
         if world == 1 and M == 1 and want_files:
             try:
-                files = files_leg(a, devs[0], 5)
+                files, files_plain = files_leg(a, devs[0], 5)
             except Exception as e:  # the headline stands without it
                 files = {"error": "%s: %s" % (type(e).__name__, e)}
+        want_c4 = a.c4_leg if a.c4_leg is not None else (a.config == "c3")
+        if world == 1 and M == 1 and want_c4:
+            try:
+                c4 = c4_leg(a, devs[0])
+            except Exception as e:  # the headline stands without it
+                c4 = {"error": "%s: %s" % (type(e).__name__, e)}
         line = {
             "metric": "precluster genome-pairs/sec at 10k genomes (s=1000) + sketch Gbases/s",
             "value": round(npairs / (elapsed_max / a.steps), 1), "unit": "genome-pairs/s", "n_gpus": n_dev,
@@ -720,6 +909,8 @@ def run_lib(a, world, rank):
             "cpu_baseline": cpu,
             "downstream": downstream,
             "files": files,
+            "files_plain": files_plain,
+            "c4_one_gpu": c4,
         }
     if world > 1:
         dist.destroy_process_group()

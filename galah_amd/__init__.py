@@ -50,7 +50,7 @@ EXPORTED_SYMBOLS = (
     "gg_partition_preclusters", "gg_precluster_pairs", "gg_synth_mixed_lengths", "gg_synth_mixed_device",
     "gg_sketch_cache_load", "gg_sketch_cache_store", "gg_sketch_files", "gg_precluster_files_cached",
     "gg_create_multi", "gg_device_count", "gg_device_ctx", "gg_set_host_threads", "gg_phase_times",
-    "gg_precluster_shards", "gg_fallbacks", "gg_peer_links", "gg_info_line",
+    "gg_precluster_shards", "gg_fallbacks", "gg_peer_links", "gg_info_line", "gg_precluster_files_each",
 )
 
 GG_OK = 0
@@ -132,6 +132,11 @@ _sig("gg_precluster_files", _i32, [_vp, ctypes.POINTER(ctypes.c_char_p), _u32, c
 _sig("gg_precluster_files_cached", _i32, [_vp, ctypes.POINTER(ctypes.c_char_p), _u32, ctypes.c_float,
                                           ctypes.c_char_p, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
                                           ctypes.POINTER(_u64), ctypes.POINTER(_u32)])
+# gg_pair_sink: int (*)(void* user, const gg_pair* pairs, uint64_t n)
+PAIR_SINK = ctypes.CFUNCTYPE(_i32, _vp, _vp, _u64)
+_sig("gg_precluster_files_each", _i32, [_vp, ctypes.POINTER(ctypes.c_char_p), _u32, ctypes.c_float, ctypes.c_char_p,
+                                        PAIR_SINK, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                        ctypes.POINTER(_u64), ctypes.POINTER(_u32)])
 _sig("gg_sketch_files", _i32, [_vp, ctypes.POINTER(ctypes.c_char_p), _u32, ctypes.c_char_p, _vp, _vp,
                                ctypes.POINTER(_u32)])
 _sig("gg_sketch_cache_load", _i32, [ctypes.c_char_p, ctypes.c_char_p, _i32, _u32, _u64, _vp,
@@ -611,6 +616,37 @@ class Context:
             raise self._err(st)
         return self._pairs_ani(pp, ap, cnt.value)
 
+    def precluster_files_each(self, paths, min_ani, each, cache_dir=None):
+        """precluster_files, and every compared pair (i < j, all N (N - 1) / 2,
+        whatever the ANI) handed to each(block) in (i, j) order as PAIR_DTYPE
+        arrays of at most ~4M pairs (gg_precluster_files_each: galah's debug
+        level, src/finch.rs:65-68, without holding every pair).  each returning
+        True stops the call (GalahGpuError, status 9)."""
+        arr = (ctypes.c_char_p * max(len(paths), 1))(*[os.fsencode(p) for p in paths])
+        pp, ap, cnt, hits = _vp(), _vp(), _u64(), _u32()
+        raised = []
+
+        def sink(_user, ptr, n):
+            try:
+                blk = np.empty(n, dtype=PAIR_DTYPE)
+                if n:
+                    ctypes.memmove(blk.ctypes.data, ptr, n * PAIR_DTYPE.itemsize)
+                return 1 if each(blk) else 0
+            except BaseException as e:  # (an exception may not cross the C frame)
+                raised.append(e)
+                return 1
+
+        cb = PAIR_SINK(sink)
+        st = _L.gg_precluster_files_each(self._c, arr, len(paths), ctypes.c_float(min_ani),
+                                         None if cache_dir is None else os.fsencode(cache_dir), cb, None,
+                                         ctypes.byref(pp), ctypes.byref(ap), ctypes.byref(cnt), ctypes.byref(hits))
+        self.last_cached = hits.value
+        if raised:
+            raise raised[0]
+        if st != GG_OK:
+            raise self._err(st)
+        return self._pairs_ani(pp, ap, cnt.value)
+
     # -- device-resident API (torch tensors on this context's device) ---------
     def sketch_device(self, d_words, runs, n_genomes, d_out, d_lens, stream=None):
         rp, nr, runs = _runs_arg(runs)
@@ -758,31 +794,34 @@ def distances(genome_fasta_paths, min_ani, num_kmers, kmer_length, sketch_cache_
     unchanged genome files from earlier runs; the result is the same."""
     log = logging.getLogger("galah")
     # At debug level the reference logs every compared pair
-    # (src/finch.rs:65-68): the call then asks for every pair (min_ani 0: the
-    # gate kernel emits all N (N - 1) / 2), logs each with its f64 distance and
-    # keeps those at or above min_ani, as the reference's loop does.
+    # (src/finch.rs:65-68): the library then streams all N (N - 1) / 2 pairs
+    # in row blocks (gg_precluster_files_each), each logged with its f64
+    # distance in the reference's loop order; the cache is filled from the
+    # passing pairs as at any other level, so no block outlives its lines.
     every = log.isEnabledFor(logging.DEBUG)
     paths = list(genome_fasta_paths)
+    k = int(kmer_length)
+
+    def each(block):
+        for p in block:
+            d = ani_f64(int(p["common"]), int(p["total"]), k)
+            log.debug("Comparing %s and %s, distance %s", paths[int(p["i"])], paths[int(p["j"])], rust_f64(d))
+        return False
+
     try:
-        ctx = _context(int(kmer_length), int(num_kmers))
+        ctx = _context(k, int(num_kmers))
         log.info("Sketching MinHash representations of each genome with finch ..")  # src/finch.rs:46
-        pairs, ani = ctx.precluster_files(paths, 0.0 if every else float(np.float32(min_ani)),
-                                          cache_dir=sketch_cache_dir)
+        thr = float(np.float32(min_ani))
+        if every:
+            pairs, ani = ctx.precluster_files_each(paths, thr, each, cache_dir=sketch_cache_dir)
+        else:
+            pairs, ani = ctx.precluster_files(paths, thr, cache_dir=sketch_cache_dir)
     except GalahGpuError as e:
         # src/finch.rs:50
         raise RuntimeError("Failed to sketch genomes with finch: %s" % e) from e
     log.info("Finished sketching genomes")  # src/finch.rs:48
     log.info(ctx.info_line())  # device count, phase times, fallbacks (gg_info_line)
     cache = SortedPairGenomeDistanceCache()
-    if every:
-        thr = float(np.float32(min_ani))
-        for p in pairs:
-            i, j = int(p["i"]), int(p["j"])
-            d = ani_f64(int(p["common"]), int(p["total"]), int(kmer_length))
-            log.debug("Comparing %s and %s, distance %s", paths[i], paths[j], rust_f64(d))
-            if d >= thr:
-                cache.insert((i, j), np.float32(d))
-        return cache
     for p, a in zip(pairs, ani):
         cache.insert((int(p["i"]), int(p["j"])), np.float32(a))
     return cache

@@ -757,8 +757,12 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   GG_HIP(c, scratch_t(c, "idx_info", 4, &b.info));
   b.flags = reinterpret_cast<uint32_t*>(b.info + 2);
   GG_HIP(c, scratch_t(c, "idx_keys_in", total, &b.keys_in));
-  GG_HIP(c, scratch_t(c, "idx_keys_out", total, &b.keys_out));
-  GG_HIP(c, scratch_t(c, "idx_vals_in", total, &b.vals_in));
+  // (+16: the super-bin sort reads keys_out as bytes and vals_in as u32 in
+  // aligned groups of 16 entries up to ceil(total / 16) * 16; the split build
+  // places `total` of them, so the last group's tail is in bounds whatever
+  // the element widths -- ADVICE round 5)
+  GG_HIP(c, scratch_t(c, "idx_keys_out", total + 16, &b.keys_out));
+  GG_HIP(c, scratch_t(c, "idx_vals_in", total + 16, &b.vals_in));
   GG_HIP(c, scratch_t(c, "idx_vals_out", total, &b.vals_out));
   GG_HIP(c, scratch_t(c, "idx_runinfo", total, &b.runinfo));
   GG_HIP(c, scratch_t(c, "idx_mixed", (total + 31) / 32, &b.mixed));
@@ -1156,6 +1160,7 @@ const char* gg_status_string(gg_status s) {
     case GG_ERR_OUT_OF_MEMORY: return "out of memory";
     case GG_ERR_INTERNAL: return "internal error";
     case GG_ERR_OUTPUT_FULL: return "output buffer full";
+    case GG_ERR_CANCELLED: return "cancelled by the caller";
   }
   return "unknown status";
 }
@@ -1440,6 +1445,20 @@ gg_status gg_info_line(const gg_ctx* ctx, char* buf, size_t cap) {
     for (size_t i = 0; i < ctx->devs.size(); ++i)
       out += (i ? "," : "") + std::to_string(ctx->devs[i]->inflate_dev_batches);
     out += "]";
+  }
+  // device inflate: batches planned again (gzip member boundaries found on
+  // the device; full-size token areas after a tight one filled) and the
+  // largest scratch one lane used for a batch
+  uint64_t mplans = ctx->gz_member_plans, fplans = ctx->gz_full_plans, scr = ctx->gz_scratch_bytes;
+  for (const gg_ctx* m : ctx->devs) {
+    mplans += m->gz_member_plans;
+    fplans += m->gz_full_plans;
+    scr = std::max(scr, m->gz_scratch_bytes);
+  }
+  if (dev_batches) {
+    snprintf(line, sizeof line, "; inflate replans: members %llu, full areas %llu; lane scratch %.0f MB",
+             (unsigned long long)mplans, (unsigned long long)fplans, scr / 1e6);
+    out += line;
   }
   const size_t n = std::min(cap - 1, out.size());
   memcpy(buf, out.data(), n);

@@ -143,6 +143,13 @@ struct gg_ctx {
   // gg_fallbacks (the two index entries are read from pair_paths)
   uint64_t fallbacks[GG_FALLBACK_COUNT] = {};
   uint64_t inflate_dev_batches = 0;  // gzip batches inflated on the device (gg_info_line)
+  // device-inflate plans beyond a batch's first: member boundaries found by
+  // the decode (files of several gzip members), full-size token areas after
+  // a tight one filled (gg_info_line)
+  uint64_t gz_member_plans = 0, gz_full_plans = 0;
+  // the largest inflate scratch of a batch on this lane (tokens, sub-span
+  // areas, val, text), bytes: the per-lane footprint the info line reports
+  uint64_t gz_scratch_bytes = 0;
   // multi-device context: [a * M + b] = 1 when member a reaches member b's
   // memory directly (same device, or peer access enabled), gg_peer_links
   std::vector<uint8_t> peer_direct;
@@ -274,6 +281,7 @@ struct GzClaims {
   std::mutex mu;
   uint32_t cursor = 0;
   std::vector<uint32_t> back;  // claimed, given back
+  std::vector<uint32_t> abandoned;  // placed in a batch that was dropped undecoded
   uint32_t batches = 0;        // batches begun (the first ones are cut smaller)
   // the tail of the list cut into equal batches, a multiple of the stagers
   // (members x lanes), so that they finish together instead of the last
@@ -290,6 +298,7 @@ struct GzClaims {
   std::string err_msg;
   bool claim(uint32_t* i);
   void give_back(uint32_t i);
+  void abandon(const std::vector<uint32_t>& idx);
   void file_error(uint32_t i, gg_status st, const std::string& msg);
   void halt();
 };

@@ -273,7 +273,10 @@ struct InflateDecode {
   // read), the rest read global memory
   uint32_t n_staged = 0;
   uint32_t stage_words = 0;  // LDS stage of the staged kernel (0: its default; GALAHGPU_TEST_STAGE_KB)
+  uint32_t tight = 0;        // sub-span token areas sized for 1/4 token per bit (inflate::span_cap)
 };
+// The staged decode's default LDS stage, in words (inflate.hip).
+uint32_t inflate_stage_words();
 // The words from start_bit to end_bit touch, + the readers' look-ahead.
 __host__ __device__ inline uint64_t inflate_segment_words(uint64_t start_bit, uint64_t end_bit) { return (end_bit + 31) / 32 - start_bit / 32 + 8; }
 struct InflatePlace {
@@ -296,11 +299,30 @@ constexpr uint8_t kTextPtr = 0xFF;  // (a literal 0xFF byte is also read through
 // [data_off, data_off + data_len) of the batch (data_off 4-byte aligned):
 // the deflate data of a gzip member with its trailer's isize and crc, or
 // plain text (gz false)
+// One gzip member of a file: its deflate data at [off, off + len) of the
+// batch and its trailer's CRC-32 and ISIZE.
+struct GzMember {
+  uint64_t off = 0, len = 0;
+  uint32_t isize = 0, crc = 0;
+};
+// A file of several gzip members (needletail's reader, behind
+// src/finch.rs:47, reads them one after the other): `members` in file
+// order, data_off the first one's deflate data (4-byte aligned).  Empty for
+// one member (data_off / data_len / isize / crc) or plain text.
 struct InflateFile {
   uint64_t data_off = 0, data_len = 0;
   uint32_t isize = 0, crc = 0;
   bool gz = false;
+  std::vector<GzMember> members;
 };
+// The members of a BGZF file (bgzip: every member's header carries the 'BC'
+// extra subfield with the member's size) at buf[0, n), whose first byte is
+// at batch offset base; false (out untouched) when a member header lacks
+// the subfield or a size runs past n -- the members are then found on the
+// device as they end (inflate_batch).
+bool bgzf_members(const uint8_t* buf, uint64_t n, uint64_t base, std::vector<GzMember>& out);
+// A BGZF member's total size from the header at b[0, n) ('BC' subfield), 0 without one.
+uint64_t bgzf_member_size(const uint8_t* b, uint64_t n);
 bool gzip_member(const uint8_t* buf, size_t n, size_t* data_off, size_t* data_len, uint32_t* isize, uint32_t* crc);
 // The gzip header at the start of buf[0, n) (of a file of file_size bytes):
 // its length (*data_off); false when it is not gzip (CM 8), has reserved

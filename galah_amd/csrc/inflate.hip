@@ -694,8 +694,8 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       const bool act = j < nsub;
       const uint64_t S = bstart + j * L;
       const uint64_t R = j + 1 == nsub ? wend : S + L;
-      const uint64_t capL = span_cap(L), ncks = span_cks(L);
-      uint32_t* A = scr_all + j * span_words(L);  // first decode
+      const uint64_t capL = span_cap(L, a.tight), ncks = span_cks(L);
+      uint32_t* A = scr_all + j * span_words(L, a.tight);  // first decode
       uint32_t* B = A + capL;                     // second decode
       uint64_t* ck = (uint64_t*)(B + capL);       // the first decode's checkpoints
       // the first decode, from S
@@ -1131,9 +1131,13 @@ __global__ __launch_bounds__(kCrcThreads) void inflate_crc_seg_kernel(const uint
   const uint32_t f = lo;
   const uint64_t off = (uint64_t)(g - seg_first[f]) * kCrcSeg;
   const uint32_t len = (uint32_t)min<uint64_t>(kCrcSeg, file_len[f] - off);
-  const uint8_t* p = text + file_text[f] + off;  // (16-byte aligned)
+  const uint8_t* p = text + file_text[f] + off;
   uint32_t c = 0xFFFFFFFFu;
   uint32_t i = 0;
+  // (a file's text starts on a 16-byte boundary; a later gzip member's
+  // anywhere: its bytes before the first boundary one at a time)
+  const uint32_t head = min(len, (uint32_t)(16u - ((uint32_t)(uintptr_t)p & 15u)) & 15u);
+  for (; i < head; ++i) c = T[0][(c ^ p[i]) & 0xFFu] ^ (c >> 8);
   for (; i + 16 <= len; i += 16) {
     const uint4 v = *(const uint4*)(p + i);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -1245,6 +1249,8 @@ __global__ __launch_bounds__(kUploadThreads) void slot_upload_kernel(uint4* __re
 }
 
 }  // namespace
+
+uint32_t inflate_stage_words() { return kStageWords; }
 
 hipError_t launch_slot_upload(uint8_t* dst, const uint8_t* src_mapped, uint64_t bytes, hipStream_t st) {
   const uint64_t n16 = (bytes + 15) / 16;  // (both buffers are padded past bytes to a 16-byte multiple)

@@ -964,16 +964,24 @@ GG_HD void span_layout(uint64_t body0, uint64_t span_end, uint32_t max_lanes, ui
 #define GG_DECODE_WARM_BITS 256
 #endif
 constexpr uint64_t kWarmBits = GG_DECODE_WARM_BITS;  // a lane's first decode starts this far before its span
-GG_HD uint64_t span_cap(uint64_t L) { return (L + kWarmBits + kCkBits + 3) / 4 * 4; }
+// tight: a quarter of that plus 64 (FASTA streams emit ~0.08 tokens per
+// bit; a decode that fills a tight area fails its batch's first attempt,
+// which is then decoded again with full areas: inflate_host.cpp)
+GG_HD uint64_t span_cap(uint64_t L, bool tight = false) {
+  const uint64_t bits = L + kWarmBits + kCkBits;
+  return ((tight ? bits / 4 + 64 : bits) + 3) / 4 * 4;
+}
 GG_HD uint64_t span_cks(uint64_t L) { return (L / kCkBits + 4) & ~1ull; }  // (even: areas stay 16-byte aligned)
-GG_HD uint64_t span_words(uint64_t L) { return 2 * span_cap(L) + 2 * span_cks(L); }  // (u32 words, even)
+GG_HD uint64_t span_words(uint64_t L, bool tight = false) { return 2 * span_cap(L, tight) + 2 * span_cks(L); }  // (u32 words, even)
 // Scratch words the device decode of a segment of seg_bits bits needs (L
-// as span_layout makes it for the segment's longest possible body).
-GG_HD uint64_t decode_scratch(uint64_t seg_bits) {
+// as span_layout makes it for the segment's longest possible body, or for
+// the longest window of window_bits when the segment is decoded in windows
+// of at most that many bits).
+GG_HD uint64_t decode_scratch(uint64_t seg_bits, uint64_t window_bits = ~0ull, bool tight = false) {
   uint64_t L;
   uint32_t nsub;
-  span_layout(0, seg_bits, 64, L, nsub);
-  return 64 * span_words(L);
+  span_layout(0, seg_bits < window_bits ? seg_bits : window_bits, 64, L, nsub);
+  return 64 * span_words(L, tight);
 }
 
 }  // namespace inflate

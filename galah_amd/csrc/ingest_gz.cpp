@@ -71,6 +71,11 @@ void GzClaims::file_error(uint32_t i, gg_status st, const std::string& msg) {
   }
 }
 
+void GzClaims::abandon(const std::vector<uint32_t>& idx) {
+  std::lock_guard<std::mutex> lk(mu);
+  abandoned.insert(abandoned.end(), idx.begin(), idx.end());
+}
+
 void GzClaims::halt() {
   std::lock_guard<std::mutex> lk(mu);
   stop = true;
@@ -134,6 +139,7 @@ struct Probe {
   uint64_t size = 0;
   bool gz = false;       // gzip magic
   bool member = false;   // a gzip member whose header the device path reads
+  bool bgzf = false;     // its header has BGZF's member size (bgzip): the members are walked once read
   size_t doff = 0;       // its deflate data [doff, doff + dlen)
   uint64_t dlen = 0;
   uint32_t isize = 0, crc = 0;
@@ -190,6 +196,7 @@ void probe_file(const char* path, bool stamp, Probe& p) {
       p.dlen = p.size - 8 - p.doff;
       p.crc = (uint32_t)tail[0] | ((uint32_t)tail[1] << 8) | ((uint32_t)tail[2] << 16) | ((uint32_t)tail[3] << 24);
       p.isize = (uint32_t)tail[4] | ((uint32_t)tail[5] << 8) | ((uint32_t)tail[6] << 16) | ((uint32_t)tail[7] << 24);
+      p.bgzf = bgzf_member_size(head, hn) != 0;
     }
     return;  // (a gzip file whose header this path does not read: its batch is decoded on the host)
   }
@@ -233,6 +240,14 @@ class GzStager {
   GzStager(gg_ctx* m, GzClaims& cl, int threads) : m_(m), cl_(cl), threads_(threads) {}
   ~GzStager() {
     if (next_.valid()) next_.wait();
+    // a batch staged but never processed (the lane stopped on an error):
+    // its files were claimed but not decoded, so a file error among them
+    // is still to be found (gz_settle_errors); its timing events go
+    for (int si = 0; si < 2; ++si) {
+      GzStaged& g = staged_[si];
+      if (si != cur_ || !consumed_) cl_.abandon(g.idx);
+      drop_events(g);
+    }
   }
   // The next staged batch (nullptr: no more); starts staging the one after.
   GzStaged* next() {
@@ -242,8 +257,12 @@ class GzStager {
     } else {
       have = stage(slot_, staged_[slot_]);
     }
-    if (!have) return nullptr;
+    if (!have) {
+      staged_[slot_].idx.clear();  // (nothing staged there)
+      return nullptr;
+    }
     cur_ = slot_;
+    consumed_ = true;
     slot_ ^= 1;
     if (staged_[cur_].st == GG_OK && !staged_[cur_].file_err)
       next_ = std::async(std::launch::async, [this] {
@@ -259,7 +278,13 @@ class GzStager {
  private:
   // Claims files and stages them into slot si until the batch is full or no
   // file is left; false when it got no file.
+  static void drop_events(GzStaged& g) {
+    if (g.up_a) (void)hipEventDestroy(g.up_a);
+    if (g.up_b) (void)hipEventDestroy(g.up_b);
+    g.up_a = g.up_b = nullptr;
+  }
   bool stage(int si, GzStaged& g) {
+    drop_events(g);  // (a batch left unprocessed kept its upload events)
     g = GzStaged{};
     g.t0 = Clock::now();
     int ramp;
@@ -341,6 +366,7 @@ class GzStager {
         const uint64_t len = pr.converted ? pr.text.size() : pr.size;
         const uint64_t doff = pr.member ? pr.doff : 0;
         uint64_t p;
+        size_t slot_file = 0;
         {
           std::lock_guard<std::mutex> lk(bm);
           if (full || g.st != GG_OK || g.file_err) {
@@ -374,6 +400,7 @@ class GzStager {
           f.data_len = pr.member ? pr.dlen : len;
           f.isize = pr.isize;
           f.crc = pr.crc;
+          slot_file = g.files.size();
           g.idx.push_back(i);
           g.files.push_back(f);
           g.held.push_back(GzHeld{p, len, pr.gz});
@@ -391,6 +418,12 @@ class GzStager {
           std::lock_guard<std::mutex> lk(bm);
           cl_.file_error(i, GG_ERR_IO, std::string("read error in ") + cl_.paths[i]);
           g.file_err = true;
+        } else if (pr.bgzf) {  // bgzip: every member from its header's size field
+          std::vector<GzMember> ms;
+          if (bgzf_members(sl.host + p, len, p, ms)) {
+            std::lock_guard<std::mutex> lk(bm);
+            g.files[slot_file].members.swap(ms);
+          }
         }
       }
     };
@@ -418,6 +451,7 @@ class GzStager {
   int threads_;
   GzStaged staged_[2];
   int slot_ = 0, cur_ = 0;
+  bool consumed_ = false;  // staged_[cur_] was handed to the lane
   std::future<bool> next_;
 };
 
@@ -428,7 +462,10 @@ gg_status inflate_staged_batch(gg_ctx* m, GzStager& pipe, GzStaged& g, GzClaims&
                                uint32_t** d_words, uint64_t* nw, std::vector<gg_run>& runs) {
   const auto t0 = Clock::now();
   if (g.st != GG_OK) return fail(m, g.st, g.err);
-  if (g.file_err) return fail(m, GG_ERR_IO, "a file did not read");  // (the call reports the file's own error)
+  if (g.file_err) {  // (the call reports the file's own error; the batch's other files were never decoded)
+    cl.abandon(g.idx);
+    return fail(m, GG_ERR_IO, "a file did not read");
+  }
   if (g.up_a) {  // (the stager's upload, timed: the lane's events from here on)
     m->timed.push_back(gg_ctx::Timed{GG_KERNEL_UPLOAD, g.up_a, g.up_b, g.at});
     g.up_a = g.up_b = nullptr;
@@ -582,6 +619,10 @@ gg_status gz_member_ingest(gg_ctx* m, GzClaims& cl, uint64_t* d_sk, uint32_t* d_
     }
     m->inflate_dev_batches += lanes[l]->inflate_dev_batches;
     lanes[l]->inflate_dev_batches = 0;
+    m->gz_member_plans += lanes[l]->gz_member_plans;
+    m->gz_full_plans += lanes[l]->gz_full_plans;
+    lanes[l]->gz_member_plans = lanes[l]->gz_full_plans = 0;
+    m->gz_scratch_bytes = std::max(m->gz_scratch_bytes, lanes[l]->gz_scratch_bytes);
     m->timed.insert(m->timed.end(), lanes[l]->timed.begin(), lanes[l]->timed.end());  // (the events are m's now)
     lanes[l]->timed.clear();
   }
@@ -595,10 +636,16 @@ gg_status gz_member_ingest(gg_ctx* m, GzClaims& cl, uint64_t* d_sk, uint32_t* d_
 
 void gz_settle_errors(GzClaims& cl) {
   if (cl.err_idx == UINT32_MAX) return;
+  // files below the failing one that were given back, or placed in a batch
+  // that was dropped before its decode (a read error elsewhere in it, or a
+  // lane's prefetched batch after its lane stopped), were never checked
   std::vector<uint32_t> lower;
   for (uint32_t i : cl.back)
     if (i < cl.err_idx) lower.push_back(i);
+  for (uint32_t i : cl.abandoned)
+    if (i < cl.err_idx) lower.push_back(i);
   std::sort(lower.begin(), lower.end());
+  lower.erase(std::unique(lower.begin(), lower.end()), lower.end());
   for (uint32_t i : lower) {  // (never read: read and decoded here, in index order)
     Probe pr;
     probe_file(cl.paths[i], false, pr);

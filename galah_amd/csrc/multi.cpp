@@ -1003,6 +1003,64 @@ gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths, uint32_t n_
   return gg_precluster_files_cached(ctx, paths, n_paths, min_ani, nullptr, pairs, ani, n_out, nullptr);
 }
 
+gg_status gg_precluster_files_each(gg_ctx* ctx, const char* const* paths, uint32_t n_paths, float min_ani,
+                                   const char* cache_dir, gg_pair_sink sink, void* user, gg_pair** pairs,
+                                   float** ani, uint64_t* n_out, uint32_t* n_cached) {
+  if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");
+  if (!sink || !pairs || !ani || !n_out || (n_paths && !paths))
+    return fail(ctx, GG_ERR_INVALID_ARG, "gg_precluster_files_each: null argument");
+  if (std::isnan(min_ani)) return fail(ctx, GG_ERR_INVALID_ARG, "min_ani is NaN");
+  *pairs = nullptr;
+  *ani = nullptr;
+  *n_out = 0;
+  if (n_cached) *n_cached = 0;
+  for (double& x : ctx->phase_ms) x = 0.0;
+  const std::vector<gg_ctx*> ms = members(ctx);
+  std::vector<Rows> rows;
+  std::vector<RowSpan> spans;
+  std::vector<gg_pair> res;
+  auto t0 = Clock::now();
+  gg_status st = sketch_files_members(ctx, ms, paths, n_paths, cache_dir, rows, spans, nullptr, nullptr, n_cached);
+  if (st != GG_OK) return st;
+  ctx->phase_ms[GG_PHASE_SKETCH] = ms_since(t0);
+  if (n_paths >= 2) {
+    // the passing pairs as gg_precluster_files finds them (the index K2);
+    // afterwards every member holds every row
+    st = gather_pairs_merge(ctx, ms, rows, spans, n_paths, min_ani, res);
+    if (st != GG_OK) return st;
+    // every compared pair (src/finch.rs:53-68), min_ani 0 (the gate kernel
+    // emits all of them), on member 0 in blocks of whole tile rows of at
+    // most ~kEachPairs pairs, each sorted by (i, j): memory stays bounded by
+    // a block whatever N is
+    uint64_t kEachPairs = 1ull << 22;
+    if (const char* e = getenv("GALAHGPU_EACH_PAIRS"))  // (tests: smaller blocks)
+      if (atoll(e) > 0) kEachPairs = (uint64_t)atoll(e);
+    gg_ctx* m = ms[0];
+    if (hipSetDevice(m->device) != hipSuccess) return fail(ctx, GG_ERR_HIP, "hipSetDevice failed");
+    const uint64_t n = n_paths, nb = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
+    auto row_tile = [&](uint64_t I) { return I * nb - I * (I - 1) / 2; };  // first tile of tile row I
+    std::vector<gg_pair> blk;
+    for (uint64_t a = 0; a < nb;) {
+      uint64_t b = a, cnt = 0;
+      do {  // tile row b: rows [64 b, 64 b + 64) against every later genome
+        const uint64_t r0 = b * GG_PAIR_TILE, r1 = std::min(n, r0 + GG_PAIR_TILE);
+        for (uint64_t i = r0; i < r1; ++i) cnt += n - 1 - i;
+        ++b;
+      } while (b < nb && cnt < kEachPairs);
+      blk.clear();
+      st = pairs_range_to_host(m, rows[0].sk, rows[0].len, n_paths, row_tile(a), row_tile(b), 0.0f, blk, m->stream);
+      if (st != GG_OK) {
+        if (m != ctx) ctx->err = m->err;
+        return st;
+      }
+      if (sink(user, blk.data(), blk.size()) != 0)
+        return fail(ctx, GG_ERR_CANCELLED, "gg_precluster_files_each: the pair sink stopped the call");
+      a = b;
+    }
+  }
+  return pairs_with_ani(ctx, res, pairs, ani, n_out);
+}
+
 gg_status gg_precluster_shards(gg_ctx* ctx, const gg_shard* shards, float min_ani, gg_pair** pairs, float** ani,
                                uint64_t* n_out) {
   if (!ctx) return fail(nullptr, GG_ERR_INVALID_ARG, "null context");

@@ -130,11 +130,25 @@ inline SortedPairGenomeDistanceCache distances_on(gg_ctx* ctx, const std::vector
   float* ani = nullptr;
   uint64_t n = 0;
   info("Sketching MinHash representations of each genome with finch ..");  // src/finch.rs:46
-  // at debug level every pair is asked for (min_ani 0: the gate kernel emits
-  // all of them), logged with its f64 distance and kept if >= min_ani
-  const bool every = (bool)debug_sink();
-  const gg_status st = gg_precluster_files(ctx, c_paths.data(), (uint32_t)c_paths.size(), every ? 0.0f : min_ani,
-                                           &pairs, &ani, &n);
+  // at debug level every compared pair is logged (src/finch.rs:65-68): the
+  // library streams all N (N - 1) / 2 of them in row blocks, in the
+  // reference's loop order, while the returned pairs are those >= min_ani
+  struct Each {
+    const std::vector<std::string>* paths;
+    int k;
+    static int sink(void* user, const gg_pair* p, uint64_t n) {
+      const Each* e = (const Each*)user;
+      for (uint64_t x = 0; x < n; ++x)
+        debug_sink()("Comparing " + (*e->paths)[p[x].i] + " and " + (*e->paths)[p[x].j] + ", distance " +
+                     rust_f64(gg_ani_f64(p[x].common, p[x].total, e->k)));
+      return 0;
+    }
+  } each{&paths, kmer_length};
+  const gg_status st = debug_sink()
+                           ? gg_precluster_files_each(ctx, c_paths.data(), (uint32_t)c_paths.size(), min_ani, nullptr,
+                                                      &Each::sink, &each, &pairs, &ani, &n, nullptr)
+                           : gg_precluster_files(ctx, c_paths.data(), (uint32_t)c_paths.size(), min_ani, &pairs, &ani,
+                                                 &n);
   if (st != GG_OK) {
     std::string msg = gg_last_error(ctx);
     gg_destroy(ctx);
@@ -144,15 +158,7 @@ inline SortedPairGenomeDistanceCache distances_on(gg_ctx* ctx, const std::vector
   char line[1024];
   if (gg_info_line(ctx, line, sizeof line) == GG_OK) info(line);
   SortedPairGenomeDistanceCache cache;
-  for (uint64_t i = 0; i < n; ++i) {
-    if (every) {  // src/finch.rs:65-71
-      const double d = gg_ani_f64(pairs[i].common, pairs[i].total, kmer_length);
-      debug_sink()("Comparing " + paths[pairs[i].i] + " and " + paths[pairs[i].j] + ", distance " + rust_f64(d));
-      if (d >= (double)min_ani) cache.insert({pairs[i].i, pairs[i].j}, (float)d);
-    } else {
-      cache.insert({pairs[i].i, pairs[i].j}, ani[i]);  // src/finch.rs:70
-    }
-  }
+  for (uint64_t i = 0; i < n; ++i) cache.insert({pairs[i].i, pairs[i].j}, ani[i]);  // src/finch.rs:70
   gg_free(pairs);
   gg_free(ani);
   gg_destroy(ctx);

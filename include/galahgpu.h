@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define GG_ABI_VERSION 6u
+#define GG_ABI_VERSION 7u
 
 typedef enum gg_status {
   GG_OK = 0,
@@ -59,7 +59,8 @@ typedef enum gg_status {
   GG_ERR_HIP = 5,         /* HIP runtime error */
   GG_ERR_OUT_OF_MEMORY = 6,
   GG_ERR_INTERNAL = 7,
-  GG_ERR_OUTPUT_FULL = 8  /* device pair buffer too small; *count holds the need */
+  GG_ERR_OUTPUT_FULL = 8, /* device pair buffer too small; *count holds the need */
+  GG_ERR_CANCELLED = 9    /* a caller's callback asked to stop (gg_precluster_files_each) */
 } gg_status;
 
 typedef struct gg_ctx gg_ctx;
@@ -210,6 +211,20 @@ gg_status gg_pairs_device(gg_ctx* ctx, const uint64_t* d_sketches,
 gg_status gg_precluster_files(gg_ctx* ctx, const char* const* paths,
                               uint32_t n_paths, float min_ani, gg_pair** pairs,
                               float** ani, uint64_t* n_out);
+
+/* galah's debug level (src/finch.rs:65-68 logs every compared pair): the
+ * same call, plus every pair i < j of the N(N-1)/2, whatever its ANI,
+ * handed to sink in blocks of whole 64-genome tile rows (at most ~4M pairs
+ * each, common and total set; gg_ani_f64 gives the printed distance), in
+ * (i, j) order over the call, so memory stays bounded by one block.  sink
+ * returns 0 to go on; anything else ends the call with GG_ERR_CANCELLED.
+ * *pairs / *ani / *n_out are the pairs >= min_ani, as gg_precluster_files
+ * returns them.  cache_dir as gg_precluster_files_cached (NULL: none). */
+typedef int (*gg_pair_sink)(void* user, const gg_pair* pairs, uint64_t n);
+gg_status gg_precluster_files_each(gg_ctx* ctx, const char* const* paths, uint32_t n_paths,
+                                   float min_ani, const char* cache_dir, gg_pair_sink sink,
+                                   void* user, gg_pair** pairs, float** ani, uint64_t* n_out,
+                                   uint32_t* n_cached);
 
 /* One member's shard of device-resident packed genomes for
  * gg_precluster_shards: d_words lives on that member's device, runs (host

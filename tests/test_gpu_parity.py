@@ -84,6 +84,42 @@ def test_debug_logs_every_compared_pair(golden, caplog):
         assert line == "Comparing %s and %s, distance %s" % (paths[i], paths[j], ga.rust_f64(oracle.ani(c, t))), line
 
 
+@pytest.mark.parametrize("block_pairs", ["1", "10000"])
+def test_each_streams_every_pair_in_blocks(gpu_ctx, golden, block_pairs, monkeypatch):
+    """gg_precluster_files_each (the debug level's every-pair stream,
+    src/finch.rs:53-68) over 162 genomes (the 27 golden files six times:
+    three tile rows): every i < j exactly once, in (i, j) order across the
+    blocks, each with the oracle's (common, total); the returned pairs are
+    precluster_files' own.  GALAHGPU_EACH_PAIRS=1 makes every tile row a
+    block of its own; 10000 puts two rows in the first block."""
+    monkeypatch.setenv("GALAHGPU_EACH_PAIRS", block_pairs)
+    n0 = len(golden["paths"])
+    paths = golden["paths"] * 6
+    n = len(paths)
+    table = {(int(i), int(j)): (int(c), int(t)) for (i, j, c, t, _a) in golden["pairs"]}
+    lens = golden["lens"]
+    blocks = []
+    min_ani = ga.parse_percentage(95)
+    pairs, ani = gpu_ctx.precluster_files_each(paths, min_ani, lambda b: blocks.append(b.copy()))
+    want_pairs, want_ani = gpu_ctx.precluster_files(paths, min_ani)
+    assert as_tuples(pairs) == as_tuples(want_pairs) and (ani == want_ani).all()
+    assert len(blocks) == (3 if block_pairs == "1" else 2)
+    got = np.concatenate(blocks)
+    assert len(got) == n * (n - 1) // 2
+    ij = [(i, j) for i in range(n) for j in range(i + 1, n)]
+    assert [(int(r["i"]), int(r["j"])) for r in got] == ij
+    for r in got:
+        a, b = int(r["i"]) % n0, int(r["j"]) % n0
+        exp = (int(lens[a]), int(lens[a])) if a == b else table[(min(a, b), max(a, b))]
+        assert (int(r["common"]), int(r["total"])) == exp
+
+
+def test_each_sink_can_stop_the_call(gpu_ctx, golden):
+    with pytest.raises(ga.GalahGpuError) as e:
+        gpu_ctx.precluster_files_each(golden["paths"], np.float32(0.9), lambda b: True)
+    assert e.value.status == 9
+
+
 def test_precluster_files_matches_oracle(gpu_ctx, golden):
     min_ani = ga.parse_percentage(90)
     pairs, ani = gpu_ctx.precluster_files(golden["paths"], min_ani)

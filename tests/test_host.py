@@ -48,7 +48,7 @@ def test_abi_exports_every_declared_symbol():
     L = ga.lib()
     for name in declared:
         assert hasattr(L, name), name
-    assert ga.abi_version() == 6
+    assert ga.abi_version() == 7
 
 
 def test_no_oracle_in_product_library():

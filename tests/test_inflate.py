@@ -130,18 +130,127 @@ def test_device_inflate_streams_and_handbacks(tmp_path, monkeypatch):
     dsk, dl, fb = sketch_files(paths, monkeypatch, "device")
     assert fb["inflate_host"] == 0
     assert (dl == hl).all() and all((dsk[g][:dl[g]] == hsk[g][:hl[g]]).all() for g in range(len(paths)))
-    # several members (bgzip-like) and FASTQ: the batch goes back to the host
+    # two concatenated members: inflated on the device (its boundary found
+    # by the decode); FASTQ: the batch goes back to the host
     seq = acgt[rng.integers(0, 4, 100000)].tobytes()
     multi = tmp_path / "multi.fa.gz"
     multi.write_bytes(gzip.compress(b">m\n" + seq[:50000]) + gzip.compress(seq[50000:] + b"\n"))
     fq = tmp_path / "reads.fq.gz"
     fq.write_bytes(gzip.compress(b"@r1\n" + seq[:5000] + b"\n+\n" + b"I" * 5000 + b"\n"))
-    for extra in (multi, fq):
+    for extra, host_batches in ((multi, 0), (fq, 1)):
         ps = paths[:3] + [str(extra)]
         hsk, hl, _ = sketch_files(ps, monkeypatch, "host")
         dsk, dl, fb = sketch_files(ps, monkeypatch, "device")
-        assert fb["inflate_host"] == 1, extra
+        assert fb["inflate_host"] == host_batches, extra
         assert (dl == hl).all() and all((dsk[g][:dl[g]] == hsk[g][:hl[g]]).all() for g in range(len(ps)))
+
+
+def bgzip(data, level=6, block=65280, eof=True):
+    """BGZF (bgzip; SAM/BAM specification 4.1): members of <= 64 KB of
+    input, each header with the 'BC' extra subfield holding the member's
+    size - 1, then the 28-byte empty end-of-file member."""
+    out = []
+    for i in range(0, max(len(data), 1), block):
+        chunk = data[i:i + block]
+        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+        body = c.compress(chunk) + c.flush()
+        bsize = 18 + len(body) + 8 - 1
+        hdr = bytes([0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 66, 67, 2, 0]) + bsize.to_bytes(2, "little")
+        out.append(hdr + body + zlib.crc32(chunk).to_bytes(4, "little") + (len(chunk) & 0xffffffff).to_bytes(4, "little"))
+    if eof:
+        out.append(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+    return b"".join(out)
+
+
+def fasta_text(rng, n, name, width=80):
+    seq = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)].tobytes()
+    return b">%s\n" % name + b"\n".join(seq[j:j + width] for j in range(0, len(seq), width)) + b"\n"
+
+
+@pytest.mark.gpu
+def test_device_inflate_gzip_members(tmp_path, monkeypatch):
+    """needletail 0.5 (Cargo.toml:32, behind src/finch.rs:47) reads a file of
+    several gzip members as one stream.  bgzip (BGZF) files -- their members
+    known from the headers' size field -- and concatenated members of plain
+    gzip (`cat a.gz b.gz`, boundaries found by the decode) in a list with
+    single-member files: every batch inflated on the device (inflate_host 0),
+    sketches equal to the oracle's (zlib's gzread reads every member)."""
+    rng = np.random.default_rng(31)
+    paths = []
+    for i in range(6):  # bgzip: 1.2 Mbp, ~19 members of 64 KB each + the EOF member
+        p = tmp_path / ("bgz%d.fna.gz" % i)
+        p.write_bytes(bgzip(fasta_text(rng, 1200000, b"bgz%d" % i), level=1 + i % 9))
+        paths.append(str(p))
+    for i in range(4):  # concatenated: 2-5 members of random sizes, some beyond a search chunk
+        parts, text = [], fasta_text(rng, int(rng.integers(300000, 900000)), b"cat%d" % i)
+        cuts = sorted(rng.choice(np.arange(1, len(text)), size=1 + i, replace=False).tolist())
+        for a, b in zip([0] + cuts, cuts + [len(text)]):
+            parts.append(gzip.compress(text[a:b], 6))
+        p = tmp_path / ("cat%d.fna.gz" % i)
+        p.write_bytes(b"".join(parts))
+        paths.append(str(p))
+    for i in range(3):  # single members between them
+        p = tmp_path / ("one%d.fna.gz" % i)
+        p.write_bytes(gzip.compress(fasta_text(rng, 700000, b"one%d" % i), 6))
+        paths.insert(3 * i + 1, str(p))
+    small = tmp_path / "bgz_small.fna.gz"  # one data member + the EOF member
+    small.write_bytes(bgzip(fasta_text(rng, 20000, b"small")))
+    paths.append(str(small))
+    exp_sk, exp_len = oracle.sketch_files(paths, threads=8)
+    for batch_files in ("4096", "3"):
+        monkeypatch.setenv("GALAHGPU_GZ_BATCH_FILES", batch_files)
+        monkeypatch.setenv("GALAHGPU_INFLATE", "device")
+        with ga.Context(k=21, sketch_size=1000) as ctx:
+            sk, lens, _ = ctx.sketch_files(paths)
+            fb = ctx.fallbacks()
+            line = ctx.info_line()
+        assert fb["inflate_host"] == 0, line
+        assert "inflate replans: members " in line and "members 0," not in line, line
+        assert (lens == exp_len).all()
+        for g in range(len(paths)):
+            assert (sk[g][:lens[g]] == exp_sk[g][:lens[g]]).all(), paths[g]
+    # a member header after the last member's end that is cut short: the host path's result
+    bad = tmp_path / "cat_trailing.fna.gz"
+    bad.write_bytes(gzip.compress(fasta_text(rng, 100000, b"t"), 6) + b"\x1f\x8b\x08\x00")
+    errs = {}
+    for mode in ("host", "device"):
+        monkeypatch.setenv("GALAHGPU_INFLATE", mode)
+        with ga.Context(k=21, sketch_size=1000) as ctx:
+            try:
+                sk, lens, _ = ctx.sketch_files([str(bad)])
+                errs[mode] = ("ok", sk[0][:lens[0]].tolist())
+            except ga.GalahGpuError as e:
+                errs[mode] = (e.status, str(e))
+    assert errs["device"] == errs["host"]
+
+
+@pytest.mark.gpu
+def test_device_inflate_full_areas_after_a_tight_plan(tmp_path, monkeypatch):
+    """Token areas are first sized at 1/4 token per compressed bit; a stream
+    denser than that (Huffman-only over a 2-letter alphabet: ~1 token per
+    1.x bits) fills them, and the batch is planned again with full areas --
+    same sketches as the host path, no batch handed back, the replan counted
+    in the info line.  GALAHGPU_GZ_TIGHT=0 starts with full areas."""
+    rng = np.random.default_rng(41)
+    paths = []
+    for i in range(3):
+        seq = np.frombuffer(b"AC", np.uint8)[rng.integers(0, 2, 600000)].tobytes()
+        text = b">dense%d\n" % i + b"\n".join(seq[j:j + 70] for j in range(0, len(seq), 70)) + b"\n"
+        c = zlib.compressobj(6, zlib.DEFLATED, 31, 8, zlib.Z_HUFFMAN_ONLY)
+        p = tmp_path / ("dense%d.fna.gz" % i)
+        p.write_bytes(c.compress(text) + c.flush())
+        paths.append(str(p))
+    hsk, hl, _ = sketch_files(paths, monkeypatch, "host")
+    for tight in ("1", "0"):
+        monkeypatch.setenv("GALAHGPU_GZ_TIGHT", tight)
+        monkeypatch.setenv("GALAHGPU_INFLATE", "device")
+        with ga.Context(k=21, sketch_size=1000) as ctx:
+            dsk, dl, _ = ctx.sketch_files(paths)
+            fb = ctx.fallbacks()
+            line = ctx.info_line()
+        assert fb["inflate_host"] == 0, line
+        assert ("full areas 0;" in line) == (tight == "0"), line
+        assert (dl == hl).all() and all((dsk[g][:dl[g]] == hsk[g][:hl[g]]).all() for g in range(len(paths)))
 
 
 @pytest.mark.gpu
