@@ -865,6 +865,7 @@ def run_lib(a, world, rank):
             cpu = cpu_baseline(sample, a.genome_len, d_sk.cpu().numpy().view(np.uint64),
                                d_len.cpu().numpy().view(np.uint32), a.k, s, min_ani, N, a.cpu_budget_s)
         del d_sk, d_len
+        pair_paths, fallbacks = ctx.pair_paths(), ctx.fallbacks()
         # the headline workload's context and inputs are released before the
         # files leg, which is a separate call as galah makes it in a fresh
         # process (with the C3 context and its ~10 GB of inputs still held, the
@@ -904,6 +905,8 @@ def run_lib(a, world, rank):
                                    "finalize": round(kst["finalize"]["ms"] / a.steps, 3),
                                    "k2": round(kst["pairs"]["ms"] / a.steps, 3)},
             "pairs_found": found,
+            "pair_paths": pair_paths,
+            "fallbacks": fallbacks,
             "roofline": roof,
             "roofline_k2": roof_k2,
             "cpu_baseline": cpu,

@@ -116,21 +116,22 @@ hipEvent_t take_event(gg_ctx* c) {
 namespace {
 
 // Number of pairs (i < j < n) in tiles [tb, te).
+// (O(tile rows): tile row I holds tiles (I, J), J = I .. nb - 1, numbered
+// from t0(I); the tiles of [tb, te) in it are J in [Ja, Jb))
 uint64_t pairs_in_tiles(uint32_t n, uint64_t tb, uint64_t te) {
   const uint64_t nb = (n + GG_PAIR_TILE - 1) / GG_PAIR_TILE;
-  uint64_t t = 0, acc = 0;
-  for (uint64_t I = 0; I < nb && t < te; ++I) {
-    const uint64_t ri = std::min<uint64_t>(GG_PAIR_TILE, n - I * GG_PAIR_TILE);
-    const uint64_t row_tiles = nb - I;
-    if (t + row_tiles <= tb) {
-      t += row_tiles;
-      continue;
+  uint64_t t0 = 0, acc = 0;
+  for (uint64_t I = 0; I < nb && t0 < te; ++I) {
+    const uint64_t row_tiles = nb - I, t1 = t0 + row_tiles;
+    const uint64_t a = std::max(t0, tb), b = std::min(t1, te);
+    if (a < b) {
+      const uint64_t Ja = I + (a - t0), Jb = I + (b - t0);
+      const uint64_t ri = std::min<uint64_t>(GG_PAIR_TILE, n - I * GG_PAIR_TILE);
+      if (Ja == I) acc += ri * (ri - 1) / 2;  // the diagonal tile
+      const uint64_t c0 = std::max(Ja, I + 1) * GG_PAIR_TILE, c1 = std::min<uint64_t>(Jb * GG_PAIR_TILE, n);
+      if (c1 > c0) acc += ri * (c1 - c0);
     }
-    for (uint64_t J = I; J < nb && t < te; ++J, ++t) {
-      if (t < tb) continue;
-      const uint64_t cj = std::min<uint64_t>(GG_PAIR_TILE, n - J * GG_PAIR_TILE);
-      acc += (I == J) ? ri * (ri - 1) / 2 : ri * cj;
-    }
+    t0 = t1;
   }
   return acc;
 }
@@ -739,9 +740,15 @@ gg_status pairs_gate(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
 // the caller's.
 gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, uint32_t n, uint64_t nb,
                       uint64_t tb, uint64_t te, const uint32_t* d_cmin, const uint32_t* d_sufmin, gg_pair* d_out,
-                      uint64_t cap, uint64_t* d_count, uint64_t work, hipStream_t st, bool* used) {
-  constexpr uint32_t kMaxRun = 4096;
+                      uint64_t cap, uint64_t* d_count, uint64_t work, hipStream_t st, bool* used, bool* costly,
+                      bool weigh_cost) {
+  // (runs in row order -- every build but the row-range one -- read only the
+  // members after each entry; a longer run's start is found by walks that
+  // grow with it, so past this the gate kernel runs instead)
+  constexpr uint32_t kMaxRun = 1u << 16;
+  constexpr uint64_t kBigMapRun = 1536;  // runs longer than the small partner map's fill: the large map
   *used = false;
+  *costly = false;
   const uint64_t total = (uint64_t)n * c->s;
   uint32_t kbits = 1;
   while ((1u << kbits) < c->s) ++kbits;
@@ -754,8 +761,9 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
   b.max_run = kMaxRun;
   GG_HIP(c, scratch_t(c, "idx_offs", std::max(n, 1u), &b.offs));
   // info (2 u64) and flags (4 u32) adjacent: one read-back
-  GG_HIP(c, scratch_t(c, "idx_info", 4, &b.info));
+  GG_HIP(c, scratch_t(c, "idx_info", 4 + index_cost_bytes() / sizeof(uint64_t), &b.info));
   b.flags = reinterpret_cast<uint32_t*>(b.info + 2);
+  b.cost = reinterpret_cast<unsigned long long*>(b.info + 4);
   GG_HIP(c, scratch_t(c, "idx_keys_in", total, &b.keys_in));
   // (+16: the super-bin sort reads keys_out as bytes and vals_in as u32 in
   // aligned groups of 16 entries up to ceil(total / 16) * 16; the split build
@@ -832,6 +840,22 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
     a.max_split_log2 = e && *e ? (uint32_t)std::min(16, std::max(0, atoi(e))) : 16u;
   }
   a.overflow = b.flags + 2;  // (zeroed by index_fill)
+  // The index's cost is its pairs kernel's member reads (the run passes sum
+  // them into b.cost: per entry of a shared hash, the other sketches holding
+  // it); the gate kernel's, the pair count x s.  Clusters of thousands of
+  // near-identical genomes make the first grow as g^2 per hash (C3 with
+  // clusters of 1,000: 2.7e9 reads, index 25 ms against ~3 ms of gate), so
+  // past kIndexCost x s x pairs member reads the pairs kernel emits nothing
+  // and the gate kernel runs instead (GALAHGPU_INDEX_COST=<factor>, 0: never;
+  // never either when the index is asked for by GALAHGPU_PAIRS_KERNEL=index)
+  {
+    const char* e = getenv("GALAHGPU_INDEX_COST");
+    const double k = !weigh_cost ? 0.0 : e && *e ? atof(e) : 0.0;
+    // (a member of a multi-device call weighs its share: the pairs of its tiles)
+    const double lim = k * (double)c->s * (double)pairs_in_tiles(n, tb, te);
+    a.cost = b.cost;
+    a.cost_limit = k > 0 && lim < 1.8e19 ? (unsigned long long)lim : ~0ull;
+  }
   // the output count before the pairs launch: restored if a row overflows
   uint64_t* d_count0;
   GG_HIP(c, scratch_t(c, "idx_count0", 1, &d_count0));
@@ -868,12 +892,16 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
     gg_status ps = launch_pairs(true);
     if (ps != GG_OK) return ps;
     uint64_t* h_if;
-    GG_HIP(c, host_scratch_t(c, "idx_info", 4, &h_if));
-    GG_HIP(c, hipMemcpyAsync(h_if, b.info, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(c, host_scratch_t(c, "idx_info", 5, &h_if));
+    GG_HIP(c, hipMemcpyAsync(h_if, b.info, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(c, hipStreamSynchronize(st));
     memcpy(info, h_if, sizeof info);
     memcpy(flags, h_if + 2, sizeof flags);
     built = paired = flags[3] == 0;
+    if (built && !flags[0] && h_if[4] > a.cost_limit) {  // (the pairs kernel emitted nothing)
+      *costly = true;
+      return GG_OK;
+    }
   } else {
     uint32_t nbuckets = 0;
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, total, st, [&] { return index_fill(b, st); }));
@@ -911,8 +939,29 @@ gg_status pairs_index(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, u
     GG_HIP(c, scratch(c, "idx_sort_tmp", b.sort_tmp_bytes, &b.sort_tmp));
     GG_HIP(c, timed_launch(c, GG_KERNEL_PAIRS_INDEX, 0, st,
                            [&] { return index_build(b, n_entries, sh, end_bit, st); }));
-    GG_HIP(c, hipMemcpyAsync(flags, b.flags, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    uint64_t* h_if;
+    GG_HIP(c, host_scratch_t(c, "idx_info", 6, &h_if));
+    GG_HIP(c, hipMemcpyAsync(h_if, b.info, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(c, hipStreamSynchronize(st));
+    memcpy(flags, h_if + 2, sizeof(uint32_t));
+    if (!flags[0] && h_if[4] > a.cost_limit) {
+      *costly = true;
+      return GG_OK;
+    }
+    // a run longer than the partner map's fill limit (clusters of thousands
+    // of near-identical genomes): rows with that many partners, which the
+    // large map counts in one pass instead of several over their runs (C3
+    // in clusters of 5,000: K2 429 -> 197 ms)
+    a.big_map = h_if[5] > kBigMapRun;
+  } else if (!paired && !flags[0]) {  // (row-range bucketed build: its cost before the pairs kernel)
+    uint64_t cost[2] = {0, 0};
+    GG_HIP(c, hipMemcpyAsync(cost, b.info + 4, sizeof cost, hipMemcpyDeviceToHost, st));
+    GG_HIP(c, hipStreamSynchronize(st));
+    if (cost[0] > a.cost_limit) {
+      *costly = true;
+      return GG_OK;
+    }
+    a.big_map = cost[1] > kBigMapRun;
   }
   if (flags[0]) return GG_OK;  // a run longer than kMaxRun (the pairs kernel, if queued, emitted nothing)
   if (!paired) {
@@ -959,11 +1008,12 @@ gg_status pairs_core(gg_ctx* c, const uint64_t* d_sk, const uint32_t* d_lens, ui
     while ((1u << kbits) < c->s) ++kbits;
     const bool fits = (uint64_t)n * c->s < (1ull << 31) && kbits < 32 && ((uint64_t)n << kbits) <= (1ull << 32);
     if (c->sufmin_host[0] != 0 && fits && n >= 2 && (kern == 4 || n >= 512)) {
-      bool used = false;
+      bool used = false, costly = false;
       gg_status is = pairs_index(c, d_sk, d_lens, n, nb, tb, te, d_cmin, d_sufmin, d_out, cap, d_count, work, st,
-                                 &used);
+                                 &used, &costly, kern == 0);
       if (is != GG_OK) return is;
       ++c->pair_paths[used ? GG_PATH_INDEX : GG_PATH_INDEX_ABANDONED];
+      if (costly) ++c->index_costly;
       if (used) return GG_OK;
     }
     kern = 0;
@@ -1440,12 +1490,6 @@ gg_status gg_info_line(const gg_ctx* ctx, char* buf, size_t cap) {
            (unsigned long long)fb[3], (unsigned long long)fb[5], (unsigned long long)fb[4],
            (unsigned long long)dev_batches);
   std::string out = line;
-  if (ctx->devs.size() > 1) {  // the device-inflated batches of each member
-    out += " [";
-    for (size_t i = 0; i < ctx->devs.size(); ++i)
-      out += (i ? "," : "") + std::to_string(ctx->devs[i]->inflate_dev_batches);
-    out += "]";
-  }
   // device inflate: batches planned again (gzip member boundaries found on
   // the device; full-size token areas after a tight one filled) and the
   // largest scratch one lane used for a batch
@@ -1459,6 +1503,20 @@ gg_status gg_info_line(const gg_ctx* ctx, char* buf, size_t cap) {
     snprintf(line, sizeof line, "; inflate replans: members %llu, full areas %llu; lane scratch %.0f MB",
              (unsigned long long)mplans, (unsigned long long)fplans, scr / 1e6);
     out += line;
+  }
+  // the index calls that went to the gate kernel because their member reads
+  // (large clusters of near-identical genomes) outweighed its merges
+  uint64_t costly = ctx->index_costly;
+  for (const gg_ctx* m : ctx->devs) costly += m->index_costly;
+  if (costly) {
+    snprintf(line, sizeof line, "; index->gate by cost %llu", (unsigned long long)costly);
+    out += line;
+  }
+  if (ctx->devs.size() > 1) {  // (last) the device-inflated batches of each member
+    out += " [";
+    for (size_t i = 0; i < ctx->devs.size(); ++i)
+      out += (i ? "," : "") + std::to_string(ctx->devs[i]->inflate_dev_batches);
+    out += "]";
   }
   const size_t n = std::min(cap - 1, out.size());
   memcpy(buf, out.data(), n);

@@ -140,6 +140,9 @@ struct gg_ctx {
   // first use), so the copies from different peers run at once
   std::vector<hipStream_t> peer_streams;
   uint64_t pair_paths[GG_PATH_COUNT] = {};  // gg_pair_paths
+  // of the index calls abandoned for the gate kernel (GG_PATH_INDEX_ABANDONED),
+  // those whose member reads outweighed the gate kernel's merges (gg_info_line)
+  uint64_t index_costly = 0;
   // gg_fallbacks (the two index entries are read from pair_paths)
   uint64_t fallbacks[GG_FALLBACK_COUNT] = {};
   uint64_t inflate_dev_batches = 0;  // gzip batches inflated on the device (gg_info_line)

@@ -362,6 +362,11 @@ struct IndexBuild {
   void* sort_tmp;
   size_t sort_tmp_bytes;
   uint32_t* flags;     // [4]: overflow
+  // [1] after flags: the member reads the pairs kernel would make, summed
+  // by the run passes (per entry of a run of g >= 2: the members after it
+  // when the run is in row order, else g) -- the index's cost, which
+  // pairs_index weighs against the gate kernel's before the pairs kernel
+  unsigned long long* cost;
   // Row-range index (a device that evaluates only rows [r0, r1) of a
   // multi-device call): bloom != null keeps just the entries whose hash may
   // occur in those rows (a Bloom filter of the rows' hashes: no false
@@ -414,6 +419,11 @@ struct IndexLaunch {
   uint32_t* overflow;       // set when a row's partners overflow the LDS map at the last split
   const uint32_t* build_flags = nullptr;  // the build's flags: [0] or [3] set -> emit nothing
   bool ents16 = false;                     // vals holds 16-bit rows (bucketed build, index_ents16)
+  // the build's member-read count (IndexBuild::cost) and the count past
+  // which the gate kernel is cheaper: with build_flags, more -> emit nothing
+  const unsigned long long* cost = nullptr;
+  unsigned long long cost_limit = ~0ull;
+  bool big_map = false;  // the 2^13-slot partner map (rows that read thousands of members)
 };
 // Row offsets, the entry count and the largest hash (info[0], info[1]);
 // then, with the key shift and the sort's bit range, the keys, the sort and
@@ -427,6 +437,9 @@ hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_
 // index_bucket_bound(entries))
 hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_bound, hipStream_t st);
 uint32_t index_bucket_bound(uint64_t entries);
+// bytes of the build's member-read counters (IndexBuild::cost: the total in
+// word 0, the partial sums after it), cleared by index_fill with the flags
+size_t index_cost_bytes();
 // temporary storage of the full build's sort over bits [0, end_bit), and of
 // the bucketed build's
 size_t index_sort_tmp_bytes(uint64_t total, uint32_t end_bit);

@@ -38,9 +38,8 @@ namespace gg {
 namespace {
 
 constexpr int kRowThreads = 256;
-constexpr uint32_t kMapLog2 = 11;
-constexpr uint32_t kMap = 1u << kMapLog2;  // LDS partner map slots per row
-constexpr uint32_t kMapFull = kMap * 3 / 4;
+// (the pairs kernel's LDS partner map per row: 2^11 slots, 2^13 for heavy
+// indexes; index_pairs_kernel)
 constexpr int kScanThreads = 1024;
 constexpr uint32_t kXcds = 8;  // MI355X: 8 XCDs, each with its own L2
 
@@ -640,6 +639,47 @@ __global__ __launch_bounds__(256) void index_fill_range_kernel(
   }
 }
 
+// The member-read count of a build (IndexBuild::cost) is summed in
+// kCostSlots partial counters 128 B apart (one per workgroup modulo the
+// slots; a single counter, added to by every wave of the run passes, cost
+// C3's K2 1.8 ms of atomics on one address), then into cost[0] by
+// index_cost_sum_kernel before the pairs kernel reads it.
+// The longest run goes the same way (word 1 of each slot, cost[1]): a run
+// longer than the partner map's fill limit means rows with that many
+// partners, which the large map serves in one pass.
+constexpr uint32_t kCostSlots = 64, kCostStride = 16;  // (u64 words: 128 B apart)
+__device__ __forceinline__ void cost_add(unsigned long long* cost, unsigned long long reads, uint32_t g) {
+  for (int o = 32; o > 0; o >>= 1) {
+    reads += __shfl_xor(reads, o);
+    g = max(g, (uint32_t)__shfl_xor(g, o));
+  }
+  if ((threadIdx.x & 63) == 0 && reads) {
+    unsigned long long* slot = &cost[kCostStride * (1 + (blockIdx.x + (threadIdx.x >> 6)) % kCostSlots)];
+    atomicAdd(slot, reads);
+    atomicMax(slot + 1, (unsigned long long)g);
+  }
+}
+__global__ void index_cost_sum_kernel(unsigned long long* cost) {
+  unsigned long long v = cost[kCostStride * (1 + threadIdx.x)], g = cost[kCostStride * (1 + threadIdx.x) + 1];
+  for (int o = 32; o > 0; o >>= 1) {
+    v += __shfl_xor(v, o);
+    g = max(g, (unsigned long long)__shfl_xor(g, o));
+  }
+  if (threadIdx.x == 0) {
+    cost[0] = v;
+    cost[1] = g;
+  }
+}
+
+// runinfo of an entry of a hash other sketches hold too: the members of its
+// run the pairs kernel reads for it, ents[first, first + count) -- when the
+// run is in row order, the members after the entry (count = g - 1 - rank,
+// 0 for the last: nothing to read), otherwise the whole run (count = g; the
+// kernel skips the entry's own row).  0: a hash no other sketch holds.
+__device__ __forceinline__ uint64_t run_reads(uint64_t first, uint32_t count) {
+  return count ? first | ((uint64_t)count << 32) : 0ull;
+}
+
 // Runs of equal keys, one thread per sorted entry p (every lane busy: the
 // run pass was thread-per-run before, with ~4 of 5 lanes idle at the
 // non-starts and its 8-byte runinfo stores issued by one lane per run).
@@ -652,6 +692,12 @@ __global__ __launch_bounds__(256) void index_fill_range_kernel(
 //   runinfo[row, k] = start | g << 32 (g >= 2) or 0 (a hash no other
 //   sketch holds; every evaluated row's entries are written, so runinfo needs
 //   no clearing).
+// When the fill wrote the entries in row-major order (rows_ordered: every
+// build but the row-range one, whose workgroups append), the stable sort
+// keeps each run in row order: the entry's rank p - start goes into runinfo
+// as run_reads' count, and the pairs kernel reads only the members after it.
+// Every entry adds the member reads the pairs kernel will make for it (the
+// members after it in a sorted run, else all g) to *cost.
 // A run of equal keys whose members do not all carry the start's low hash
 // word (two hashes with the same top bits: rare) marks its start in the
 // `mixed` bitset; index_mixed_kernel then sorts it and writes its sub-runs.
@@ -667,9 +713,12 @@ __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restr
                                                          const uint64_t* __restrict__ vals, uint64_t total,
                                                          uint32_t stride, uint32_t kbits, uint32_t max_run,
                                                          uint64_t* __restrict__ runinfo, uint32_t* __restrict__ ents,
-                                                         uint32_t* __restrict__ mixed, uint32_t* __restrict__ overflow) {
+                                                         uint32_t* __restrict__ mixed, uint32_t* __restrict__ overflow,
+                                                         uint32_t rows_ordered, unsigned long long* __restrict__ cost) {
   const uint32_t kmask = (1u << kbits) - 1u;
   const uint32_t lane = threadIdx.x & 63;
+  unsigned long long reads = 0;
+  uint32_t gmax = 0;
   // XCD-aware: the sorted entries are cut into kXcds contiguous chunks and
   // the workgroups of XCD x (blockIdx % kXcds, the dispatcher's round robin)
   // sweep chunk x.  The runinfo stores land on every row wherever the sweep
@@ -726,9 +775,15 @@ __global__ __launch_bounds__(256) void index_runs_kernel(const uint32_t* __restr
       atomicOr(overflow, 1u);
       continue;
     }
-    runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] = g >= 2 ? ((uint64_t)start | ((uint64_t)g << 32)) : 0ull;
+    const uint32_t after = end - (uint32_t)p - 1u;  // the run's members after this entry
+    const uint32_t cnt = g < 2 ? 0u : rows_ordered ? after : g;
+    runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] = run_reads(rows_ordered ? p + 1 : start, cnt);
+    reads += cnt;
+    gmax = max(gmax, g);
     if (lo != lo0) atomicOr(&mixed[start >> 5], 1u << (start & 31));
   }
+  // (every lane of the wave is here: the sweep's bounds are the wave's)
+  cost_add(cost, reads, gmax);
 }
 
 // The runs index_runs_kernel marked mixed (equal top bits, more than one
@@ -783,11 +838,11 @@ __global__ __launch_bounds__(256) void index_mixed_kernel(const uint32_t* __rest
         const uint32_t lo = (uint32_t)(vals[a] >> 32);
         uint64_t b = a + 1;
         while (b < e && (uint32_t)(vals[b] >> 32) == lo) ++b;
-        const uint64_t sub = b - a >= 2 ? (a | ((b - a) << 32)) : 0ull;
+        // (sorted by (low word, entry): each sub-run is in row order)
         for (uint64_t q = a; q < b; ++q) {
           const uint32_t v = (uint32_t)vals[q];
           ents[q] = v;
-          runinfo[(uint64_t)(v >> kbits) * stride + (v & kmask)] = sub;
+          runinfo[(uint64_t)(v >> kbits) * stride + (v & kmask)] = run_reads(q + 1, (uint32_t)(b - q - 1));
         }
         a = b;
       }
@@ -798,12 +853,6 @@ __global__ __launch_bounds__(256) void index_mixed_kernel(const uint32_t* __rest
 // Bucketed build, after the sort by bucket (16-bit keys, entry values):
 // bstart[b] = first sorted entry of bucket b (bstart[nb] = total), written
 // where the bucket changes (one coalesced pass over the keys).
-// runinfo of an entry in a run of g >= 2 equal hashes: the run's first
-// member in ents (bits 0-31), g (bits 32-44), and, when the run's members
-// are in row order (kRunSorted), the entry's own rank in it (bits 45-57)
-constexpr uint32_t kRunGMask = 0x1FFFu;
-constexpr uint32_t kRunRankShift = 45;
-constexpr uint64_t kRunSorted = 1ull << 58;
 constexpr uint32_t kRowSortedRun = 32;  // longer runs of the bucketed build keep their arrival order
 constexpr uint32_t kBucketCap = 3072;    // entries of one bucket grouped in LDS
 constexpr uint32_t kBucketSlots = 4096;  // its LDS hash table (load <= 0.75)
@@ -860,7 +909,7 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
     const uint32_t* __restrict__ sorted, const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ nbuckets_p,
     uint64_t total, const uint64_t* __restrict__ sk, uint32_t stride, uint32_t kbits,
     uint32_t max_run, uint64_t* __restrict__ runinfo, uint32_t* __restrict__ ents, uint32_t ents16,
-    uint32_t* __restrict__ flags) {
+    uint32_t* __restrict__ flags, unsigned long long* __restrict__ cost) {
   __shared__ uint64_t tkey[kBucketSlots];
   __shared__ uint32_t tcnt[kBucketSlots + 1];  // group size; after the scan start << 12 | size
   constexpr uint32_t kBucketPer = kBucketCap / kBucketThreads;
@@ -981,6 +1030,7 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
     if (q < n) grp[(tcnt[slot[r]] >> 12) + rank[r]] = ent[r];
   }
   __syncthreads();
+  uint32_t reads = 0, gmax = 0;  // the pairs kernel's member reads for this thread's entries (index_runs_kernel's *cost)
 #pragma unroll
   for (uint32_t r = 0; r < kBucketPer; ++r) {
     const uint32_t q = tid + r * kBucketThreads;
@@ -989,12 +1039,12 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
       const uint32_t start = t >> 12, g = t & 0xFFFu;
       const uint32_t e = ent[r];
       uint32_t rk = rank[r];
-      uint64_t sorted_flag = 0;
+      bool sorted_run = false;
       if (g >= 2 && g <= kRowSortedRun) {
         const uint32_t row = e >> kbits;
         rk = 0;
         for (uint32_t x = 0; x < g; ++x) rk += (grp[start + x] >> kbits) < row ? 1u : 0u;
-        sorted_flag = kRunSorted;
+        sorted_run = true;
       }
       if (ents16) ((uint16_t*)ents)[lo + start + rk] = (uint16_t)(e >> kbits);
       else ents[lo + start + rk] = e;
@@ -1002,11 +1052,14 @@ __global__ __launch_bounds__(kBucketThreads) void index_bucket_kernel(
         atomicOr(&flags[0], 1u);
         continue;
       }
+      const uint32_t cnt = g < 2 ? 0u : sorted_run ? g - 1u - rk : g;
       runinfo[(uint64_t)(e >> kbits) * stride + (e & kmask)] =
-          g >= 2 ? ((uint64_t)(lo + start) | ((uint64_t)g << 32) | ((uint64_t)rk << kRunRankShift) | sorted_flag)
-                 : 0ull;
+          run_reads((uint64_t)lo + start + (sorted_run ? rk + 1u : 0u), cnt);
+      reads += cnt;
+      gmax = max(gmax, g);
     }
   }
+  cost_add(cost, reads, gmax);
 }
 
 // Allowed column interval [jlo, jhi) of row i inside tiles [tb, te) (tile
@@ -1035,8 +1088,13 @@ __device__ __forceinline__ uint32_t part_of(uint32_t j, uint32_t plog2) {
 // Rows whose partners overflow the LDS map are redone in 2, 4, ... passes,
 // each counting one hash class of partners.
 constexpr uint32_t kMemberLoads = 8;  // run members loaded together per step
-template <bool E16>
+template <bool E16, uint32_t MAPLOG2>
 __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a) {
+  // (MAPLOG2: 11, or 13 for an index whose rows read thousands of run
+  // members each -- clusters of thousands of near-identical genomes: their
+  // partners overflow the 2,048-slot map and every extra pass reads the
+  // row's runs again; 64 KB of LDS, 2 workgroups per CU)
+  constexpr uint32_t kMapLog2 = MAPLOG2, kMap = 1u << kMapLog2, kMapFull = kMap * 3 / 4;
   __shared__ uint32_t mkey[kMap];  // partner + 1 (0 = empty)
   __shared__ uint32_t mcnt[kMap];
   __shared__ uint32_t fill;
@@ -1053,7 +1111,7 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
   if (i >= a.n) return;
   // (launched right after the build, before the host has seen its flags: a
   // run over the limit or a bucket too large left runinfo incomplete)
-  if (a.build_flags && (a.build_flags[0] | a.build_flags[3])) return;
+  if (a.build_flags && ((a.build_flags[0] | a.build_flags[3]) || (a.cost && *a.cost > a.cost_limit))) return;
   uint32_t jlo, jhi;
   row_columns(i, a.n, a.nb, a.tile_begin, a.tile_end, jlo, jhi);
   const uint32_t la = a.lens[i];
@@ -1074,11 +1132,11 @@ __global__ __launch_bounds__(kRowThreads) void index_pairs_kernel(IndexLaunch a)
       if (over) break;
       const uint64_t info = info_next;
       info_next = k + kRowThreads < la ? ri[k + kRowThreads] : 0ull;
-      const uint32_t g = (uint32_t)(info >> 32) & kRunGMask;
-      if (g < 2) continue;
-      // a run in row order: only the members after row i's own (j > i)
-      const uint32_t st = (uint32_t)info, end = st + g;
-      const uint32_t q_first = (info & kRunSorted) ? st + 1u + ((uint32_t)(info >> kRunRankShift) & kRunGMask) : st;
+      // the members to read (run_reads): in a run in row order only those
+      // after row i's own (j > i)
+      const uint32_t cnt = (uint32_t)(info >> 32);
+      if (cnt == 0) continue;
+      const uint32_t q_first = (uint32_t)info, end = q_first + cnt;
       bool stop = false;
       for (uint32_t q0 = q_first; q0 < end && !stop; q0 += kMemberLoads) {
         uint32_t jv[kMemberLoads];
@@ -1157,7 +1215,8 @@ static bool hist_sampling() {
 }
 
 hipError_t index_fill(const IndexBuild& b, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(b.flags, 0, 4 * sizeof(uint32_t), st);
+  // (flags [4] u32 and the cost counters after them: one clear)
+  hipError_t e = hipMemsetAsync(b.flags, 0, 4 * sizeof(uint32_t) + index_cost_bytes(), st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(index_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, b.sketches, b.lens, b.n, b.stride,
                      b.offs, (unsigned long long*)b.info);
@@ -1215,14 +1274,19 @@ hipError_t index_build(const IndexBuild& b, uint64_t total, uint32_t sh, uint32_
                                                                                   (4 * kXcds))) * kXcds);
   // the entries of shared hashes land in keys_in (free after the sort)
   hipLaunchKernelGGL(index_runs_kernel, dim3(blocks), dim3(256), 0, st, b.keys_out, b.vals_out, total, b.stride,
-                     b.kbits, b.max_run, b.runinfo, b.keys_in, b.mixed, b.flags);
+                     b.kbits, b.max_run, b.runinfo, b.keys_in, b.mixed, b.flags, b.bloom ? 0u : 1u, b.cost);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint64_t words = (total + 31) / 32;
   hipLaunchKernelGGL(index_mixed_kernel, dim3((uint32_t)std::min<uint64_t>(4096, (words + 255) / 256)), dim3(256), 0,
                      st, b.keys_out, b.vals_out, total, b.stride, b.kbits, b.mixed, b.runinfo, b.keys_in);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(index_cost_sum_kernel, dim3(1), dim3(kCostSlots), 0, st, b.cost);
   return hipGetLastError();
 }
+
+size_t index_cost_bytes() { return (size_t)(1 + kCostSlots) * kCostStride * sizeof(unsigned long long); }
 
 static hipError_t index_sort_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_bound, hipStream_t st);
 
@@ -1265,11 +1329,15 @@ hipError_t index_build_buckets(const IndexBuild& b, uint64_t total, uint32_t nb_
   const int threads = bt && *bt ? atoi(bt) : 1024;
   auto go = [&](auto kern, int t) {
     hipLaunchKernelGGL(kern, dim3(per_xcd * kXcds), dim3(t), 0, st, vout, b.bstart, nbuckets_d, total, b.sketches,
-                       b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in, index_ents16(b.n) ? 1u : 0u, b.flags);
+                       b.stride, b.kbits, b.max_run, b.runinfo, b.keys_in, index_ents16(b.n) ? 1u : 0u, b.flags,
+                       b.cost);
   };
   if (threads == 256) go(index_bucket_kernel<256>, 256);
   else if (threads == 512) go(index_bucket_kernel<512>, 512);
   else go(index_bucket_kernel<1024>, 1024);
+  hipError_t e2 = hipGetLastError();
+  if (e2 != hipSuccess) return e2;
+  hipLaunchKernelGGL(index_cost_sum_kernel, dim3(1), dim3(kCostSlots), 0, st, b.cost);
   return hipGetLastError();
 }
 
@@ -1334,10 +1402,13 @@ hipError_t launch_index_pairs(const IndexLaunch& a, uint32_t n_rows, hipStream_t
   IndexLaunch b = a;
   b.n_rows = n_rows;
   const dim3 grid((n_rows + kXcds - 1) / kXcds * kXcds);
-  if (a.ents16)
-    hipLaunchKernelGGL(index_pairs_kernel<true>, grid, dim3(kRowThreads), 0, st, b);
-  else
-    hipLaunchKernelGGL(index_pairs_kernel<false>, grid, dim3(kRowThreads), 0, st, b);
+  if (a.ents16) {
+    if (a.big_map) hipLaunchKernelGGL((index_pairs_kernel<true, 13>), grid, dim3(kRowThreads), 0, st, b);
+    else hipLaunchKernelGGL((index_pairs_kernel<true, 11>), grid, dim3(kRowThreads), 0, st, b);
+  } else {
+    if (a.big_map) hipLaunchKernelGGL((index_pairs_kernel<false, 13>), grid, dim3(kRowThreads), 0, st, b);
+    else hipLaunchKernelGGL((index_pairs_kernel<false, 11>), grid, dim3(kRowThreads), 0, st, b);
+  }
   return hipGetLastError();
 }
 

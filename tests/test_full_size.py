@@ -244,3 +244,135 @@ def test_c5_full_size():
         check_config(ctx, d_words, runs, n, s, ga.parse_percentage(95), lens_bp, spot)
     del d_words
     torch.cuda.empty_cache()
+
+
+def test_sampled_histogram_missing_a_heavy_bin():
+    """Past 2^26 entries the coarse histogram samples one 128-B line (16
+    entries) in 8 of every row (row i: lines i % 8, i % 8 + 8, ...;
+    pairs_index.hip bucket_hist_kernel).  Here 70,000 rows of 1,000 hashes
+    (7.0e7 entries) put 96 hashes each into one coarse bin (top 12 bits
+    0x800) at row positions the sample never reads -- 6.7M entries the
+    histogram does not see, so that bin gets one bucket of millions of
+    entries.  The build must notice (bucket over kBucketCap: the full-sort
+    rebuild, counted in index_full_sort) and the result must be exact: rows
+    2t and 2t + 1 share 990 hashes (every other pair shares none), so the
+    passing pairs are exactly those 35,000, each with the oracle's (common,
+    total).  Round 5's C5 failure (a missed bin's entries sent to bucket
+    `nbuckets`) is this failure class; this pins it without relying on C5's
+    natural hash distribution."""
+    rng = np.random.default_rng(61)
+    n, s, shared, heavy = 70000, 1000, 990, 96
+    B = np.uint64(0x800 << 52)
+    lo_span, hi_start = int(B), int(B) + (1 << 52)  # bin 0x800 is [B, B + 2^52)
+    sk = np.empty((n, s), np.uint64)
+    for t in range(n // 2):
+        e = (2 * t) & 7
+        c = 16 * (e + 2) + 256  # hashes below the bin: the bin's run starts in line e + 2 (mod 8) for rows 2t and 2t+1
+        below = rng.integers(1, lo_span, c, dtype=np.uint64)
+        binv = B + rng.integers(0, 1 << 52, heavy, dtype=np.uint64)
+        above = rng.integers(hi_start, (1 << 64) - 1, s - c - heavy + 10, dtype=np.uint64)
+        common = np.concatenate([below, binv, above[:s - c - heavy - 10]])
+        for r, extra in ((2 * t, above[-20:-10]), (2 * t + 1, above[-10:])):
+            sk[r] = np.sort(np.concatenate([common, extra]))
+    assert all(len(np.unique(sk[i])) == s for i in (0, 1, 12345, n - 1))  # (distinct with near certainty; checked on a few)
+    # the construction: no sampled line of any row holds a bin-0x800 hash
+    bins = (sk >> np.uint64(52)).astype(np.uint32)
+    line = np.arange(s) // 16
+    rows = np.arange(n)
+    sampled = (line[None, :] % 8) == (rows[:, None] % 8)
+    assert not (sampled & (bins == 0x800)).any() and (bins == 0x800).sum() == heavy * n
+    lens = np.full(n, s, np.uint32)
+    thr = ga.parse_percentage(95)
+    with ga.Context(k=21, sketch_size=s) as ctx:
+        p = ctx.pairs(sk, lens, thr)
+        paths = ctx.pair_paths()
+    assert paths["index"] >= 1 and paths["index_full_sort"] >= 1 and paths["index_abandoned"] == 0, paths
+    got = [(int(r["i"]), int(r["j"])) for r in p]
+    assert got == [(2 * t, 2 * t + 1) for t in range(n // 2)]
+    for r in p[::97]:  # (the oracle's merge on a spread of them)
+        i, j = int(r["i"]), int(r["j"])
+        assert (int(r["common"]), int(r["total"])) == oracle.raw_distance(sk[i], sk[j])
+
+
+@pytest.mark.parametrize("cluster,s,max_sub,pct", [(1000, 1000, MAX_SUB, 95), (5000, 1000, MAX_SUB, 95),
+                                                   (1000, 10000, MAX_SUB, 95), (10000, 1000, 0.01, 99.9)])
+def test_large_clusters(cluster, s, max_sub, pct):
+    """Dereplicating many strains of one species: 10k x 3 Mbp genomes in
+    clusters of 1,000 and 5,000 (s = 1000), of 1,000 at s = 10000, and one
+    cluster of 10,000 near-identical genomes (substitution rate <= 1%, so a
+    hash is held by up to ~9,000 sketches: runs past a bucket and past the
+    old 4,096 / 8,191 run limits, at 99.9% so that few pairs pass).  Runs of
+    hundreds to thousands of members overflow the bucketed build's buckets:
+    the full-sort build keeps each run in row order and each member reads
+    only the members after it; rows with thousands of partners take the
+    large partner map.  The index runs to completion (no
+    abandon), its pairs equal the gate kernel's over every pair, and
+    (common, total) and the pass decision equal the oracle's on 6,000
+    sampled within-cluster pairs and 2,000 across clusters."""
+    torch = torch_dev()
+    n, glen = 10000, 3000000
+    thr = ga.parse_percentage(pct)
+    with ga.Context(k=21, sketch_size=s) as ctx:
+        d_words = torch.empty(n * glen // 16, dtype=torch.int32, device="cuda")
+        runs = ctx.synth_device(n, glen, cluster, max_sub, 11, d_words)
+        d_sk = torch.zeros((n, s), dtype=torch.int64, device="cuda")
+        d_len = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ctx.sketch_device(d_words, runs, n, d_sk, d_len)
+        torch.cuda.synchronize()
+        del d_words
+        sk = d_sk.cpu().numpy().view(np.uint64)
+        ln = d_len.cpu().numpy().view(np.uint32)
+        assert (ln == s).all()
+
+        def all_pairs(c):
+            cap = 1 << 24
+            d_out = torch.empty(cap * 4, dtype=torch.int32, device="cuda")
+            d_cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+            c.pairs_device(d_sk, d_len, n, 0, ga.pair_tiles(n), thr, d_out, cap, d_cnt)
+            torch.cuda.synchronize()
+            k = int(d_cnt.item())
+            assert k <= cap
+            p = d_out[:k * 4].cpu().numpy().view(np.uint32).reshape(-1, 4)
+            return p[np.lexsort((p[:, 1], p[:, 0]))]
+
+        P = all_pairs(ctx)
+        paths = ctx.pair_paths()
+        assert paths["index"] == 1 and paths["index_abandoned"] == 0 and paths["gate"] == 0, paths
+    old = os.environ.get("GALAHGPU_PAIRS_KERNEL")
+    os.environ["GALAHGPU_PAIRS_KERNEL"] = "gate"
+    try:
+        with ga.Context(k=21, sketch_size=s) as gctx:
+            PG = all_pairs(gctx)
+            assert gctx.pair_paths()["gate"] == 1
+    finally:
+        if old is None:
+            os.environ.pop("GALAHGPU_PAIRS_KERNEL")
+        else:
+            os.environ["GALAHGPU_PAIRS_KERNEL"] = old
+    assert np.array_equal(P, PG)
+    got = {(int(a), int(b)): (int(c), int(t)) for a, b, c, t in P}
+    rng = np.random.default_rng(cluster + s)
+    cl = rng.integers(0, n // cluster, 6000)
+    a = rng.integers(0, cluster, 6000)
+    b = rng.integers(0, cluster, 6000)
+    keep = a != b
+    ii = (cl * cluster + np.minimum(a, b))[keep].astype(np.uint32)
+    jj = (cl * cluster + np.maximum(a, b))[keep].astype(np.uint32)
+    if n // cluster > 1:
+        ri = rng.integers(0, n, 4000).astype(np.uint32)
+        rj = rng.integers(0, n, 4000).astype(np.uint32)
+        x = (ri // cluster) != (rj // cluster)
+        ii = np.concatenate([ii, np.minimum(ri, rj)[x][:2000]])
+        jj = np.concatenate([jj, np.maximum(ri, rj)[x][:2000]])
+    oc, ot = oracle.pair_list(sk, ln.astype(np.int32), ii, jj)
+    opass = oracle.ani_array(oc, ot) >= np.float64(np.float32(thr))
+    for q in range(len(ii)):
+        key = (int(ii[q]), int(jj[q]))
+        if opass[q]:
+            assert got.get(key) == (int(oc[q]), int(ot[q])), key
+        else:
+            assert key not in got, key
+    assert len(P) > 0 and not opass.all()
+    print("\nclusters of %d, s=%d: %d passing pairs; index (full sort, row-ordered runs) == gate" % (cluster, s, len(P)))
+    del d_sk, d_len
+    torch.cuda.empty_cache()

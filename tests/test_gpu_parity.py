@@ -564,7 +564,10 @@ def test_index_kernel_many_partners_and_long_runs(monkeypatch):
                     assert ctx.fallbacks()["index_to_gate"] == 1
                     assert "index->gate 1," in ctx.info_line()
         monkeypatch.delenv("GALAHGPU_INDEX_MAX_SPLIT")
-    # 5,000 sketches that all hold one hash: a run of 5,000 > the run limit
+    # 5,000 sketches that all hold one hash: a run of 5,000 (over one bucket
+    # of the bucketed build and over the old 4,096 run limit): the full-sort
+    # build keeps the run in row order, each member reads the members after
+    # it, and rows with thousands of partners take the large partner map
     n = 5000
     s = 40
     shared = np.uint64(12345)
@@ -580,9 +583,10 @@ def test_index_kernel_many_partners_and_long_runs(monkeypatch):
     monkeypatch.setenv("GALAHGPU_PAIRS_KERNEL", "index")
     with ga.Context(k=21, sketch_size=s) as ctx:
         assert as_tuples(ctx.pairs(sk, lens, np.float32(0.01))) == exp
-        # (one attempt per output-buffer pass: every one abandoned for the gate kernel)
+        # (one index call per output-buffer pass, none abandoned)
         paths = ctx.pair_paths()
-        assert paths["index"] == 0 and paths["index_abandoned"] >= 1 and paths["gate"] == paths["index_abandoned"]
+        assert paths["index"] >= 1 and paths["index_abandoned"] == 0 and paths["gate"] == 0, paths
+        assert paths["index_full_sort"] == paths["index"]
 
 
 def _part_of(j, plog2):

@@ -404,3 +404,35 @@ def test_device_inflate_is_the_default_and_knobs_change_nothing(golden, monkeypa
             monkeypatch.delenv(k)
         assert fb["inflate_host"] == 0
         assert (lens == l0).all() and all((sk[g][:lens[g]] == sk0[g][:l0[g]]).all() for g in range(len(lens)))
+
+
+@pytest.mark.gpu
+def test_lowest_failing_file_reported_when_its_batch_is_dropped(tmp_path, monkeypatch):
+    """a corrupt .gz (index 2) and an unreadable path (index 4)
+    claimed into one batch: the unreadable file stops the batch before any
+    decode, so the corrupt one was never decoded there.  The call must still
+    report the corrupt file -- the lowest failing index, as a serial reader
+    (and the host path) meets it -- not the unreadable one."""
+    rng = np.random.default_rng(51)
+    paths = []
+    for i in range(6):
+        p = tmp_path / ("f%d.fna.gz" % i)
+        data = gzip.compress(fasta_text(rng, 200000, b"f%d" % i), 6)
+        if i == 2:
+            bad = bytearray(data)
+            bad[len(bad) // 2] ^= 0x55
+            data = bytes(bad)
+        if i != 4:
+            p.write_bytes(data)
+        paths.append(str(p))
+    monkeypatch.setenv("GALAHGPU_GZ_COPY_THREADS", "1")
+    monkeypatch.setenv("GALAHGPU_GZ_LANES", "1")
+    errs = {}
+    for mode in ("host", "device"):
+        monkeypatch.setenv("GALAHGPU_INFLATE", mode)
+        with ga.Context(k=21, sketch_size=1000) as ctx:
+            with pytest.raises(ga.GalahGpuError) as e:
+                ctx.sketch_files(paths)
+            errs[mode] = (e.value.status, str(e.value))
+    assert errs["device"] == errs["host"]
+    assert "f2.fna.gz" in errs["device"][1] and "f4.fna.gz" not in errs["device"][1], errs
