@@ -44,6 +44,15 @@ hipError_t scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
     // boundary) would otherwise reallocate it call after call, and hipFree
     // waits for every stream of the device
     const size_t grown = e.second ? e.second + e.second / 4 : 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Tally {  // (the regrowth's wall time, gg_info_line: a hipFree waits for the device)
+      gg_ctx* c;
+      std::chrono::steady_clock::time_point t0;
+      ~Tally() {
+        ++c->scratch_regrows;
+        c->scratch_regrow_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      }
+    } tally{c, t0};
     if (e.first) {
       hipError_t err = hipFree(e.first);
       if (err != hipSuccess) return err;
@@ -70,6 +79,14 @@ hipError_t scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
 hipError_t host_scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
   auto& e = c->host_scratch[key];
   if (e.second < bytes) {
+    struct Tally {
+      gg_ctx* c;
+      std::chrono::steady_clock::time_point t0;
+      ~Tally() {
+        ++c->scratch_regrows;
+        c->scratch_regrow_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      }
+    } tally{c, std::chrono::steady_clock::now()};
     if (e.first) {
       hipError_t err = hipHostFree(e.first);
       if (err != hipSuccess) return err;
@@ -1512,6 +1529,26 @@ gg_status gg_info_line(const gg_ctx* ctx, char* buf, size_t cap) {
     snprintf(line, sizeof line, "; index->gate by cost %llu", (unsigned long long)costly);
     out += line;
   }
+  // device / pinned scratch buffers grown since the context was created
+  // (and the wall time that took: hipFree waits for the device), its lanes'
+  // included -- a call that grows one runs long
+  uint64_t regrows = ctx->scratch_regrows;
+  double regrow_ms = ctx->scratch_regrow_ms;
+  auto add_lanes = [&](const gg_ctx* m) {
+    for (const gg_ctx* l : m->lanes)
+      if (l) {
+        regrows += l->scratch_regrows;
+        regrow_ms += l->scratch_regrow_ms;
+      }
+  };
+  add_lanes(ctx);
+  for (const gg_ctx* m : ctx->devs) {
+    regrows += m->scratch_regrows;
+    regrow_ms += m->scratch_regrow_ms;
+    add_lanes(m);
+  }
+  snprintf(line, sizeof line, "; scratch regrows %llu (%.1f ms)", (unsigned long long)regrows, regrow_ms);
+  out += line;
   if (ctx->devs.size() > 1) {  // (last) the device-inflated batches of each member
     out += " [";
     for (size_t i = 0; i < ctx->devs.size(); ++i)

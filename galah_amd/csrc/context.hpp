@@ -153,6 +153,9 @@ struct gg_ctx {
   // the largest inflate scratch of a batch on this lane (tokens, sub-span
   // areas, val, text), bytes: the per-lane footprint the info line reports
   uint64_t gz_scratch_bytes = 0;
+  // scratch / host-scratch buffers regrown (and the wall ms it took), gg_info_line
+  uint64_t scratch_regrows = 0;
+  double scratch_regrow_ms = 0;
   // multi-device context: [a * M + b] = 1 when member a reaches member b's
   // memory directly (same device, or peer access enabled), gg_peer_links
   std::vector<uint8_t> peer_direct;

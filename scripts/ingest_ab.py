@@ -61,7 +61,13 @@ try:
 
     with cf.ThreadPoolExecutor(16) as ex:
         paths = list(ex.map(write, range(n)))
-    res = {name: {"wall": [], "lane1_wall": [], "ms": {}} for name, _ in settings}
+    import re
+
+    def regrows(ctx):
+        m = re.search(r"scratch regrows (\d+) \(([0-9.]+) ms\)", ctx.info_line())
+        return (int(m.group(1)), float(m.group(2))) if m else (0, 0.0)
+
+    res = {name: {"wall": [], "lane1_wall": [], "ms": {}, "regrow": []} for name, _ in settings}
     with ga.Context(k=21, sketch_size=1000, seed=0, host_threads=16) as ctx:
         for name, env in settings:  # (warm-up: buffers sized for each setting)
             os.environ.update(env)
@@ -71,9 +77,12 @@ try:
         for c in range(calls):
             for name, env in settings:
                 os.environ.update(env)
+                r0 = regrows(ctx)
                 t1 = time.perf_counter()
                 ctx.precluster_files(paths, 0.95)
                 res[name]["wall"].append(time.perf_counter() - t1)
+                r1 = regrows(ctx)
+                res[name]["regrow"].append([r1[0] - r0[0], round(r1[1] - r0[1], 2)])
                 os.environ["GALAHGPU_GZ_LANES"] = "1"
                 ctx.timing_enable(True)
                 t1 = time.perf_counter()
@@ -91,6 +100,7 @@ try:
         print(json.dumps({"setting": name, "files": n, "format": fmt, "calls": calls,
                           "wall_median_s": round(float(np.median(r["wall"])), 4),
                           "wall_s": [round(x, 4) for x in r["wall"]],
+                          "regrows_per_call": r["regrow"],
                           "gbases_per_s": round(n * glen / float(np.median(r["wall"])) / 1e9, 2),
                           "lane1_wall_median_s": round(float(np.median(r["lane1_wall"])), 4),
                           "kernel_ms_median": {k: round(float(np.median(v)), 3) for k, v in r["ms"].items()}}),
