@@ -59,7 +59,7 @@ hipError_t scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
       e.first = nullptr;
       e.second = 0;
     }
-    size_t want = std::max<size_t>(std::max(bytes, grown), 256);
+    size_t want = std::max<size_t>(std::max(std::max(bytes, grown), (size_t)((double)bytes * c->scratch_hint)), 256);
     hipError_t err = hipMalloc(&e.first, want);
     if (err == hipErrorOutOfMemory && want > bytes) {  // (no room for the headroom: just what is asked)
       (void)hipGetLastError();

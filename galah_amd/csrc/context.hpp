@@ -156,6 +156,11 @@ struct gg_ctx {
   // scratch / host-scratch buffers regrown (and the wall ms it took), gg_info_line
   uint64_t scratch_regrows = 0;
   double scratch_regrow_ms = 0;
+  // a device scratch buffer that grows is allocated for this many times the
+  // size asked (an ingest batch smaller than the largest the call may stage:
+  // its buffers sized for that one at once, so that no later batch regrows
+  // them -- a regrowth's hipFree waits for the whole device)
+  double scratch_hint = 1.0;
   // multi-device context: [a * M + b] = 1 when member a reaches member b's
   // memory directly (same device, or peer access enabled), gg_peer_links
   std::vector<uint8_t> peer_direct;

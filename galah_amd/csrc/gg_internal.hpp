@@ -285,16 +285,19 @@ struct InflatePlace {
   const uint64_t* n_tok;
   const uint32_t* lane_file;
   const uint64_t* lane_out;    // [n_lanes] text position of the lane's first byte
-  const uint64_t* lane_pad;    // [n_lanes] its file's last lane: end of the '\n' padding after it (else 0)
   const uint64_t* lane_len;    // [n_lanes] the bytes the decode counted for it (its tokens must make as many)
-  const uint64_t* file_text;   // [n_files] text position of the file's first byte
-  uint32_t n_lanes;
-  uint8_t* text;               // [text_len] the bytes, kTextPtr where the byte is still a pointer
-  uint32_t* val;               // [text_len] literal (0x80000000 | byte) or the position copied
-  uint32_t* flags;             // bit 0: a distance before its file's start, bit 1: a runaway chain or a
-                               // pointer out of range, bit 2: a lane's tokens make other than lane_len bytes
+  const uint64_t* file_text;   // [n_units] text position of the unit's first byte
+  const uint64_t* unit_len;    // [n_units] its bytes
+  const uint64_t* unit_pad;    // [n_units] a file's last unit: end of the '\n' padding after it (else 0)
+  const uint32_t* unit_lane;   // [n_units + 1] the unit's lanes: unit_lane[u] .. unit_lane[u + 1] - 1
+  uint32_t n_lanes, n_units;
+  uint8_t* text;               // [text_len] the bytes (written by the resolve)
+  uint16_t* sym;               // [text_len] a literal byte (< 0x100), or kSymPtr | (position copied & 0x7FFF):
+                               // a byte of the 32 KB before the lane's first byte
+  uint32_t* flags;             // bit 0: a distance before its file's start,
+                               // bit 2: a lane's tokens make other than lane_len bytes
 };
-constexpr uint8_t kTextPtr = 0xFF;  // (a literal 0xFF byte is also read through val: still exact)
+constexpr uint16_t kSymPtr = 0x8000u;
 // one file of an inflate batch (inflate_host.cpp): its bytes at
 // [data_off, data_off + data_len) of the batch (data_off 4-byte aligned):
 // the deflate data of a gzip member with its trailer's isize and crc, or
@@ -333,10 +336,11 @@ hipError_t launch_inflate_search(const InflateSearch& a, hipStream_t st);
 // kernel on st (inflate.hip); both buffers hold a multiple of 16 bytes
 hipError_t launch_slot_upload(uint8_t* dst, const uint8_t* src_mapped, uint64_t bytes, hipStream_t st);
 hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st);
-// the text of a batch: expand (every lane's tokens into text + val), then
-// resolve (text[0, text_len); val is read only where the expand wrote it)
+// the text of a batch: expand (every lane's tokens into sym), then resolve
+// (each unit's lanes in order into text, the padding after a file's last
+// unit; sym is read only in the units' ranges, where the expand wrote it)
 hipError_t launch_inflate_expand(const InflatePlace& a, hipStream_t st);
-hipError_t launch_inflate_resolve(const InflatePlace& a, uint64_t text_len, hipStream_t st);
+hipError_t launch_inflate_resolve(const InflatePlace& a, hipStream_t st);
 // CRC-32 per file (file f's 4 KB segments are seg_first[f] .. seg_first[f +
 // 1] - 1; crc receives n_files CRCs, then each file's first byte)
 constexpr uint32_t kInflateCrcSeg = 4096;

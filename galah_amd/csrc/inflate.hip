@@ -18,9 +18,11 @@
 //   inflate_expand_kernel   one workgroup per segment, in order: token output
 //                           offsets by a block scan, the bytes of each step
 //                           built in LDS (back-references inside the segment
-//                           copied, those before it left as pointers)
-//   inflate_resolve_kernel  pointers (into earlier segments only) followed to
-//                           their literals, 16 bytes per thread
+//                           copied, those before it left as pointers into
+//                           the 32 KB before the segment): u16 per byte
+//   inflate_resolve_kernel  one workgroup per gzip member, its segments in
+//                           order: the member's last 32 KB of text in an LDS
+//                           ring, so every pointer is one LDS read
 //   inflate_crc_seg_kernel  CRC-32 of every 4 KB of text, one thread each
 //   inflate_crc_fold_kernel per file its segments' CRCs folded with x^(8n)
 //                           mod P; checked with ISIZE against the gzip
@@ -49,6 +51,46 @@ constexpr uint32_t kSearchStep = 4096;  // positions per step: 64 consecutive pe
 constexpr uint32_t kSearchCands = 256;  // candidates listed at most (more: the scan resumes after the last listed)
 constexpr uint32_t kCheckAt = 48;       // candidates that trigger a round of full checks (~1 per 1,100 positions)
 constexpr uint32_t kWinWords = kSearchStep / 32 + 8;  // a step's bits plus the 160 after its first lane's last
+#ifndef GG_CHK_LDS  // (A/B builds: -DGG_CHK_LDS=1, a round's stream copied to LDS first: search 7.7 -> 8.8-9.0 ms per 600 C2-like files)
+#define GG_CHK_LDS 0
+#endif
+constexpr uint32_t kChkWords = GG_CHK_LDS ? 2048 : 1;  // the stream from a check round's first candidate on, in LDS (~48 candidates span ~1,700)
+
+// The stream as a lane's full check reads it: words [wb, wb + nw) from the
+// LDS copy (one coalesced copy per round), the rest (a walk that runs past
+// it) from global memory, through a register window of three words that a
+// walk moving on by a word shifts, loading the word after it -- which it
+// needs a few symbols later -- so a code-length symbol waits on no stream
+// read (a round of checks is one walk of a real header, ~300 dependent
+// symbols long).
+struct WinBits {
+  const uint32_t* lds;
+  const uint32_t* g;
+  uint64_t wb;
+  uint32_t nw;
+  mutable uint64_t wi = ~0ull;  // the window's first word
+  mutable uint32_t a = 0, b = 0, c = 0;
+  __device__ uint32_t word(uint64_t w) const {
+    const uint64_t i = w - wb;  // (w < wb wraps to the global read)
+    return i < nw ? lds[i] : g[w];
+  }
+  __device__ uint32_t peek(uint64_t pos) const {
+    const uint64_t w = pos >> 5;
+    if (w != wi) {
+      if (w == wi + 1) {
+        a = b;
+        b = c;
+        c = word(w + 2);
+      } else {
+        a = word(w);
+        b = word(w + 1);
+        c = word(w + 2);
+      }
+      wi = w;
+    }
+    return __builtin_amdgcn_alignbit(b, a, (uint32_t)pos & 31u);
+  }
+};
 
 // block_header_quick (inflate_core.hpp) for the 64 positions of a lane at
 // once.  A[0..4]: the 160 stream bits from the lane's first position.  The
@@ -93,6 +135,7 @@ __device__ __forceinline__ uint64_t quick64(const uint32_t (&A)[5], const uint8_
 __global__ __launch_bounds__(64 * kSearchWaves, 4) void inflate_search_kernel(InflateSearch a) {
   __shared__ uint64_t cand[kSearchWaves][kSearchCands];
   __shared__ uint32_t win[kSearchWaves][kWinWords];
+  __shared__ uint32_t chk[kSearchWaves][kChkWords];
   __shared__ ClLds cls[kSearchWaves][64];
   __shared__ uint8_t kraft3[512];  // sum over 3 code-length fields of 128 >> len (0 for len 0)
   for (uint32_t i = threadIdx.x; i < 512; i += 64 * kSearchWaves) {
@@ -118,7 +161,6 @@ __global__ __launch_bounds__(64 * kSearchWaves, 4) void inflate_search_kernel(In
   // words a position before b1 can touch in the filter (its 128 bits; the
   // file's trailer or the batch's padding follows its deflate data)
   const uint64_t wend = (a.file_bits[f] + 31) / 32 + 5;
-  const Bits in{stream};
   uint64_t found = ~0ull;
   uint32_t nc = 0;  // candidates listed, not yet checked (uniform)
   uint64_t tp = a.prof ? clock64() : 0;
@@ -179,6 +221,13 @@ __global__ __launch_bounds__(64 * kSearchWaves, 4) void inflate_search_kernel(In
     }
     // the full checks of the listed candidates, in order
     if (a.prof && lane == 0) atomicAdd((unsigned long long*)&a.prof[4], (unsigned long long)nc);
+    WinBits wbits{chk[wv], stream, 0, 0};
+    if (GG_CHK_LDS && nc) {  // the stream from the first candidate on into LDS (the words the filter may read: up to wend)
+      wbits.wb = cw[0] >> 5;
+      wbits.nw = wend > wbits.wb ? (uint32_t)min<uint64_t>(kChkWords, wend - wbits.wb) : 0u;
+      for (uint32_t i = lane; i < wbits.nw; i += 64) chk[wv][i] = stream[wbits.wb + i];
+      __builtin_amdgcn_wave_barrier();
+    }
     // (each lane walks one candidate a symbol per step and takes the next
     // unclaimed one when its own is decided; done when a candidate passed
     // and none before it is still walking, or all are decided)
@@ -193,11 +242,11 @@ __global__ __launch_bounds__(64 * kSearchWaves, 4) void inflate_search_kernel(In
         const uint32_t lim = min(nc, best);
         if (need) {
           const uint32_t k = next + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull));
-          if (k < lim) mine = hw.start(in, cw[k], cl) ? (int)k : -1;  // (rejected at once: the lane claims again)
+          if (k < lim) mine = hw.start(wbits, cw[k], cl) ? (int)k : -1;  // (rejected at once: the lane claims again)
         }
         next = min(lim, next + (uint32_t)__popcll(nm));
         int r = 0;
-        if (mine >= 0) r = hw.step(in, cl);
+        if (mine >= 0) r = hw.step(wbits, cl);
         const uint64_t pm = __ballot(r == 1);
         if (pm) {
           uint32_t b = r == 1 ? (uint32_t)mine : ~0u;
@@ -244,29 +293,23 @@ struct LdsStore {
 
 constexpr uint32_t kSpanLanes = 64;  // one wave per segment, one sub-span per lane
 
-// A lane's tokens to its scratch area: the last 4 held for one 16-byte store
-// (the area is 16-byte aligned).
+// A lane's tokens to its scratch area, interleaved with the wave's other
+// lanes (token k of lane j at p[64 k], p = the area + j): the wave's k-th
+// tokens share cache lines, so a store instruction writes a few whole lines
+// instead of a 16-byte piece of 64 lines, which the L2 evicted half written
+// (round 5: the decode moved 6.1x its bytes), and the copy-out's loads are
+// coalesced the same way.
 struct TokSink {
   uint32_t* p;
   uint32_t cap;
   uint32_t k = 0;
-  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0;
   __device__ bool operator()(uint32_t tk) {
     if (k >= cap) return false;
-    w0 = w1;
-    w1 = w2;
-    w2 = w3;
-    w3 = tk;
+    p[(size_t)k * kSpanLanes] = tk;
     ++k;
-    if ((k & 3u) == 0) *(uint4*)(p + k - 4) = make_uint4(w0, w1, w2, w3);
     return true;
   }
-  __device__ void flush() {
-    const uint32_t r = k & 3u;
-    if (r >= 1) p[k - 1] = w3;
-    if (r >= 2) p[k - 2] = w2;
-    if (r >= 3) p[k - 3] = w1;
-  }
+  __device__ void flush() {}
 };
 
 // A block's header read by the whole wave.  Lane 0 parses the fields and
@@ -531,9 +574,10 @@ __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_
   return st;
 }
 
-// n tokens from a lane's scratch to the segment's tokens, kCopyBatch loads
-// in flight (a plain loop waited on each load in turn; with 8 in flight a
-// window's ~85 tokens per lane still took ~11 waits: 16% of the decode)
+// n tokens from a lane's scratch (stride kSpanLanes: TokSink) to the
+// segment's tokens, kCopyBatch loads in flight (a plain loop waited on each
+// load in turn; with 8 in flight a window's ~85 tokens per lane still took
+// ~11 waits: 16% of the decode)
 #ifndef GG_COPY_BATCH  // (A/B builds: -DGG_COPY_BATCH=8)
 #define GG_COPY_BATCH 32
 #endif
@@ -543,7 +587,7 @@ __device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restri
   for (; i + kCopyBatch <= n; i += kCopyBatch) {
     uint32_t v[kCopyBatch];
 #pragma unroll
-    for (uint32_t k = 0; k < kCopyBatch; ++k) v[k] = src[i + k];
+    for (uint32_t k = 0; k < kCopyBatch; ++k) v[k] = src[(size_t)(i + k) * kSpanLanes];
 #pragma unroll
     for (uint32_t k = 0; k < kCopyBatch; ++k) dst[i + k] = v[k];
   }
@@ -551,7 +595,7 @@ __device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restri
   uint32_t v[kCopyBatch];
 #pragma unroll
   for (uint32_t k = 0; k < kCopyBatch; ++k)
-    if (i + k < n) v[k] = src[i + k];
+    if (i + k < n) v[k] = src[(size_t)(i + k) * kSpanLanes];
 #pragma unroll
   for (uint32_t k = 0; k < kCopyBatch; ++k)
     if (i + k < n) dst[i + k] = v[k];
@@ -695,9 +739,11 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       const uint64_t S = bstart + j * L;
       const uint64_t R = j + 1 == nsub ? wend : S + L;
       const uint64_t capL = span_cap(L, a.tight), ncks = span_cks(L);
-      uint32_t* A = scr_all + j * span_words(L, a.tight);  // first decode
-      uint32_t* B = A + capL;                     // second decode
-      uint64_t* ck = (uint64_t*)(B + capL);       // the first decode's checkpoints
+      // the wave's areas, each lane's entries interleaved (stride kSpanLanes)
+      uint32_t* A = scr_all + j;                                   // first decode
+      uint32_t* B = scr_all + kSpanLanes * capL + j;               // second decode
+      uint64_t* ck = (uint64_t*)(scr_all + 2 * kSpanLanes * capL) + j;  // the first decode's checkpoints
+#define CK(k) ck[(size_t)(k) * kSpanLanes]
       // the first decode, from S
       uint32_t na = 0, nck = 0, sa = kSpanRange;
       uint64_t ba = 0, Ea = S;
@@ -705,7 +751,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
         TokSink sink{A, (uint32_t)capL};
         auto ck1 = [&](uint32_t k, uint64_t c) {
           if (k < ncks) {
-            ck[k] = c;
+            CK(k) = c;
             nck = k + 1;
           }
           return true;
@@ -721,7 +767,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
         sink.flush();
       }
       phase(1);
-      uint64_t first = act && nck ? S + ck_off(ck[0]) : ~0ull;
+      uint64_t first = act && nck ? S + ck_off(CK(0)) : ~0ull;
       bool redone = false;
       int synced = -1;
       uint32_t nb = 0, sb = kSpanRange;
@@ -760,7 +806,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
           first = eprev;
           TokSink sink{B, (uint32_t)capL};
           auto ck2 = [&](uint32_t k, uint64_t cc) {
-            if (k < nck && ck_off(cc) == ck_off(ck[k])) {
+            if (k < nck && ck_off(cc) == ck_off(CK(k))) {
               synced = (int)k;
               return false;
             }
@@ -798,8 +844,8 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       uint64_t vbytes = 0;
       if (j <= c_end) {
         if (!redone) {
-          const uint64_t c0 = ck[0];
-          p1 = A + ck_tok(c0);
+          const uint64_t c0 = CK(0);
+          p1 = A + (size_t)ck_tok(c0) * kSpanLanes;
           n1 = na - ck_tok(c0);
           vbytes = ba - ck_bytes(c0);
         } else {
@@ -807,8 +853,8 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
           n1 = nb;
           vbytes = bb;
           if (synced >= 0) {
-            const uint64_t ck_s = ck[synced];
-            p2 = A + ck_tok(ck_s);
+            const uint64_t ck_s = CK(synced);
+            p2 = A + (size_t)ck_tok(ck_s) * kSpanLanes;
             n2 = na - ck_tok(ck_s);
             vbytes += ba - ck_bytes(ck_s);
           }
@@ -832,6 +878,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       uint32_t* dst = out + n_out + (incl - valid);
       copy_tokens(dst, p1, n1);
       copy_tokens(dst + n1, p2, n2);
+#undef CK
       phase(3);
       if (a.prof && j == 0) {
         atomicAdd((unsigned long long*)&a.prof[4], 1ull);
@@ -871,9 +918,14 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
 // staged as literals, pointers to before the segment (the segment before is
 // not expanded yet: the resolve pass follows them), ring values, or kIntra |
 // the step byte they copy; kIntra pointers are followed inside the step by
-// pointer jumping, and the step goes to val (coalesced) and to the ring.
-// So pointers left in val reach only into earlier segments and the resolve
-// chains are short.
+// pointer jumping, and the step goes to sym (coalesced, u16 per byte) and to
+// the ring.  So a pointer left in sym reaches only into the 32 KB before the
+// segment, and is stored as that byte's position mod 32 KB (kSymPtr |
+// position & 0x7FFF): the resolve's ring index.  (Spreading a step's bytes
+// over the threads instead of its tokens -- a max-scan of token marks giving
+// each byte its token, no loop as long as the wave's longest match --
+// measured slower: 17.0-18.3 against 14.8-15.3 ms per 1,000 C2-like files,
+// profiles/r06/expand_bytes_ab.txt.)
 // 512 threads and steps of <= 4000 bytes: 80 KB of LDS, two workgroups per
 // CU, one's barriers overlapping the other's work (1024 threads and 8 KB
 // steps, one per CU: 2.20 ms per C2 batch; this: 1.81; 1024 threads with
@@ -900,7 +952,7 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
   const uint32_t* tok = a.tok + a.tok_off[seg];
   const uint64_t n = a.n_tok[seg];
   const uint64_t o0 = a.lane_out[seg];                 // the segment's first text position
-  const uint64_t f0 = a.file_text[a.lane_file[seg]];  // its file's
+  const uint64_t f0 = a.file_text[a.lane_file[seg]];  // its unit's
   const uint64_t lim = o0 + a.lane_len[seg];           // (a corrupt stream's tokens may make more or fewer bytes
                                                        //  than the decode counted: nothing is written past lim)
   uint64_t base = o0;
@@ -979,8 +1031,7 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
     const uint32_t nw = base + nb <= lim ? nb : base < lim ? (uint32_t)(lim - base) : 0u;
     for (uint32_t i = tid; i < nw; i += kExpandThreads) {
       const uint32_t x = v[i];
-      a.val[base + i] = x;
-      a.text[base + i] = x >> 31 ? (uint8_t)x : kTextPtr;  // (kTextPtr: the resolve pass follows val there)
+      a.sym[base + i] = x >> 31 ? (uint16_t)(x & 0xFFu) : (uint16_t)(kSymPtr | (x & (kRing - 1)));
       ring[(uint32_t)(base + i) & (kRing - 1)] =
           x >> 31 ? (uint16_t)(x & 0xFFu) : (uint16_t)(kRingPtr | (uint32_t)(o0 - 1 - x));
     }
@@ -988,83 +1039,83 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
     base += nb;
     t0 += nt;
   }
-  // a file's last segment: the padding up to the next file ('\n' parses as nothing)
-  for (uint64_t i = lim + tid; i < a.lane_pad[seg]; i += kExpandThreads) a.text[i] = '\n';
   if (bad) atomicOr(a.flags, 1u);
   if (base != lim && tid == 0) atomicOr(a.flags, 4u);
 }
 
-// Pointers (into earlier segments) followed to their literals, 16 text
-// bytes per thread: a group with no kTextPtr byte is done as the expand
-// wrote it; the others load their 16 val entries (one 64-byte load) and
-// follow every pointer at once (independent loads), hop after hop until
-// none is left (one or two hops: a pointer's target is a literal or, if it
-// lies in the first 32 KB of its own segment, a pointer one segment further
-// back).  (A literal 0xFF byte only sends its group down the val path.)
-__global__ __launch_bounds__(256) void inflate_resolve_kernel(const uint32_t* __restrict__ val,
-                                                              uint8_t* __restrict__ text, uint64_t n,
-                                                              uint32_t* __restrict__ flags) {
-  for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g * 16 < n; g += (uint64_t)gridDim.x * 256) {
-    const bool whole = g * 16 + 16 <= n;
-    if (whole) {
-      const uint4 q = *(const uint4*)(text + g * 16);
-      const uint32_t w[4] = {~q.x, ~q.y, ~q.z, ~q.w};  // (a kTextPtr byte: a zero byte of ~w)
-      bool any = false;
+// One workgroup per unit (gzip member): its lanes' bytes in order, the
+// unit's last 32 KB of text in an LDS ring (position & 0x7FFF).  A lane's
+// pointers reach only into the 32 KB before its first byte (the expand
+// followed every back-reference inside the lane), so with the ring holding
+// the text before the lane every byte is final after one LDS read, and the
+// lane's bytes are independent of each other: the threads go through them
+// without a barrier, 16 bytes per thread and step (two 16-byte sym loads, one
+// 16-byte text store).  The lane's last 32 KB go to the other ring, which
+// serves the next lane.  Traffic: 2 B of sym read and 1 B of text written per
+// byte (the round-5 resolve followed u32 pointers hop by hop over the whole
+// batch: 3.6x its bytes).
+constexpr int kResolveThreads = 512;
+constexpr int kResolveGroups = 4;  // 16-byte groups per thread in flight (their sym loads issued together)
+__global__ __launch_bounds__(kResolveThreads) void inflate_resolve_kernel(InflatePlace a) {
+  __shared__ uint8_t ring[2][kRing];
+  const uint32_t u = blockIdx.x, tid = threadIdx.x;
+  const uint64_t u0 = a.file_text[u];
+  const uint16_t* __restrict__ sym = a.sym;
+  uint8_t* __restrict__ text = a.text;
+  int cur = 0;
+  for (uint32_t l = a.unit_lane[u]; l < a.unit_lane[u + 1]; ++l) {
+    const uint64_t o0 = a.lane_out[l], o1 = o0 + a.lane_len[l];
+    const uint64_t tail0 = o1 - o0 > kRing ? o1 - kRing : o0;  // from here on the bytes also go to the next ring
+    const uint8_t* R = ring[cur];
+    uint8_t* N = ring[cur ^ 1];
+    const uint64_t g0 = o0 / 16, g1 = (o1 + 15) / 16;
+    for (uint64_t gb = g0; gb < g1; gb += kResolveThreads * kResolveGroups) {
+      uint4 q[kResolveGroups][2];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) any |= ((w[k] - 0x01010101u) & ~w[k] & 0x80808080u) != 0;
-      if (!any) continue;
-    }
-    // only the kTextPtr bytes are read through val: the other bytes are
-    // final as the expand wrote them, and val holds nothing at a file's
-    // padding (the '\n' up to the next file), which is never written
-    uint32_t x[16];
-    if (whole) {
-      const uint4 t = *(const uint4*)(text + g * 16);
-      const uint32_t tw[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 w = *(const uint4*)(val + g * 16 + 4 * q);
-        const uint32_t v[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t byte = (tw[q] >> (8 * k)) & 0xFFu;
-          x[4 * q + k] = byte == kTextPtr ? v[k] : 0x80000000u | byte;
+      for (int k = 0; k < kResolveGroups; ++k) {
+        const uint64_t g = gb + tid + (uint64_t)k * kResolveThreads;
+        if (g < g1) {
+          q[k][0] = *(const uint4*)(sym + 16 * g);
+          q[k][1] = *(const uint4*)(sym + 16 * g + 8);
         }
       }
-    } else {
 #pragma unroll
-      for (int b = 0; b < 16; ++b) {
-        const uint64_t i = g * 16 + b;
-        x[b] = i < n && text[i] == kTextPtr ? val[i] : 0x80000000u | (i < n ? text[i] : (uint32_t)'\n');
-      }
-    }
-    for (uint32_t hop = 0;; ++hop) {
-      bool any = false;
+      for (int k = 0; k < kResolveGroups; ++k) {
+        const uint64_t g = gb + tid + (uint64_t)k * kResolveThreads;
+        if (g >= g1) break;
+        const uint32_t w[8] = {q[k][0].x, q[k][0].y, q[k][0].z, q[k][0].w, q[k][1].x, q[k][1].y, q[k][1].z, q[k][1].w};
+        uint32_t out[4] = {0, 0, 0, 0};
 #pragma unroll
-      for (int b = 0; b < 16; ++b) any |= !(x[b] >> 31);
-      if (!any) break;
-      if (hop > 64) {  // (cannot happen: every pointer goes back a segment)
-        atomicOr(flags, 2u);
-        break;
-      }
-#pragma unroll
-      for (int b = 0; b < 16; ++b)
-        if (!(x[b] >> 31)) {
-          if (x[b] < n) {
-            x[b] = val[x[b]];
-          } else {  // (only in a batch the expand flagged: the host decodes it)
-            atomicOr(flags, 2u);
-            x[b] = 0x80000000u | '\n';
-          }
+        for (int b = 0; b < 16; ++b) {
+          const uint32_t v = (w[b >> 1] >> (16 * (b & 1))) & 0xFFFFu;
+          const uint32_t r = R[v & (kRing - 1)];  // (read for a literal too: the 64 reads issue without a branch or wait each)
+          const uint32_t byte = v & kSymPtr ? r : v & 0xFFu;
+          out[b >> 2] |= byte << (8 * (b & 3));
         }
-    }
-    uint32_t out[4] = {0, 0, 0, 0};
+        const uint64_t p0 = 16 * g;
+        if (p0 >= o0 && p0 + 16 <= o1) {
+          *(uint4*)(text + p0) = make_uint4(out[0], out[1], out[2], out[3]);
+        } else {  // (a group the lane shares with the lane before or after it)
 #pragma unroll
-    for (int b = 0; b < 16; ++b) out[b >> 2] |= (x[b] & 0xFFu) << (8 * (b & 3));
-    if (whole) *(uint4*)(text + g * 16) = make_uint4(out[0], out[1], out[2], out[3]);
-    else
-      for (int b = 0; b < 16 && g * 16 + b < n; ++b) text[g * 16 + b] = (uint8_t)(out[b >> 2] >> (8 * (b & 3)));
+          for (int b = 0; b < 16; ++b)
+            if (p0 + b >= o0 && p0 + b < o1) text[p0 + b] = (uint8_t)(out[b >> 2] >> (8 * (b & 3)));
+        }
+        if (p0 + 16 > tail0) {
+#pragma unroll
+          for (int b = 0; b < 16; ++b)
+            if (p0 + b >= tail0 && p0 + b < o1) N[(p0 + b) & (kRing - 1)] = (uint8_t)(out[b >> 2] >> (8 * (b & 3)));
+        }
+      }
+    }
+    // a lane shorter than the ring: the ring's older bytes (after the unit's
+    // start) carry over to the next lane
+    const uint64_t keep0 = o1 > u0 + kRing ? o1 - kRing : u0;
+    for (uint64_t p = keep0 + tid; p < tail0; p += kResolveThreads) N[p & (kRing - 1)] = R[p & (kRing - 1)];
+    __syncthreads();
+    cur ^= 1;
   }
+  // a file's last unit: the padding up to the next file ('\n' parses as nothing)
+  for (uint64_t i = u0 + a.unit_len[u] + tid; i < a.unit_pad[u]; i += kResolveThreads) text[i] = '\n';
 }
 
 // CRC-32 (gzip, reflected 0xEDB88320), table in LDS.
@@ -1282,11 +1333,8 @@ hipError_t launch_inflate_expand(const InflatePlace& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_inflate_resolve(const InflatePlace& a, uint64_t text_len, hipStream_t st) {
-  const uint64_t groups = (text_len + 15) / 16;
-  if (groups)
-    hipLaunchKernelGGL(inflate_resolve_kernel, dim3((uint32_t)std::min<uint64_t>(65536, (groups + 255) / 256)),
-                       dim3(256), 0, st, a.val, a.text, text_len, a.flags);
+hipError_t launch_inflate_resolve(const InflatePlace& a, hipStream_t st) {
+  if (a.n_units) hipLaunchKernelGGL(inflate_resolve_kernel, dim3(a.n_units), dim3(kResolveThreads), 0, st, a);
   return hipGetLastError();
 }
 

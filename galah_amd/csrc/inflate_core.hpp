@@ -239,6 +239,15 @@ constexpr uint8_t kClOrder[kClSyms] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 constexpr int kClBits = 7;  // longest code-length code
 struct ClCode {
   uint32_t limit[kClBits + 1];  // left-justified 7-bit codes below limit[l] have length <= l
+  int32_t base[kClBits + 1];    // st.base(l), kept in registers: a symbol then costs one table read, not two
+                                // dependent ones (the search's and the decode's header walks are chains of them)
+  // base[L] by selects (an indexed read of a register array would go through scratch memory)
+  GG_HD int32_t base_of(uint32_t L) const {
+    int32_t b = base[1];
+#pragma unroll
+    for (int l = 2; l <= kClBits; ++l) b = L == (uint32_t)l ? base[l] : b;
+    return b;
+  }
 };
 struct ClArrays {
   int32_t b[kClBits + 1];
@@ -279,11 +288,13 @@ GG_HD bool read_cl_code(const B& in, uint64_t& pos, uint32_t hclen, ClCode& cl, 
     left = (left << 1) - (int)count[l];
     cl.limit[l] = (first + count[l]) << (kClBits - l);
     st.base(l) = (int32_t)offs - (int32_t)first;
+    cl.base[l] = (int32_t)offs - (int32_t)first;
     st.off(l) = (uint8_t)offs;
     offs += count[l];
     first = (first + count[l]) << 1;
   }
   cl.limit[0] = 0;
+  cl.base[0] = 0;
   if (left != 0) return false;  // incomplete or over-subscribed
 #pragma unroll
   for (int s = 0; s < kClSyms; ++s) {
@@ -305,7 +316,7 @@ GG_HD int decode_cl_sym(const B& in, uint64_t& pos, const ClCode& cl, ClS& st) {
   for (int l = 1; l < kClBits; ++l) L += x >= cl.limit[l] ? 1 : 0;
   if (x >= cl.limit[kClBits]) return -1;
   pos += (uint32_t)L;
-  return st.sym(st.base(L) + (int)(x >> (kClBits - L)));
+  return st.sym(cl.base_of((uint32_t)L) + (int)(x >> (kClBits - L)));
 }
 
 // Walks the lit/len + distance code lengths of a dynamic header (after the
@@ -451,7 +462,7 @@ struct HeaderWalk {
     uint32_t L = 1;
 #pragma unroll
     for (int l = 1; l < kClBits; ++l) L += y >= cl.limit[l] ? 1u : 0u;
-    const int s = st.sym(st.base((int)L) + (int)(y >> (kClBits - L)));
+    const int s = st.sym(cl.base_of(L) + (int)(y >> (kClBits - L)));
     pos += L;
     if (s < 16) {
       if (s) add((uint32_t)s, 1);
@@ -495,7 +506,10 @@ struct HeaderWalk {
 // Decode entries: the value in bits 0..15 (a literal byte, a length base or
 // a distance base), its extra bits in 16..19, the code length in 20..23
 // (fast tables only; 0 = not in the table), the kind in 24..25.
-constexpr int kFastBits = 10;
+#ifndef GG_FAST_BITS  // (A/B builds: -DGG_FAST_BITS=9)
+#define GG_FAST_BITS 10
+#endif
+constexpr int kFastBits = GG_FAST_BITS;
 constexpr uint32_t kFastSize = 1u << kFastBits;
 constexpr int kFastLenShift = 20;
 constexpr uint32_t kFastLenMask = 15u << kFastLenShift;

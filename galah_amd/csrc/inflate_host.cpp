@@ -526,61 +526,70 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
   if (text_len >= (1ull << 30)) return hand_back(o, "batch text over 1 GiB", 0);  // (30-bit expand pointers)
   for (uint32_t u = 0; u < nu; ++u) utext[u] += foff[units[u].file];
   for (size_t l = 0; l < lane_out.size(); ++l) lane_out[l] += utext[live[l].unit];
-  uint32_t *d_val, *d_flags, *d_crc, *d_lfile;
-  uint64_t *d_lout, *d_ftext, *d_flen;
-  GZ_SCRATCH(m, "gz_val", std::max<uint64_t>(text_len, 1), &d_val);
-  m->gz_scratch_bytes = std::max<uint64_t>(m->gz_scratch_bytes, 4 * (toks + scr) + 5 * text_len);
-  // (tests: GALAHGPU_TEST_POISON_VAL=<u32> fills val with that word first --
+  uint32_t *d_flags, *d_crc, *d_lfile, *d_ulane;
+  uint16_t* d_sym;
+  uint64_t *d_lout, *d_ftext, *d_flen, *d_upad;
+  GZ_SCRATCH(m, "gz_sym", text_len + 16, &d_sym);
+  m->gz_scratch_bytes = std::max<uint64_t>(m->gz_scratch_bytes, 4 * (toks + scr) + 3 * text_len);
+  // (tests: GALAHGPU_TEST_POISON_VAL=<u16> fills sym with that value first --
   // what a previous batch or another allocation left there -- and no result
-  // may change: the resolve reads val only where the expand wrote it)
+  // may change: the resolve reads sym only where the expand wrote it)
   const char* poison = getenv("GALAHGPU_TEST_POISON_VAL");
   if (poison && *poison && text_len)
-    GG_HIP(m, hipMemsetD32Async(d_val, (int)strtoul(poison, nullptr, 0), text_len, st));
+    GG_HIP(m, hipMemsetD16Async(d_sym, (unsigned short)strtoul(poison, nullptr, 0), text_len, st));
   GG_HIP(m, scratch_t(m, "stage_text", std::max<uint64_t>(text_len, 16) + 16, d_text));
-  // per live lane: text position, token offset, token count, end of the
-  // padding after it (its file's last lane: the next file's start; else 0)
-  // (u64), then its unit (u32)
+  // per live lane: text position, token offset, token count, bytes (u64),
+  // then its unit (u32)
   const size_t NL = std::max<size_t>(live.size(), 1);
-  GG_HIP(m, scratch_t(m, "gz_lout", 5 * NL + (NL + 1) / 2, &d_lout));
-  d_lfile = (uint32_t*)(d_lout + 5 * NL);
+  GG_HIP(m, scratch_t(m, "gz_lout", 4 * NL + (NL + 1) / 2, &d_lout));
+  d_lfile = (uint32_t*)(d_lout + 4 * NL);
+  // per unit: text position, bytes, end of the padding after it (a file's
+  // last unit: the next file's start; else 0) (u64), then its first lane (u32)
   const uint32_t NU = std::max(nu, 1u);
-  GG_HIP(m, scratch_t(m, "gz_ftext", 2 * (size_t)NU + 1, &d_ftext));
+  GG_HIP(m, scratch_t(m, "gz_ftext", 3 * (size_t)NU + 1 + (NU + 2) / 2, &d_ftext));
   d_flen = d_ftext + NU;
+  d_upad = d_ftext + 2 * (size_t)NU;
+  d_ulane = (uint32_t*)(d_ftext + 3 * (size_t)NU + 1);
   GG_HIP(m, scratch_t(m, "gz_flags", 2 * (size_t)NU + 1, &d_flags));
   d_crc = d_flags + 1;
   for (uint32_t f = 0; f < nf; ++f)  // (plain files: their text is copied in after the resolve; until then
     if (!fl[f].gz && foff[f + 1] > foff[f])  //  no byte of theirs may send the resolve to val)
       GG_HIP(m, hipMemsetAsync(*d_text + foff[f], '\n', foff[f + 1] - foff[f], st));
   GG_HIP(m, hipMemsetAsync(d_flags, 0, sizeof(uint32_t), st));
-  std::vector<uint64_t> ftext(2 * (size_t)NU, 0);
+  std::vector<uint64_t> ftext(3 * (size_t)NU + 1 + (NU + 2) / 2, 0);
+  uint32_t* ulane = (uint32_t*)(ftext.data() + 3 * (size_t)NU + 1);
   for (uint32_t u = 0; u < nu; ++u) {
     ftext[u] = utext[u];
     ftext[NU + u] = ulen[u];
+    ftext[2 * (size_t)NU + u] = units[u].last ? foff[units[u].file + 1] : 0;
   }
+  for (size_t l = live.size(); l-- > 0;) ulane[live[l].unit] = (uint32_t)l;  // (every unit has a lane)
+  ulane[nu] = (uint32_t)live.size();
   GG_HIP(m, hipMemcpyAsync(d_ftext, ftext.data(), ftext.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-  std::vector<uint64_t> lv(5 * NL + (NL + 1) / 2, 0);
+  std::vector<uint64_t> lv(4 * NL + (NL + 1) / 2, 0);
   for (size_t l = 0; l < live.size(); ++l) {
-    const Unit& u = units[live[l].unit];
     lv[l] = lane_out[l];
     lv[NL + l] = live[l].tok_off;
     lv[2 * NL + l] = live[l].n_tok;
-    if (u.last && (l + 1 == live.size() || live[l + 1].unit != live[l].unit)) lv[3 * NL + l] = foff[u.file + 1];
-    lv[4 * NL + l] = live[l].out_len;
-    ((uint32_t*)(lv.data() + 5 * NL))[l] = live[l].unit;
+    lv[3 * NL + l] = live[l].out_len;
+    ((uint32_t*)(lv.data() + 4 * NL))[l] = live[l].unit;
   }
   GG_HIP(m, hipMemcpyAsync(d_lout, lv.data(), lv.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   InflatePlace p;
   p.tok = d_tok;
   p.tok_off = d_lout + NL;
   p.n_tok = d_lout + 2 * NL;
-  p.lane_pad = d_lout + 3 * NL;
-  p.lane_len = d_lout + 4 * NL;
+  p.lane_len = d_lout + 3 * NL;
   p.lane_file = d_lfile;
   p.lane_out = d_lout;
   p.file_text = d_ftext;
+  p.unit_len = d_flen;
+  p.unit_pad = d_upad;
+  p.unit_lane = d_ulane;
   p.n_lanes = (uint32_t)live.size();
+  p.n_units = nu;
   p.text = *d_text;
-  p.val = d_val;
+  p.sym = d_sym;
   p.flags = d_flags;
   std::vector<uint32_t> seg_first(nu + 1, 0);
   for (uint32_t u = 0; u < nu; ++u) seg_first[u + 1] = seg_first[u] + (uint32_t)((ulen[u] + kInflateCrcSeg - 1) / kInflateCrcSeg);
@@ -590,8 +599,7 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
   GG_HIP(m, scratch_t(m, "gz_scrc", std::max(nseg, 1u), &d_scrc));
   GG_HIP(m, hipMemcpyAsync(d_sfirst, seg_first.data(), (nu + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
   GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_EXPAND, text_len, st, [&] { return launch_inflate_expand(p, st); }));
-  GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_RESOLVE, text_len, st,
-                         [&] { return launch_inflate_resolve(p, text_len, st); }));
+  GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_RESOLVE, text_len, st, [&] { return launch_inflate_resolve(p, st); }));
   GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_CRC, text_len, st, [&] {
     return launch_inflate_crc(*d_text, nu, d_ftext, d_flen, d_sfirst, nseg, d_scrc, d_crc, st);
   }));
@@ -605,9 +613,7 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
   GG_HIP(m, hipStreamSynchronize(st));
   stamp("expand + resolve + crc");
   if (chk[0])
-    return hand_back(o, chk[0] & 1   ? "distance before the member's start"
-                        : chk[0] & 4 ? "token bytes disagree with the decode's count"
-                                     : "pointer chain",
+    return hand_back(o, chk[0] & 1 ? "distance before the member's start" : "token bytes disagree with the decode's count",
                      0);
   // every gzip file's text starts with '>' (FASTQ, an empty file, anything
   // else: the host path, which reads it or reports it): its first byte is

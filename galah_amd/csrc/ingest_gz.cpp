@@ -547,6 +547,14 @@ gg_status run_lane(gg_ctx* x, GzClaims& cl, uint64_t* d_sk, uint32_t* d_len, int
     runs.clear();
     uint64_t nw = 0;
     uint32_t* d_words = nullptr;
+    // (scratch that grows is sized for the largest batch at once: a batch
+    // cut smaller -- the ramp at a call's start, the tail -- would otherwise
+    // leave it to grow again, with a device-wide wait, in a later call)
+    struct Hint {
+      gg_ctx* m;
+      ~Hint() { m->scratch_hint = 1.0; }
+    } hint{x};
+    x->scratch_hint = g->at ? std::min(16.0, std::max(1.0, (double)gz_batch_bytes() / (double)g->at)) : 1.0;
     const gg_status is = inflate_staged_batch(x, pipe, *g, cl, host_threads, &d_words, &nw, runs);
     if (is != GG_OK) return is;
     const uint32_t ng = (uint32_t)g->idx.size();

@@ -358,19 +358,16 @@ def test_device_inflate_corrupt_streams_fail_as_host(tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("poison", ["0", "257", "0x7fffffff"])
+@pytest.mark.parametrize("poison", ["0", "0x8101", "0xffff"])
 def test_device_inflate_does_not_read_stale_val(golden, monkeypatch, tmp_path, poison):
-    """The resolve pass reads the expand's val array only at the bytes the
-    expand left as pointers.  Before round 5 it read all 16 entries of a
-    group, including the '\\n' padding between files, which no kernel
-    writes, and wrote what those stale words resolved to into the padding:
-    harmless while they held zeros (file 0's '>' started an empty record),
-    but other stale words appended bases to a genome's last record (the
-    round-4 __launch_bounds__(64, 4) build, whose scratch allocation changed
-    what the buffer held).  val filled with a pointer into file 0's sequence
-    (257), with zeros, and with an out-of-range word: the same sketches, no
-    batch handed back; a plain FASTA file first in the batch (its text is
-    never in val) included."""
+    """The resolve pass reads the expand's sym array (u16 per text byte) only
+    in the gzip members' ranges, where the expand wrote every byte.  Before
+    round 5 the resolve read val (u32) entries in the '\n' padding between
+    files, which no kernel writes, and stale words there appended bases to a
+    genome's last record.  sym filled with zeros, with a pointer into the
+    ring (0x8101) and with an invalid value: the same sketches, no batch
+    handed back; a plain FASTA file first in the batch (its text is never in
+    sym) included."""
     monkeypatch.setenv("GALAHGPU_TEST_POISON_VAL", poison)
     plain = tmp_path / "plain_first.fna"
     with gzip.open(golden["paths"][0], "rb") as f:
