@@ -27,6 +27,9 @@
 //   inflate_crc_fold_kernel per file its segments' CRCs folded with x^(8n)
 //                           mod P; checked with ISIZE against the gzip
 //                           trailer by the host
+#include <cstdlib>
+#include <cstring>
+
 #include "device_util.hpp"
 #include "gg_internal.hpp"
 #include "inflate_core.hpp"
@@ -672,6 +675,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
     sbase = w0 * 32;
     slimit = min(seg_end, sbase + (uint64_t)(nw - 8) * 32);
   };
+  const uint64_t t_wave = a.prof ? wall_clock64() : 0;  // (debug: the wave's wall time, for the tail)
   uint32_t* out = a.tok + a.tok_off[seg];
   const uint64_t cap = a.tok_cap[seg];
   uint32_t* scr_all = a.scr + a.scr_off[seg];
@@ -900,6 +904,11 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       status = final_seg ? kDecOk : kDecFinalEarly;
       break;
     }
+  }
+  if (a.prof && j == 0) {
+    const uint64_t dt = wall_clock64() - t_wave;
+    atomicMax((unsigned long long*)&a.prof[6], (unsigned long long)dt);
+    atomicAdd((unsigned long long*)&a.prof[7], (unsigned long long)dt);
   }
   if (j == 0) {
     a.status[seg] = status;
@@ -1277,26 +1286,39 @@ const CrcPowers& crc_powers() {
   return pw;
 }
 
-// A staged batch from its pinned host slot to the device, read by the
-// kernel over PCIe (the host memory is mapped into the device's address
-// space): the bulk of a call's host-to-device bytes goes this way instead of
-// through the DMA engine, where every small copy of the processing lanes (a
-// decode pass's lane table, a parse pass's counts) would wait behind
-// hundreds of MB of queued uploads.  A few workgroups, each thread with four
-// 16-byte loads in flight, keep PCIe busy without taking the CUs.
+// A staged batch from its pinned host slot to the device (launch_slot_upload:
+// a DMA-engine copy; this kernel, GALAHGPU_GZ_UPLOAD=kernel, reads the
+// mapped slot over PCIe -- a few workgroups, each thread with four 16-byte
+// loads in flight -- and was the default until round 6, when its PCIe reads
+// were found to slow the kernels running beside it).
 constexpr int kUploadThreads = 256, kUploadBlocks = 64;
+template <bool kNt>
 __global__ __launch_bounds__(kUploadThreads) void slot_upload_kernel(uint4* __restrict__ dst, const uint4* __restrict__ src,
                                                                      uint64_t n16) {
   const uint64_t stride = (uint64_t)gridDim.x * kUploadThreads;
   uint64_t i = (uint64_t)blockIdx.x * kUploadThreads + threadIdx.x;
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  auto ld = [&](uint64_t k) {
+    if (!kNt) return src[k];
+    const v4u v = __builtin_nontemporal_load((const v4u*)(src + k));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  };
+  auto st = [&](uint64_t k, uint4 v) {
+    if (kNt) {
+      const v4u w = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(w, (v4u*)(dst + k));
+    } else {
+      dst[k] = v;
+    }
+  };
   for (; i + 3 * stride < n16; i += 4 * stride) {
-    const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-    dst[i] = a;
-    dst[i + stride] = b;
-    dst[i + 2 * stride] = c;
-    dst[i + 3 * stride] = d;
+    const uint4 a = ld(i), b = ld(i + stride), c = ld(i + 2 * stride), d = ld(i + 3 * stride);
+    st(i, a);
+    st(i + stride, b);
+    st(i + 2 * stride, c);
+    st(i + 3 * stride, d);
   }
-  for (; i < n16; i += stride) dst[i] = src[i];
+  for (; i < n16; i += stride) st(i, ld(i));
 }
 
 }  // namespace
@@ -1306,9 +1328,25 @@ uint32_t inflate_stage_words() { return kStageWords; }
 hipError_t launch_slot_upload(uint8_t* dst, const uint8_t* src_mapped, uint64_t bytes, hipStream_t st) {
   const uint64_t n16 = (bytes + 15) / 16;  // (both buffers are padded past bytes to a 16-byte multiple)
   if (n16 == 0) return hipSuccess;
-  const uint32_t blocks = (uint32_t)std::min<uint64_t>(kUploadBlocks, (n16 + kUploadThreads - 1) / kUploadThreads);
-  hipLaunchKernelGGL(slot_upload_kernel, dim3(blocks), dim3(kUploadThreads), 0, st, (uint4*)dst, (const uint4*)src_mapped,
-                     n16);
+  // A DMA-engine copy by default: the copy kernel's PCIe reads, running
+  // beside the other lane's kernels, slowed the latency-bound decode ~2x
+  // (a full batch's decode 1.65 ms alone, 4.5-4.8 ms beside the kernel;
+  // 600 C2-like files: decode 14.0 -> 6.6 ms per call, the call 0.038 ->
+  // 0.0315 s, profiles/r06/upload_ab.txt).  GALAHGPU_GZ_UPLOAD=kernel keeps the
+  // kernel (GALAHGPU_GZ_UPLOAD_BLOCKS, GALAHGPU_GZ_UPLOAD_NT=1: its workgroups,
+  // non-temporal accesses -- A/B knobs, read per call).
+  const char* mode = getenv("GALAHGPU_GZ_UPLOAD");
+  if (!(mode && strcmp(mode, "kernel") == 0)) return hipMemcpyAsync(dst, src_mapped, bytes, hipMemcpyHostToDevice, st);
+  const char* eb = getenv("GALAHGPU_GZ_UPLOAD_BLOCKS");
+  const uint64_t want = eb && atoi(eb) > 0 ? (uint64_t)atoi(eb) : (uint64_t)kUploadBlocks;
+  const uint32_t blocks = (uint32_t)std::min<uint64_t>(want, (n16 + kUploadThreads - 1) / kUploadThreads);
+  const char* nt = getenv("GALAHGPU_GZ_UPLOAD_NT");
+  if (nt && *nt == '1')
+    hipLaunchKernelGGL(slot_upload_kernel<true>, dim3(blocks), dim3(kUploadThreads), 0, st, (uint4*)dst,
+                       (const uint4*)src_mapped, n16);
+  else
+    hipLaunchKernelGGL(slot_upload_kernel<false>, dim3(blocks), dim3(kUploadThreads), 0, st, (uint4*)dst,
+                       (const uint4*)src_mapped, n16);
   return hipGetLastError();
 }
 

@@ -411,9 +411,13 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
       GG_HIP(m, hipStreamSynchronize(st));
       GG_HIP(m, hipMemcpy(pr, d_prof, sizeof pr, hipMemcpyDeviceToHost));
       const double nb = (double)std::max<uint64_t>(pr[4], 1);
+      int wc_khz = 0;
+      (void)hipDeviceGetAttribute(&wc_khz, hipDeviceAttributeWallClockRate, m->device);
+      const double us = wc_khz > 0 ? 1e3 / wc_khz : 0.0;  // (wall_clock64 ticks to microseconds)
       fprintf(stderr, "[inflate] decode: %u lanes, %llu blocks, %.0f tokens/block; cycles per block: header %.0f, "
-              "first decode %.0f, resync %.0f, copy %.0f\n", nl, (unsigned long long)pr[4], pr[5] / nb, pr[0] / nb,
-              pr[1] / nb, pr[2] / nb, pr[3] / nb);
+              "first decode %.0f, resync %.0f, copy %.0f; wave wall mean %.1f us, max %.1f us\n", nl,
+              (unsigned long long)pr[4], pr[5] / nb, pr[0] / nb, pr[1] / nb, pr[2] / nb, pr[3] / nb,
+              pr[7] * us / std::max(nl, 1u), pr[6] * us);
     }
     std::vector<uint64_t> res((size_t)nl * 4);
     GG_HIP(m, hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));

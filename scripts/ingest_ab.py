@@ -73,7 +73,7 @@ try:
             os.environ.update(env)
             ctx.precluster_files(paths, 0.95)
             for k in env:
-                os.environ.pop(k)
+                os.environ.pop(k, None)
         for c in range(calls):
             for name, env in settings:
                 os.environ.update(env)
@@ -93,7 +93,7 @@ try:
                 ctx.timing_enable(False)
                 os.environ.pop("GALAHGPU_GZ_LANES")
                 for k in env:
-                    os.environ.pop(k)
+                    os.environ.pop(k, None)
         info = ctx.info_line()
     for name, _ in settings:
         r = res[name]
