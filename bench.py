@@ -56,7 +56,7 @@ ISSUE_MODEL = os.path.join(ROOT, "profiles", "r04_k1_issue_model.json")
 # scripts/k2_pmc.sh + scripts/k2_pmc_model.py
 K2_PMC = os.path.join(ROOT, "profiles", "r05_k2_pmc.json")
 # the device-inflate ingest kernels' counters at C2 (scripts/ingest_pmc.sh + ingest_pmc_model.py)
-INGEST_PMC = os.path.join(ROOT, "profiles", "r05_ingest_pmc.json")
+INGEST_PMC = os.path.join(ROOT, "profiles", "r06", "ingest_pmc.json")
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 from host_cpus import host_cpu_info  # noqa: E402
 
@@ -428,21 +428,21 @@ def roofline_ingest(ks, wall_s, gz_bytes, text_bytes, pcie_gbps=None):
     HIP-event ms per call of each kernel class on the stream it ran on (one
     call with one processing lane, so no kernel shares the GPU with
     another), its algorithmic bytes against 8 TB/s HBM, and the PMC pass's
-    VALU issue share and HBM bytes (profiles/r05_ingest_pmc.json, the same
-    C2 workload).  Algorithmic bytes per call (G = gzip bytes, X = text
+    VALU issue share and HBM bytes (profiles/r06/ingest_pmc.json, 1,000
+    C2-like files).  Algorithmic bytes per call (G = gzip bytes, X = text
     bytes, T = tokens the decode wrote):
       upload  G (host -> device over PCIe: priced against the box's measured
               PCIe H2D rate, pcie_h2d_gbps, not HBM; not a candidate for
               the dominant HBM kernel)
       search  G read once
       decode  G read + 4 T (tokens written)
-      expand  4 T read + 5 X (val u32 + the text byte per text byte)
-      resolve 2 X (the text read and rewritten)
+      expand  4 T read + 2 X (sym: u16 per text byte)
+      resolve 3 X (sym read, the text written)
       crc     X
       parse   3.25 X (three passes over the text, X / 4 of packed words)"""
     G, X = float(gz_bytes), float(text_bytes)
     T = float(ks["decode"]["work"]) if ks.get("decode") else 0.0
-    alg = {"upload": G, "search": G, "decode": G + 4 * T, "expand": 4 * T + 5 * X, "resolve": 2 * X, "crc": X,
+    alg = {"upload": G, "search": G, "decode": G + 4 * T, "expand": 4 * T + 2 * X, "resolve": 3 * X, "crc": X,
            "parse": 3.25 * X}
     pmc = {}
     if os.path.exists(INGEST_PMC):
@@ -494,7 +494,7 @@ def roofline_ingest(ks, wall_s, gz_bytes, text_bytes, pcie_gbps=None):
                     "bench.py roofline_ingest) / their summed HIP-event time on their own streams, one call with "
                     "one lane (GALAHGPU_GZ_LANES=1); the default two lanes overlap these kernels; upload (host "
                     "memory over PCIe) is priced against pcie_h2d_GBps, the box's pinned H2D DMA rate; pmc: "
-                    "profiles/r05_ingest_pmc.json (valu_frac_guide = VALU wave-instructions / (1024 SIMDs x "
+                    "profiles/r06/ingest_pmc.json (valu_frac_guide = VALU wave-instructions / (1024 SIMDs x "
                     "cycles / 2), hbm_bytes = FETCH_SIZE x 2 + WRITE_SIZE)"}
 
 

@@ -1,5 +1,5 @@
 """Per-kernel PMC summary of the device-inflate ingest (one C2 file list
-through gg_precluster_files, one lane) -> profiles/r05_ingest_pmc.json.
+through gg_precluster_files, one lane) -> profiles/r06/ingest_pmc.json.
 
 Input: the directory scripts/ingest_pmc.sh wrote, one rocprofv3 run per
 pass over `scripts/inflate_probe.py 1000 1` (a warm-up call and a timed one:
@@ -43,7 +43,7 @@ def short(name):
 
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--out")]
-    out_path = os.path.join(km.ROOT, "profiles", "r05_ingest_pmc.json")
+    out_path = os.path.join(km.ROOT, "profiles", "r06", "ingest_pmc.json")
     for a in sys.argv[1:]:
         if a.startswith("--out="):
             out_path = a.split("=", 1)[1]
