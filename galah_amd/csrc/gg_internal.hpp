@@ -296,6 +296,7 @@ struct InflatePlace {
                                // a byte of the 32 KB before the lane's first byte
   uint32_t* flags;             // bit 0: a distance before its file's start,
                                // bit 2: a lane's tokens make other than lane_len bytes
+  uint64_t* prof = nullptr;    // (debug) expand cycles: fill, pointer rounds, write-out; steps, rounds
 };
 constexpr uint16_t kSymPtr = 0x8000u;
 // one file of an inflate batch (inflate_host.cpp): its bytes at

@@ -967,6 +967,14 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
   uint64_t base = o0;
   bool bad = false;
   uint32_t tk_next = tid < n ? tok[tid] : 0u;  // (the next step's token, loaded a step ahead)
+  uint64_t tp = a.prof ? clock64() : 0;  // (GALAHGPU_INFLATE_DEBUG: cycles per phase, thread 0)
+  auto phase = [&](int k) {
+    if (a.prof) {
+      const uint64_t t = clock64();
+      if (tid == 0) atomicAdd((unsigned long long*)&a.prof[k], (unsigned long long)(t - tp));
+      tp = t;
+    }
+  };
   for (uint64_t t0 = 0; t0 < n;) {
     const uint64_t ti = t0 + tid;
     const uint32_t tk = tk_next;
@@ -1025,7 +1033,9 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
       const uint64_t tn = t0 + nt + tid;  // the next step's token (in flight during this step's LDS work)
       tk_next = tn < n ? tok[tn] : 0u;
     }
+    phase(0);
     for (;;) {  // kIntra pointers followed inside the step (each points to an earlier byte)
+      if (a.prof && tid == 0) atomicAdd((unsigned long long*)&a.prof[4], 1ull);
       bool more = false;
       for (uint32_t i = tid; i < nb; i += kExpandThreads) {
         const uint32_t x = v[i];
@@ -1037,6 +1047,7 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
       }
       if (!__syncthreads_or(more)) break;
     }
+    phase(1);
     const uint32_t nw = base + nb <= lim ? nb : base < lim ? (uint32_t)(lim - base) : 0u;
     for (uint32_t i = tid; i < nw; i += kExpandThreads) {
       const uint32_t x = v[i];
@@ -1045,6 +1056,8 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
           x >> 31 ? (uint16_t)(x & 0xFFu) : (uint16_t)(kRingPtr | (uint32_t)(o0 - 1 - x));
     }
     __syncthreads();
+    phase(2);
+    if (a.prof && tid == 0) atomicAdd((unsigned long long*)&a.prof[3], 1ull);
     base += nb;
     t0 += nt;
   }

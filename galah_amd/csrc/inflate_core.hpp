@@ -239,15 +239,12 @@ constexpr uint8_t kClOrder[kClSyms] = {16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 
 constexpr int kClBits = 7;  // longest code-length code
 struct ClCode {
   uint32_t limit[kClBits + 1];  // left-justified 7-bit codes below limit[l] have length <= l
-  int32_t base[kClBits + 1];    // st.base(l), kept in registers: a symbol then costs one table read, not two
-                                // dependent ones (the search's and the decode's header walks are chains of them)
-  // base[L] by selects (an indexed read of a register array would go through scratch memory)
-  GG_HD int32_t base_of(uint32_t L) const {
-    int32_t b = base[1];
-#pragma unroll
-    for (int l = 2; l <= kClBits; ++l) b = L == (uint32_t)l ? base[l] : b;
-    return b;
-  }
+  // st.base(l) for l = 1..7 as signed bytes of one register pair (|base| <
+  // 128: 19 symbols, 7-bit codes), so a symbol costs one table read, not two
+  // dependent ones (the search's and the decode's header walks are chains of
+  // them); an array here was indexed from scratch memory
+  uint64_t base8;
+  GG_HD int32_t base_of(uint32_t L) const { return (int32_t)(int8_t)(uint8_t)(base8 >> (8 * L)); }
 };
 struct ClArrays {
   int32_t b[kClBits + 1];
@@ -283,18 +280,19 @@ GG_HD bool read_cl_code(const B& in, uint64_t& pos, uint32_t hclen, ClCode& cl, 
   }
   int left = 1;
   uint32_t first = 0, offs = 0;
+  uint64_t base8 = 0;
 #pragma unroll
   for (int l = 1; l <= kClBits; ++l) {
     left = (left << 1) - (int)count[l];
     cl.limit[l] = (first + count[l]) << (kClBits - l);
     st.base(l) = (int32_t)offs - (int32_t)first;
-    cl.base[l] = (int32_t)offs - (int32_t)first;
+    base8 |= (uint64_t)(uint8_t)(int8_t)((int32_t)offs - (int32_t)first) << (8 * l);
     st.off(l) = (uint8_t)offs;
     offs += count[l];
     first = (first + count[l]) << 1;
   }
   cl.limit[0] = 0;
-  cl.base[0] = 0;
+  cl.base8 = base8;
   if (left != 0) return false;  // incomplete or over-subscribed
 #pragma unroll
   for (int s = 0; s < kClSyms; ++s) {

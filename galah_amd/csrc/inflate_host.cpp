@@ -602,7 +602,22 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
   GG_HIP(m, scratch_t(m, "gz_sfirst", nu + 1, &d_sfirst));
   GG_HIP(m, scratch_t(m, "gz_scrc", std::max(nseg, 1u), &d_scrc));
   GG_HIP(m, hipMemcpyAsync(d_sfirst, seg_first.data(), (nu + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  uint64_t* d_eprof = nullptr;
+  if (inflate_debug()) {
+    GG_HIP(m, scratch_t(m, "gz_eprof", 8, &d_eprof));
+    GG_HIP(m, hipMemsetAsync(d_eprof, 0, 8 * sizeof(uint64_t), st));
+    p.prof = d_eprof;
+  }
   GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_EXPAND, text_len, st, [&] { return launch_inflate_expand(p, st); }));
+  if (d_eprof) {
+    uint64_t pr[8];
+    GG_HIP(m, hipStreamSynchronize(st));
+    GG_HIP(m, hipMemcpy(pr, d_eprof, sizeof pr, hipMemcpyDeviceToHost));
+    const double ns = (double)std::max<uint64_t>(pr[3], 1);
+    fprintf(stderr, "[inflate] expand: %zu lanes, %.1f steps each, %.2f pointer rounds per step; cycles per step: "
+            "fill %.0f, pointer rounds %.0f, write-out %.0f\n", live.size(), pr[3] / (double)std::max<size_t>(live.size(), 1),
+            pr[4] / ns, pr[0] / ns, pr[1] / ns, pr[2] / ns);
+  }
   GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_RESOLVE, text_len, st, [&] { return launch_inflate_resolve(p, st); }));
   GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_CRC, text_len, st, [&] {
     return launch_inflate_crc(*d_text, nu, d_ftext, d_flen, d_sfirst, nseg, d_scrc, d_crc, st);
