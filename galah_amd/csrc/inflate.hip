@@ -920,26 +920,28 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
 }
 
 // One workgroup per segment, its output built in order in steps of up to
-// kExpandThreads tokens / kExpandBytes bytes.  The segment's last 32 KB of output stay
-// in an LDS ring (u16 per byte: a literal, or a back-reference to before
-// the segment as its distance from the segment's start), so every
+// kExpandThreads tokens / kExpandBytes bytes.  The segment's last 32 KB of
+// output stay in an LDS ring in sym's form (u16 per byte: a literal, or
+// kSymPtr | the position mod 32 KB of a byte before the segment), so every
 // back-reference inside the segment is an LDS read: a step's bytes are
-// staged as literals, pointers to before the segment (the segment before is
-// not expanded yet: the resolve pass follows them), ring values, or kIntra |
-// the step byte they copy; kIntra pointers are followed inside the step by
-// pointer jumping, and the step goes to sym (coalesced, u16 per byte) and to
-// the ring.  So a pointer left in sym reaches only into the 32 KB before the
-// segment, and is stored as that byte's position mod 32 KB (kSymPtr |
-// position & 0x7FFF): the resolve's ring index.  (Spreading a step's bytes
-// over the threads instead of its tokens -- a max-scan of token marks giving
-// each byte its token, no loop as long as the wave's longest match --
-// measured slower: 17.0-18.3 against 14.8-15.3 ms per 1,000 C2-like files,
-// profiles/r06/expand_bytes_ab.txt.)
+// staged (u16) as literals, pointers to before the segment (the segment
+// before is not expanded yet: the resolve pass follows them), ring values,
+// or kStepRef | the step byte they copy; kStepRef entries are followed
+// inside the step by pointer jumping, and the step goes to sym (coalesced)
+// and to the ring.  So a pointer left in sym reaches only into the 32 KB
+// before the segment, as the resolve's ring index.
+//
+// The tokens come from global memory kTokBuf at a time into LDS.  A wave
+// waits for a global load with every older global store of its own
+// outstanding (one counter for both, completed in order), and the step's
+// sym stores take ~25 us to complete: reading the next step's tokens from
+// global memory cost ~65k cycles per step against ~11k of work
+// (GALAHGPU_INFLATE_DEBUG with -DGG_EXPAND_PROF); with the LDS buffer one
+// step in four waits.  (Spreading a step's bytes over the threads instead of
+// its tokens measured slower: profiles/r06/expand_bytes_ab.txt.)
 // 512 threads and steps of <= 4000 bytes: 80 KB of LDS, two workgroups per
-// CU, one's barriers overlapping the other's work (1024 threads and 8 KB
-// steps, one per CU: 2.20 ms per C2 batch; this: 1.81; 1024 threads with
-// 4000-byte steps: 2.34).  (A/B builds: scripts/ab_lib.sh with
-// -DGG_EXPAND_THREADS=... -DGG_EXPAND_BYTES=...)
+// CU.  (A/B builds: scripts/ab_lib.sh with -DGG_EXPAND_THREADS=...
+// -DGG_EXPAND_BYTES=..., -DGG_EXPAND_PROF: the debug line's phase cycles)
 #ifndef GG_EXPAND_THREADS
 #define GG_EXPAND_THREADS 512
 #endif
@@ -948,12 +950,15 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
 #endif
 constexpr int kExpandThreads = GG_EXPAND_THREADS;
 constexpr uint32_t kExpandBytes = GG_EXPAND_BYTES;
-constexpr uint32_t kRing = 32768;          // the DEFLATE window
-constexpr uint32_t kIntra = 0x40000000u;   // (batch text < 2^30 bytes: pointers leave bit 30 clear)
-constexpr uint16_t kRingPtr = 0x8000u;     // ring entry: pointer to o0 - 1 - (entry & 0x7FFF)
+constexpr uint32_t kTokBuf = 4 * kExpandThreads - 128;  // tokens held in LDS (~4 steps of FASTA; the
+                                                        // total stays within 80 KB: two workgroups per CU)
+constexpr uint32_t kRing = 32768;       // the DEFLATE window
+constexpr uint16_t kStepRef = 0x4000u;  // step entry: the value of step byte (entry & 0x0FFF)
+static_assert(kExpandBytes <= 0x1000, "step bytes are 12-bit kStepRef indices");
 __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflatePlace a) {
-  __shared__ uint32_t v[kExpandBytes];
+  __shared__ uint16_t v[kExpandBytes];
   __shared__ uint16_t ring[kRing];
+  __shared__ uint32_t tb[kTokBuf];
   __shared__ uint32_t s_take, s_bytes;
   __shared__ uint32_t wsum[kExpandThreads / 64];
   const uint32_t seg = blockIdx.x;
@@ -966,8 +971,9 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
                                                        //  than the decode counted: nothing is written past lim)
   uint64_t base = o0;
   bool bad = false;
-  uint32_t tk_next = tid < n ? tok[tid] : 0u;  // (the next step's token, loaded a step ahead)
-  uint64_t tp = a.prof ? clock64() : 0;  // (GALAHGPU_INFLATE_DEBUG: cycles per phase, thread 0)
+  uint64_t tb0 = 0, tb1 = 0;  // tokens [tb0, tb1) are in tb
+#ifdef GG_EXPAND_PROF
+  uint64_t tp = a.prof ? clock64() : 0;
   auto phase = [&](int k) {
     if (a.prof) {
       const uint64_t t = clock64();
@@ -975,9 +981,22 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
       tp = t;
     }
   };
+#else
+  auto phase = [](int) {};
+#endif
   for (uint64_t t0 = 0; t0 < n;) {
+    if (t0 + kExpandThreads > tb1 && tb1 < n) {  // (uniform) the buffer from t0 on
+      tb0 = t0;
+      tb1 = min(n, t0 + kTokBuf);
+#pragma unroll
+      for (uint32_t k = 0; k < (kTokBuf + kExpandThreads - 1) / kExpandThreads; ++k) {
+        const uint64_t ti = t0 + tid + k * kExpandThreads;
+        if (ti < tb1) tb[tid + k * kExpandThreads] = tok[ti];
+      }
+      __syncthreads();
+    }
     const uint64_t ti = t0 + tid;
-    const uint32_t tk = tk_next;
+    const uint32_t tk = ti < n ? tb[(uint32_t)(ti - tb0)] : 0u;
     const uint32_t len = ti < n ? tok_len(tk) : 0u;
     uint32_t inc = len;
 #pragma unroll
@@ -991,6 +1010,7 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
       s_bytes = 0;
     }
     __syncthreads();
+    phase(5);
     for (uint32_t w = 0; w < wave; ++w) inc += wsum[w];
     const uint32_t before = inc - len;
     const bool take = ti < n && inc <= kExpandBytes;  // (a prefix of the threads; thread 0 always)
@@ -1002,26 +1022,21 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
     }
     if (take) {
       if (!tok_is_match(tk)) {
-        v[before] = 0x80000000u | tk;
+        v[before] = (uint16_t)(tk & 0xFFu);
       } else {
         const uint32_t dist = tok_dist(tk);
         const uint64_t p = base + before;
         if (p < f0 + dist) {
-          bad = true;  // a distance before the file's first byte
-          for (uint32_t k = 0; k < len; ++k) v[before + k] = 0x80000000u | '\n';
+          bad = true;  // a distance before the unit's first byte
+          for (uint32_t k = 0; k < len; ++k) v[before + k] = (uint16_t)'\n';
         } else {
           const uint64_t src = p - dist;
           for (uint32_t k = 0; k < len; ++k) {
             const uint64_t s = src + k;
-            uint32_t x;
-            if (s >= base) {
-              x = kIntra | (uint32_t)(s - base);
-            } else if (s < o0) {
-              x = (uint32_t)s;
-            } else {
-              const uint32_t r = ring[(uint32_t)s & (kRing - 1)];
-              x = r & kRingPtr ? (uint32_t)(o0 - 1 - (r & 0x7FFFu)) : 0x80000000u | r;
-            }
+            uint16_t x;
+            if (s >= base) x = (uint16_t)(kStepRef | (uint32_t)(s - base));
+            else if (s < o0) x = (uint16_t)(kSymPtr | ((uint32_t)s & (kRing - 1)));
+            else x = ring[(uint32_t)s & (kRing - 1)];
             v[before + k] = x;
           }
         }
@@ -1029,20 +1044,18 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
     }
     __syncthreads();
     const uint32_t nb = s_bytes, nt = s_take;
-    {
-      const uint64_t tn = t0 + nt + tid;  // the next step's token (in flight during this step's LDS work)
-      tk_next = tn < n ? tok[tn] : 0u;
-    }
     phase(0);
-    for (;;) {  // kIntra pointers followed inside the step (each points to an earlier byte)
+    for (;;) {  // kStepRef entries followed inside the step (each points to an earlier byte)
+#ifdef GG_EXPAND_PROF
       if (a.prof && tid == 0) atomicAdd((unsigned long long*)&a.prof[4], 1ull);
+#endif
       bool more = false;
       for (uint32_t i = tid; i < nb; i += kExpandThreads) {
         const uint32_t x = v[i];
-        if ((x & 0xC0000000u) == kIntra) {
-          const uint32_t y = v[x & 0x3FFFFFFFu];
-          v[i] = y;
-          more |= (y & 0xC0000000u) == kIntra;
+        if ((x & 0xC000u) == kStepRef) {
+          const uint32_t y = v[x & 0x0FFFu];
+          v[i] = (uint16_t)y;
+          more |= (y & 0xC000u) == kStepRef;
         }
       }
       if (!__syncthreads_or(more)) break;
@@ -1050,14 +1063,15 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
     phase(1);
     const uint32_t nw = base + nb <= lim ? nb : base < lim ? (uint32_t)(lim - base) : 0u;
     for (uint32_t i = tid; i < nw; i += kExpandThreads) {
-      const uint32_t x = v[i];
-      a.sym[base + i] = x >> 31 ? (uint16_t)(x & 0xFFu) : (uint16_t)(kSymPtr | (x & (kRing - 1)));
-      ring[(uint32_t)(base + i) & (kRing - 1)] =
-          x >> 31 ? (uint16_t)(x & 0xFFu) : (uint16_t)(kRingPtr | (uint32_t)(o0 - 1 - x));
+      const uint16_t x = v[i];
+      a.sym[base + i] = x;
+      ring[(uint32_t)(base + i) & (kRing - 1)] = x;
     }
     __syncthreads();
     phase(2);
+#ifdef GG_EXPAND_PROF
     if (a.prof && tid == 0) atomicAdd((unsigned long long*)&a.prof[3], 1ull);
+#endif
     base += nb;
     t0 += nt;
   }

@@ -615,8 +615,8 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
     GG_HIP(m, hipMemcpy(pr, d_eprof, sizeof pr, hipMemcpyDeviceToHost));
     const double ns = (double)std::max<uint64_t>(pr[3], 1);
     fprintf(stderr, "[inflate] expand: %zu lanes, %.1f steps each, %.2f pointer rounds per step; cycles per step: "
-            "fill %.0f, pointer rounds %.0f, write-out %.0f\n", live.size(), pr[3] / (double)std::max<size_t>(live.size(), 1),
-            pr[4] / ns, pr[0] / ns, pr[1] / ns, pr[2] / ns);
+            "token wait + scan %.0f, fill %.0f, pointer rounds %.0f, write-out %.0f\n", live.size(),
+            pr[3] / (double)std::max<size_t>(live.size(), 1), pr[4] / ns, pr[5] / ns, pr[0] / ns, pr[1] / ns, pr[2] / ns);
   }
   GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_RESOLVE, text_len, st, [&] { return launch_inflate_resolve(p, st); }));
   GG_HIP(m, timed_launch(m, GG_KERNEL_INFLATE_CRC, text_len, st, [&] {
