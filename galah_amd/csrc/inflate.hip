@@ -302,13 +302,16 @@ constexpr uint32_t kSpanLanes = 64;  // one wave per segment, one sub-span per l
 // instead of a 16-byte piece of 64 lines, which the L2 evicted half written
 // (round 5: the decode moved 6.1x its bytes), and the copy-out's loads are
 // coalesced the same way.
+// Tokens before `on` is set (a first decode's, before its first checkpoint:
+// they are dropped) keep their index but are not stored.
 struct TokSink {
   uint32_t* p;
   uint32_t cap;
+  bool on;
   uint32_t k = 0;
   __device__ bool operator()(uint32_t tk) {
     if (k >= cap) return false;
-    p[(size_t)k * kSpanLanes] = tk;
+    if (on) p[(size_t)k * kSpanLanes] = tk;
     ++k;
     return true;
   }
@@ -484,11 +487,10 @@ struct LdsCursor {
 template <class Emit, class Ck>
 __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_t base, uint64_t start, uint64_t s_nom,
                                     uint64_t range_end, LaneTables<LdsStore>& t, Emit&& emit, Ck&& ck, uint32_t& n,
-                                    uint64_t& bytes_out, uint64_t& stop) {
+                                    uint64_t& stop) {
   LdsCursor cur{lds};
   cur.seek((uint32_t)(start - base));
   n = 0;
-  uint32_t bytes = 0;
   uint32_t k = 0;
   uint32_t next_ck = (uint32_t)(s_nom - base);
   const uint32_t rend = (uint32_t)(range_end - base);
@@ -501,7 +503,7 @@ __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_
         break;
       }
       if (cur.pos >= next_ck) {
-        if (!ck(k, ck_pack(cur.pos - next_ck, n, bytes))) {
+        if (!ck(k, ck_pack(cur.pos - next_ck, n, 0))) {
           st = kSpanSynced;
           break;
         }
@@ -523,11 +525,12 @@ __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_
     const uint32_t kind = entry_kind(e);
     const bool lit = kind == kEntryLit && l1 != 0;
     const bool mat = kind == kEntryLen && l1 != 0 && dl != 0 && entry_kind(de) == kEntryLen;
-    if (lit || mat) {
-      cur.advance(lit ? l1 : u + dl + dx, x, y);
-      if (!emit(lit ? entry_value(e) : tok_match(lenv, distv))) break;
+    if (lit || mat) {  // (the advance and the token by selects: one path for both kinds)
+      const uint32_t adv = lit ? l1 : u + dl + dx;
+      const uint32_t tk = lit ? entry_value(e) : tok_match(lenv, distv);
+      cur.advance(adv, x, y);
+      if (!emit(tk)) break;
       ++n;
-      bytes += lit ? 1u : lenv;
       continue;
     }
     // decode_span's handling of the other symbols
@@ -538,7 +541,6 @@ __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_
         if (entry_kind(e2) == kEntryLit) {
           if (!emit(entry_value(e2))) break;
           ++n;
-          bytes += 1;
           continue;
         }
         if (entry_kind(e2) == kEntryEob) st = kSpanEob;
@@ -550,7 +552,6 @@ __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_
       const uint32_t dist = entry_value(d2) + cur.get(entry_extra(d2));
       if (!emit(tok_match(len, dist))) break;
       ++n;
-      bytes += len;
       continue;
     }
     if (kind != kEntryLen) {  // end-of-block or an invalid code (a literal took the fast path)
@@ -566,13 +567,11 @@ __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_
       const uint32_t dist = entry_value(d2) + cur.get(entry_extra(d2));
       if (!emit(tok_match(lenv, dist))) break;
       ++n;
-      bytes += lenv;
       continue;
     }
     cur.skip(used + dl);  // an invalid distance code
     break;
   }
-  bytes_out = bytes;
   stop = base + cur.pos;
   return st;
 }
@@ -585,14 +584,18 @@ __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_
 #define GG_COPY_BATCH 32
 #endif
 constexpr uint32_t kCopyBatch = GG_COPY_BATCH;
-__device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint32_t n) {
-  uint32_t i = 0;
+// Returns the bytes the tokens stand for (the decodes count no bytes).
+__device__ uint32_t copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src, uint32_t n) {
+  uint32_t i = 0, bytes = 0;
   for (; i + kCopyBatch <= n; i += kCopyBatch) {
     uint32_t v[kCopyBatch];
 #pragma unroll
     for (uint32_t k = 0; k < kCopyBatch; ++k) v[k] = src[(size_t)(i + k) * kSpanLanes];
 #pragma unroll
-    for (uint32_t k = 0; k < kCopyBatch; ++k) dst[i + k] = v[k];
+    for (uint32_t k = 0; k < kCopyBatch; ++k) {
+      dst[i + k] = v[k];
+      bytes += tok_len(v[k]);
+    }
   }
   // the rest: all loads first, then the stores
   uint32_t v[kCopyBatch];
@@ -601,7 +604,11 @@ __device__ void copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __restri
     if (i + k < n) v[k] = src[(size_t)(i + k) * kSpanLanes];
 #pragma unroll
   for (uint32_t k = 0; k < kCopyBatch; ++k)
-    if (i + k < n) dst[i + k] = v[k];
+    if (i + k < n) {
+      dst[i + k] = v[k];
+      bytes += tok_len(v[k]);
+    }
+  return bytes;
 }
 
 // One wave per segment (a found block start up to the next one).  Per block:
@@ -746,18 +753,19 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       // the wave's areas, each lane's entries interleaved (stride kSpanLanes)
       uint32_t* A = scr_all + j;                                   // first decode
       uint32_t* B = scr_all + kSpanLanes * capL + j;               // second decode
-      uint64_t* ck = (uint64_t*)(scr_all + 2 * kSpanLanes * capL) + j;  // the first decode's checkpoints
+      uint32_t* ck = scr_all + 2 * kSpanLanes * capL + j;  // the first decode's checkpoints (ck_pack's low word)
 #define CK(k) ck[(size_t)(k) * kSpanLanes]
       // the first decode, from S
       uint32_t na = 0, nck = 0, sa = kSpanRange;
-      uint64_t ba = 0, Ea = S;
+      uint64_t Ea = S;
       if (act) {
-        TokSink sink{A, (uint32_t)capL};
+        TokSink sink{A, (uint32_t)capL, false};
         auto ck1 = [&](uint32_t k, uint64_t c) {
           if (k < ncks) {
-            CK(k) = c;
+            CK(k) = (uint32_t)c;
             nck = k + 1;
           }
+          sink.on = true;  // (from the first checkpoint on the tokens are kept)
           return true;
         };
         // (a lane after the first starts kWarmBits early, so that its decode
@@ -766,8 +774,9 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
         // whose longest kept the whole wave waiting; its tokens before the
         // first checkpoint are dropped as before)
         const uint64_t S0 = j == 0 ? S : (S - bstart > kWarmBits ? S - kWarmBits : bstart);
-        if constexpr (kStaged) sa = decode_span_lds(stage, sbase, S0, S, R, tab, sink, ck1, na, ba, Ea);
-        else sa = decode_span(in, S0, S, R, tab, sink, ck1, na, ba, Ea);
+        uint64_t unused_bytes = 0;
+        if constexpr (kStaged) sa = decode_span_lds(stage, sbase, S0, S, R, tab, sink, ck1, na, Ea);
+        else sa = decode_span(in, S0, S, R, tab, sink, ck1, na, unused_bytes, Ea);
         sink.flush();
       }
       phase(1);
@@ -775,7 +784,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       bool redone = false;
       int synced = -1;
       uint32_t nb = 0, sb = kSpanRange;
-      uint64_t bb = 0, Eb = 0;
+      uint64_t Eb = 0;
       uint32_t c_end = 0;
       bool overrun = false;
       for (;;) {
@@ -808,7 +817,7 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
           redone = true;
           synced = -1;
           first = eprev;
-          TokSink sink{B, (uint32_t)capL};
+          TokSink sink{B, (uint32_t)capL, true};
           auto ck2 = [&](uint32_t k, uint64_t cc) {
             if (k < nck && ck_off(cc) == ck_off(CK(k))) {
               synced = (int)k;
@@ -816,8 +825,9 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
             }
             return true;
           };
-          if constexpr (kStaged) sb = decode_span_lds(stage, sbase, eprev, S, R, tab, sink, ck2, nb, bb, Eb);
-          else sb = decode_span(in, eprev, S, R, tab, sink, ck2, nb, bb, Eb);
+          uint64_t unused_bytes = 0;
+          if constexpr (kStaged) sb = decode_span_lds(stage, sbase, eprev, S, R, tab, sink, ck2, nb, Eb);
+          else sb = decode_span(in, eprev, S, R, tab, sink, ck2, nb, unused_bytes, Eb);
           sink.flush();
         }
       }
@@ -845,33 +855,27 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
       const uint32_t* p1 = A;
       const uint32_t* p2 = A;
       uint32_t n1 = 0, n2 = 0;
-      uint64_t vbytes = 0;
       if (j <= c_end) {
         if (!redone) {
-          const uint64_t c0 = CK(0);
+          const uint32_t c0 = CK(0);
           p1 = A + (size_t)ck_tok(c0) * kSpanLanes;
           n1 = na - ck_tok(c0);
-          vbytes = ba - ck_bytes(c0);
         } else {
           p1 = B;
           n1 = nb;
-          vbytes = bb;
           if (synced >= 0) {
-            const uint64_t ck_s = CK(synced);
+            const uint32_t ck_s = CK(synced);
             p2 = A + (size_t)ck_tok(ck_s) * kSpanLanes;
             n2 = na - ck_tok(ck_s);
-            vbytes += ba - ck_bytes(ck_s);
           }
         }
       }
       const uint32_t valid = n1 + n2;
       uint32_t incl = valid;
-      uint64_t tb = vbytes;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(incl, o);
         if (j >= (uint32_t)o) incl += y;
-        tb += __shfl_xor(tb, o);
       }
       const uint32_t total = __shfl(incl, 63);
       if (n_out + total > cap) {
@@ -880,8 +884,10 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
         break;
       }
       uint32_t* dst = out + n_out + (incl - valid);
-      copy_tokens(dst, p1, n1);
-      copy_tokens(dst + n1, p2, n2);
+      uint64_t tb = copy_tokens(dst, p1, n1);  // (the bytes they stand for: the decodes count none)
+      tb += copy_tokens(dst + n1, p2, n2);
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) tb += __shfl_xor(tb, o);
 #undef CK
       phase(3);
       if (a.prof && j == 0) {

@@ -971,7 +971,8 @@ GG_HD void span_layout(uint64_t body0, uint64_t span_end, uint32_t max_lanes, ui
 
 // Per lane of a segment's decode: two token areas (the first decode, the
 // second) of span_cap(L) tokens each -- a decode of [S - kWarmBits, R + 48)
-// emits at most one token per bit -- and span_cks(L) checkpoints (u64).
+// emits at most one token per bit -- and span_cks(L) checkpoints (u32: the
+// low word of ck_pack; the device decode counts no bytes).
 #ifndef GG_DECODE_WARM_BITS  // (A/B builds: scripts/ab_lib.sh ... -DGG_DECODE_WARM_BITS=0)
 #define GG_DECODE_WARM_BITS 256
 #endif
@@ -984,7 +985,7 @@ GG_HD uint64_t span_cap(uint64_t L, bool tight = false) {
   return ((tight ? bits / 4 + 64 : bits) + 3) / 4 * 4;
 }
 GG_HD uint64_t span_cks(uint64_t L) { return (L / kCkBits + 4) & ~1ull; }  // (even: areas stay 16-byte aligned)
-GG_HD uint64_t span_words(uint64_t L, bool tight = false) { return 2 * span_cap(L, tight) + 2 * span_cks(L); }  // (u32 words, even)
+GG_HD uint64_t span_words(uint64_t L, bool tight = false) { return 2 * span_cap(L, tight) + span_cks(L); }  // (u32 words, even)
 // Scratch words the device decode of a segment of seg_bits bits needs (L
 // as span_layout makes it for the segment's longest possible body, or for
 // the longest window of window_bits when the segment is decoded in windows
