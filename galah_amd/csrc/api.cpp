@@ -321,11 +321,22 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   // grid was 8 waves per SIMD against an occupancy of 7 (68 VGPRs) and the
   // last eighth of the work ran as a second, thin round (C3 K1: 56.7 ms at
   // 8, 54.4 at 14, 52.5 at 56, 52.2 at 112, 52.5 at 448).
-  // GALAHGPU_K1_WG_PER_CU overrides it for A/B runs.
-  static const int wg_per_cu = [] {
+  // A smaller launch (an ingest batch of ~200 genomes) takes fewer: each
+  // workgroup first fills its LDS tables, and at 112 per CU a thread of a
+  // 200 x 3 Mbp batch owned ~2 segments (1,000 C2-like files: K1 6.73 ms at
+  // 112 per CU, 5.78 at 28, 5.74 at 14, 5.93 at 7; profiles/r06/k1_grid_ab.txt):
+  // ~15 segments per thread, in multiples of 7 per CU (the occupancy),
+  // between 14 and 112.  GALAHGPU_K1_WG_PER_CU overrides it for A/B runs.
+  static const int wg_env = [] {
     const char* e = getenv("GALAHGPU_K1_WG_PER_CU");
-    return e && *e ? std::max(1, atoi(e)) : 112;
+    return e && *e ? std::max(1, atoi(e)) : 0;
   }();
+  int wg_per_cu = wg_env;
+  if (!wg_per_cu) {
+    const double segs = (double)n_words * 16.0 / (double)seg;  // (an upper bound: runs shorter than k hold none)
+    const double per = segs / (15.0 * 256.0 * std::max(1, n_cu));
+    wg_per_cu = std::min(112, std::max(14, 7 * (int)std::ceil(per / 7.0)));
+  }
   const int grid = std::max(1, n_cu) * wg_per_cu;
 
   uint64_t* d_table;
