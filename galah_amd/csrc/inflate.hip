@@ -1096,8 +1096,14 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
 // serves the next lane.  Traffic: 2 B of sym read and 1 B of text written per
 // byte (the round-5 resolve followed u32 pointers hop by hop over the whole
 // batch: 3.6x its bytes).
-constexpr int kResolveThreads = 512;
-constexpr int kResolveGroups = 4;  // 16-byte groups per thread in flight (their sym loads issued together)
+#ifndef GG_RESOLVE_THREADS  // (A/B builds; 1,000 C2-like files: 512 x 4 groups 3.56 ms, 1024 x 2 2.52, 1024 x 4 2.56, 256 x 8 5.99)
+#define GG_RESOLVE_THREADS 1024
+#endif
+#ifndef GG_RESOLVE_GROUPS
+#define GG_RESOLVE_GROUPS 2
+#endif
+constexpr int kResolveThreads = GG_RESOLVE_THREADS;
+constexpr int kResolveGroups = GG_RESOLVE_GROUPS;  // 16-byte groups per thread in flight (their sym loads issued together)
 __global__ __launch_bounds__(kResolveThreads) void inflate_resolve_kernel(InflatePlace a) {
   __shared__ uint8_t ring[2][kRing];
   const uint32_t u = blockIdx.x, tid = threadIdx.x;
