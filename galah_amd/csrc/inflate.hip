@@ -1191,23 +1191,37 @@ __device__ uint32_t crc_x8n(uint64_t n, const uint32_t* __restrict__ x2k) {  // 
   return p;
 }
 
-// CRC-32 in two kernels: every kCrcSeg-byte segment of every file on its
-// own thread (slicing-by-8, tables in LDS, 16-byte loads), then per file the
-// segments folded in order, crc(A || B) = x^(8|B|) crc(A) ^ crc(B).
+// CRC-32 in two kernels: every kCrcSeg-byte segment of every unit on its own
+// wave -- each lane the CRC (init 0: linear) of 64 contiguous bytes
+// (slicing-by-8, tables in LDS, 16-byte loads), shifted past the bytes after
+// it by one multiplication mod P and XORed over the wave, then the init's
+// term: the segment's standard CRC-32 -- and per unit the segments folded in
+// order, crc(A || B) = x^(8|B|) crc(A) ^ crc(B).  (Round 5 gave each segment
+// one thread, whose 256 16-byte loads in a row a wave issued 4 KB apart:
+// 1.8-1.9 ms per C2-like call.)
 constexpr uint32_t kCrcSeg = kInflateCrcSeg;
+static_assert(kCrcSeg == 64 * 64, "a segment is 64 bytes per lane of one wave");
 constexpr int kCrcThreads = 256;
+struct CrcPowers {
+  uint32_t x2k[64];         // x^(2^k) mod P
+  uint32_t xseg;            // x^(8 kCrcSeg) mod P
+  uint32_t lane_shift[64];  // x^(8 * 64 * (63 - lane)) mod P: a full segment's lane shifted past the lanes after it
+  uint32_t seg_init;        // 0xFFFFFFFF * x^(8 kCrcSeg) mod P: a full segment's init term
+};
 __global__ __launch_bounds__(kCrcThreads) void inflate_crc_seg_kernel(const uint8_t* __restrict__ text,
                                                                       const uint64_t* __restrict__ file_text,
                                                                       const uint64_t* __restrict__ file_len,
                                                                       const uint32_t* __restrict__ seg_first,
                                                                       uint32_t n_files, uint32_t n_segs,
-                                                                      uint32_t* __restrict__ seg_crc) {
+                                                                      uint32_t* __restrict__ seg_crc, CrcPowers pw) {
   __shared__ uint32_t T[8][256];
+  __shared__ uint32_t x2k[64];
   {
     const uint32_t i = threadIdx.x;  // (kCrcThreads == 256: one table index per thread)
     uint32_t c = i;
     for (int k = 0; k < 8; ++k) c = c & 1 ? (c >> 1) ^ kCrcPoly : c >> 1;
     T[0][i] = c;
+    if (i < 64) x2k[i] = pw.x2k[i];
   }
   __syncthreads();
   {  // T[t][i]: byte i followed by t zero bytes
@@ -1219,9 +1233,10 @@ __global__ __launch_bounds__(kCrcThreads) void inflate_crc_seg_kernel(const uint
     }
   }
   __syncthreads();
-  const uint32_t g = blockIdx.x * kCrcThreads + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t g = blockIdx.x * (kCrcThreads / 64) + (threadIdx.x >> 6);  // (uniform per wave)
   if (g >= n_segs) return;
-  uint32_t lo = 0, hi = n_files;  // the file: seg_first[f] <= g < seg_first[f + 1]
+  uint32_t lo = 0, hi = n_files;  // the unit: seg_first[f] <= g < seg_first[f + 1]
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) / 2;
     if (seg_first[mid] <= g) lo = mid;
@@ -1231,24 +1246,35 @@ __global__ __launch_bounds__(kCrcThreads) void inflate_crc_seg_kernel(const uint
   const uint64_t off = (uint64_t)(g - seg_first[f]) * kCrcSeg;
   const uint32_t len = (uint32_t)min<uint64_t>(kCrcSeg, file_len[f] - off);
   const uint8_t* p = text + file_text[f] + off;
-  uint32_t c = 0xFFFFFFFFu;
-  uint32_t i = 0;
-  // (a file's text starts on a 16-byte boundary; a later gzip member's
-  // anywhere: its bytes before the first boundary one at a time)
-  const uint32_t head = min(len, (uint32_t)(16u - ((uint32_t)(uintptr_t)p & 15u)) & 15u);
-  for (; i < head; ++i) c = T[0][(c ^ p[i]) & 0xFFu] ^ (c >> 8);
-  for (; i + 16 <= len; i += 16) {
-    const uint4 v = *(const uint4*)(p + i);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  const uint32_t b0 = 64 * lane, b1 = min(len, b0 + 64);
+  uint32_t c = 0;  // (init 0: this lane's bytes alone)
+  if (b0 < len) {
+    // (a file's text starts on a 16-byte boundary; a later gzip member's
+    // anywhere: such a segment, and a unit's last, partly by bytes)
+    if (b1 - b0 == 64 && ((uintptr_t)(p + b0) & 15u) == 0) {
 #pragma unroll
-    for (int h = 0; h < 4; h += 2) {
-      const uint32_t a = w[h] ^ c, b = w[h + 1];
-      c = T[7][a & 0xFFu] ^ T[6][(a >> 8) & 0xFFu] ^ T[5][(a >> 16) & 0xFFu] ^ T[4][a >> 24] ^ T[3][b & 0xFFu] ^
-          T[2][(b >> 8) & 0xFFu] ^ T[1][(b >> 16) & 0xFFu] ^ T[0][b >> 24];
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = *(const uint4*)(p + b0 + 16 * q);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int h = 0; h < 4; h += 2) {
+          const uint32_t a = w[h] ^ c, b = w[h + 1];
+          c = T[7][a & 0xFFu] ^ T[6][(a >> 8) & 0xFFu] ^ T[5][(a >> 16) & 0xFFu] ^ T[4][a >> 24] ^ T[3][b & 0xFFu] ^
+              T[2][(b >> 8) & 0xFFu] ^ T[1][(b >> 16) & 0xFFu] ^ T[0][b >> 24];
+        }
+      }
+    } else {
+      for (uint32_t i = b0; i < b1; ++i) c = T[0][(c ^ p[i]) & 0xFFu] ^ (c >> 8);
     }
+    // shifted past the segment's bytes after this lane's
+    c = crc_mul(len == kCrcSeg ? pw.lane_shift[lane] : crc_x8n(len - b1, x2k), c);
   }
-  for (; i < len; ++i) c = T[0][(c ^ p[i]) & 0xFFu] ^ (c >> 8);
-  seg_crc[g] = ~c;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o);
+  if (lane == 0) {
+    const uint32_t init = len == kCrcSeg ? pw.seg_init : crc_mul(crc_x8n(len, x2k), 0xFFFFFFFFu);
+    seg_crc[g] = ~(c ^ init);
+  }
 }
 
 // One workgroup per file: each thread folds a contiguous run of the file's
@@ -1257,10 +1283,6 @@ __global__ __launch_bounds__(kCrcThreads) void inflate_crc_seg_kernel(const uint
 // runs at once (no tree of dependent rounds).  x^(2^k) mod P comes from the
 // host (a serial chain of 64 squarings each workgroup once began with).
 constexpr int kFoldThreads = 256;
-struct CrcPowers {
-  uint32_t x2k[64];  // x^(2^k) mod P
-  uint32_t xseg;     // x^(8 kCrcSeg) mod P
-};
 __global__ __launch_bounds__(kFoldThreads) void inflate_crc_fold_kernel(const uint8_t* __restrict__ text,
                                                                         const uint64_t* __restrict__ file_text,
                                                                         const uint64_t* __restrict__ file_len,
@@ -1315,11 +1337,16 @@ const CrcPowers& crc_powers() {
       x.x2k[k] = p;
       p = crc_mul_host(p, p);
     }
-    uint32_t r = 1u << 31;  // x^(8 kCrcSeg): the bits of 8 kCrcSeg
-    uint64_t n = 8ull * kCrcSeg;
-    for (int k = 0; n; ++k, n >>= 1)
-      if (n & 1) r = crc_mul_host(x.x2k[k], r);
-    x.xseg = r;
+    auto x8n = [&](uint64_t bytes) {  // x^(8 bytes) mod P
+      uint32_t r = 1u << 31;
+      uint64_t n = 8ull * bytes;
+      for (int k = 0; n; ++k, n >>= 1)
+        if (n & 1) r = crc_mul_host(x.x2k[k], r);
+      return r;
+    };
+    x.xseg = x8n(kCrcSeg);
+    for (int l = 0; l < 64; ++l) x.lane_shift[l] = x8n(64ull * (63 - l));
+    x.seg_init = crc_mul_host(x.xseg, 0xFFFFFFFFu);
     return x;
   }();
   return pw;
@@ -1419,8 +1446,9 @@ hipError_t launch_inflate_crc(const uint8_t* text, uint32_t n_files, const uint6
                               const uint32_t* seg_first, uint32_t n_segs, uint32_t* seg_crc, uint32_t* crc,
                               hipStream_t st) {
   if (n_segs)
-    hipLaunchKernelGGL(inflate_crc_seg_kernel, dim3((n_segs + kCrcThreads - 1) / kCrcThreads), dim3(kCrcThreads), 0,
-                       st, text, file_text, file_len, seg_first, n_files, n_segs, seg_crc);
+    hipLaunchKernelGGL(inflate_crc_seg_kernel, dim3((n_segs + kCrcThreads / 64 - 1) / (kCrcThreads / 64)),
+                       dim3(kCrcThreads), 0, st, text, file_text, file_len, seg_first, n_files, n_segs, seg_crc,
+                       crc_powers());
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (n_files)
