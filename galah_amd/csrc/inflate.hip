@@ -926,7 +926,10 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
 }
 
 // One workgroup per segment, its output built in order in steps of up to
-// kExpandThreads tokens / kExpandBytes bytes.  The segment's last 32 KB of
+// kExpandThreads tokens / kExpandBytes bytes (this form, one token per
+// thread, is the A/B alternative, GG_EXPAND_TPT=1; the default,
+// inflate_expand2_kernel below, takes three tokens per thread and step and
+// the same ring).  The segment's last 32 KB of
 // output stay in an LDS ring in sym's form (u16 per byte: a literal, or
 // kSymPtr | the position mod 32 KB of a byte before the segment), so every
 // back-reference inside the segment is an LDS read: a step's bytes are
@@ -1084,6 +1087,144 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
   if (bad) atomicOr(a.flags, 1u);
   if (base != lim && tid == 0) atomicOr(a.flags, 4u);
 }
+
+#ifndef GG_EXPAND_TPT  // (A/B builds; 1,000 C2-like files: 1 token per thread 13.9 ms, 2 (6,000-byte steps) 11.1, 3 (8,000) 10.8, 4 (8,000) 12.1)
+#define GG_EXPAND_TPT 3
+#endif
+#ifndef GG_EXPAND_TBYTES  // (the step's bytes with GG_EXPAND_TPT > 1)
+#define GG_EXPAND_TBYTES 8000
+#endif
+#if GG_EXPAND_TPT > 1
+// The expand with kTpt tokens per thread and step (steps of up to 512 kTpt
+// tokens / kTBytes bytes: a third of the steps, barriers and scans per
+// segment of FASTA; 13.9 -> 10.8 ms per 1,000 C2-like files,
+// profiles/r06/expand_tpt_ab.txt); the tokens are prefetched into registers
+// a step ahead (the LDS has no room for a token buffer next to 16 KB of step
+// bytes and the 64 KB ring: 81,832 bytes, two workgroups per CU).
+constexpr int kTpt = GG_EXPAND_TPT;
+constexpr uint32_t kTBytes = GG_EXPAND_TBYTES;
+constexpr uint16_t kStepRef2 = 0x4000u;  // step entry: the value of step byte (entry & 0x3FFF)
+static_assert(kTBytes <= 0x4000, "14-bit step references");
+__global__ __launch_bounds__(kExpandThreads) void inflate_expand2_kernel(InflatePlace a) {
+  __shared__ uint16_t v[kTBytes];
+  __shared__ uint16_t ring[kRing];
+  __shared__ uint32_t s_take, s_bytes;
+  __shared__ uint32_t wsum[kExpandThreads / 64];
+  const uint32_t seg = blockIdx.x;
+  const uint32_t tid = threadIdx.x, ln = tid & 63u, wave = tid >> 6;
+  const uint32_t* tok = a.tok + a.tok_off[seg];
+  const uint64_t n = a.n_tok[seg];
+  const uint64_t o0 = a.lane_out[seg];
+  const uint64_t f0 = a.file_text[a.lane_file[seg]];
+  const uint64_t lim = o0 + a.lane_len[seg];
+  const uint64_t nl = n ? n - 1 : 0;
+  uint64_t base = o0;
+  bool bad = false;
+  uint32_t nx[kTpt];
+#pragma unroll
+  for (int k = 0; k < kTpt; ++k) nx[k] = tok[min<uint64_t>((uint64_t)kTpt * tid + k, nl)];
+  auto fill = [&](uint32_t tk, uint32_t len, uint32_t before) {
+    if (!tok_is_match(tk)) {
+      v[before] = (uint16_t)(tk & 0xFFu);
+      return;
+    }
+    const uint32_t dist = tok_dist(tk);
+    const uint64_t p = base + before;
+    if (p < f0 + dist) {
+      bad = true;
+      for (uint32_t k = 0; k < len; ++k) v[before + k] = (uint16_t)'\n';
+      return;
+    }
+    const uint64_t src = p - dist;
+    for (uint32_t k = 0; k < len; ++k) {
+      const uint64_t s = src + k;
+      uint16_t x;
+      if (s >= base) x = (uint16_t)(kStepRef2 | (uint32_t)(s - base));
+      else if (s < o0) x = (uint16_t)(kSymPtr | ((uint32_t)s & (kRing - 1)));
+      else x = ring[(uint32_t)s & (kRing - 1)];
+      v[before + k] = x;
+    }
+  };
+  for (uint64_t t0 = 0; t0 < n;) {
+    const uint64_t ti = t0 + (uint64_t)kTpt * tid;
+    uint32_t tk[kTpt], l[kTpt];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kTpt; ++k) {
+      tk[k] = nx[k];
+      l[k] = ti + k < n ? tok_len(tk[k]) : 0u;
+      sum += l[k];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (ln >= (uint32_t)o) inc += y;
+    }
+    if (ln == 63) wsum[wave] = inc;
+    if (tid == 0) {
+      s_take = 0;
+      s_bytes = 0;
+    }
+    __syncthreads();
+    for (uint32_t w = 0; w < wave; ++w) inc += wsum[w];
+    uint32_t bef[kTpt];
+    bool take[kTpt];
+    uint32_t c = 0, mine = 0;
+    {
+      uint32_t at = inc - sum;
+#pragma unroll
+      for (int k = 0; k < kTpt; ++k) {
+        bef[k] = at;
+        at += l[k];
+        take[k] = ti + k < n && at <= kTBytes;  // (the taken tokens are a prefix)
+        c += (uint32_t)__popcll(__ballot(take[k]));
+        if (take[k]) mine = at;
+      }
+    }
+    uint32_t mx = mine;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, o));
+    if (c && ln == 0) {
+      atomicAdd(&s_take, c);
+      atomicMax(&s_bytes, mx);
+    }
+#pragma unroll
+    for (int k = 0; k < kTpt; ++k)
+      if (take[k]) fill(tk[k], l[k], bef[k]);
+    __syncthreads();
+    const uint32_t nb = s_bytes, nt = s_take;
+    {
+      const uint64_t tn = t0 + nt + (uint64_t)kTpt * tid;  // the next step's tokens (in flight during this step's LDS work)
+#pragma unroll
+      for (int k = 0; k < kTpt; ++k) nx[k] = tok[min(tn + k, nl)];
+    }
+    for (;;) {
+      bool more = false;
+      for (uint32_t i = tid; i < nb; i += kExpandThreads) {
+        const uint32_t x = v[i];
+        if ((x & 0xC000u) == kStepRef2) {
+          const uint32_t y = v[x & 0x3FFFu];
+          v[i] = (uint16_t)y;
+          more |= (y & 0xC000u) == kStepRef2;
+        }
+      }
+      if (!__syncthreads_or(more)) break;
+    }
+    const uint32_t nw = base + nb <= lim ? nb : base < lim ? (uint32_t)(lim - base) : 0u;
+    for (uint32_t i = tid; i < nw; i += kExpandThreads) {
+      const uint16_t x = v[i];
+      a.sym[base + i] = x;
+      ring[(uint32_t)(base + i) & (kRing - 1)] = x;
+    }
+    __syncthreads();
+    base += nb;
+    t0 += nt;
+  }
+  if (bad) atomicOr(a.flags, 1u);
+  if (base != lim && tid == 0) atomicOr(a.flags, 4u);
+}
+#endif
 
 // One workgroup per unit (gzip member): its lanes' bytes in order, the
 // unit's last 32 KB of text in an LDS ring (position & 0x7FFF).  A lane's
@@ -1433,7 +1574,11 @@ hipError_t launch_inflate_decode(const InflateDecode& a, hipStream_t st) {
 }
 
 hipError_t launch_inflate_expand(const InflatePlace& a, hipStream_t st) {
+#if GG_EXPAND_TPT > 1
+  if (a.n_lanes) hipLaunchKernelGGL(inflate_expand2_kernel, dim3(a.n_lanes), dim3(kExpandThreads), 0, st, a);
+#else
   if (a.n_lanes) hipLaunchKernelGGL(inflate_expand_kernel, dim3(a.n_lanes), dim3(kExpandThreads), 0, st, a);
+#endif
   return hipGetLastError();
 }
 
