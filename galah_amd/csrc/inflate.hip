@@ -52,7 +52,10 @@ struct ClLds {
 constexpr int kSearchWaves = 4;         // chunks per search workgroup (one wave each)
 constexpr uint32_t kSearchStep = 4096;  // positions per step: 64 consecutive per lane
 constexpr uint32_t kSearchCands = 256;  // candidates listed at most (more: the scan resumes after the last listed)
-constexpr uint32_t kCheckAt = 48;       // candidates that trigger a round of full checks (~1 per 1,100 positions)
+#ifndef GG_CHECK_AT  // (A/B builds: -DGG_CHECK_AT=...)
+#define GG_CHECK_AT 48
+#endif
+constexpr uint32_t kCheckAt = GG_CHECK_AT;  // candidates that trigger a round of full checks (~1 per 1,100 positions)
 constexpr uint32_t kWinWords = kSearchStep / 32 + 8;  // a step's bits plus the 160 after its first lane's last
 #ifndef GG_CHK_LDS  // (A/B builds: -DGG_CHK_LDS=1, a round's stream copied to LDS first: search 7.7 -> 8.8-9.0 ms per 600 C2-like files)
 #define GG_CHK_LDS 0
