@@ -1546,7 +1546,18 @@ hipError_t launch_slot_upload(uint8_t* dst, const uint8_t* src_mapped, uint64_t 
   // kernel (GALAHGPU_GZ_UPLOAD_BLOCKS, GALAHGPU_GZ_UPLOAD_NT=1: its workgroups,
   // non-temporal accesses -- A/B knobs, read per call).
   const char* mode = getenv("GALAHGPU_GZ_UPLOAD");
-  if (!(mode && strcmp(mode, "kernel") == 0)) return hipMemcpyAsync(dst, src_mapped, bytes, hipMemcpyHostToDevice, st);
+  if (!(mode && strcmp(mode, "kernel") == 0)) {
+    // (GALAHGPU_GZ_UPLOAD_CHUNK_MB: the copy in pieces of that size, so that
+    // the lanes' small copies queued on the DMA engines behind it wait for one
+    // piece at most -- an A/B knob)
+    const char* ec = getenv("GALAHGPU_GZ_UPLOAD_CHUNK_MB");
+    const uint64_t chunk = ec && atoi(ec) > 0 ? (uint64_t)atoi(ec) << 20 : bytes;
+    for (uint64_t o = 0; o < bytes; o += chunk) {
+      const hipError_t e = hipMemcpyAsync(dst + o, src_mapped + o, std::min(chunk, bytes - o), hipMemcpyHostToDevice, st);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+  }
   const char* eb = getenv("GALAHGPU_GZ_UPLOAD_BLOCKS");
   const uint64_t want = eb && atoi(eb) > 0 ? (uint64_t)atoi(eb) : (uint64_t)kUploadBlocks;
   const uint32_t blocks = (uint32_t)std::min<uint64_t>(want, (n16 + kUploadThreads - 1) / kUploadThreads);
