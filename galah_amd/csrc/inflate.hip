@@ -55,11 +55,11 @@ constexpr uint32_t kSearchCands = 256;  // candidates listed at most (more: the 
 #ifndef GG_CHECK_AT  // (A/B builds: -DGG_CHECK_AT=...)
 #define GG_CHECK_AT 48
 #endif
-constexpr uint32_t kCheckAt = GG_CHECK_AT;
+constexpr uint32_t kCheckAt = GG_CHECK_AT;  // candidates that trigger a round of full checks (~1 per 1,100 positions)
 #ifndef GG_CHECK_STEPS  // (A/B builds; 1,000 C2-like files: 1 step per round (round 5) 9.08 ms, 4 8.14, 8 7.91, 32 7.78)
 #define GG_CHECK_STEPS 32
 #endif
-constexpr uint32_t kCheckSteps = GG_CHECK_STEPS;  // candidates that trigger a round of full checks (~1 per 1,100 positions)
+constexpr uint32_t kCheckSteps = GG_CHECK_STEPS;  // header-walk symbols per round of the checks' bookkeeping
 constexpr uint32_t kWinWords = kSearchStep / 32 + 8;  // a step's bits plus the 160 after its first lane's last
 #ifndef GG_CHK_LDS  // (A/B builds: -DGG_CHK_LDS=1, a round's stream copied to LDS first: search 7.7 -> 8.8-9.0 ms per 600 C2-like files)
 #define GG_CHK_LDS 0
