@@ -1114,6 +1114,10 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand_kernel(InflateP
 constexpr int kTpt = GG_EXPAND_TPT;
 constexpr uint32_t kTBytes = GG_EXPAND_TBYTES;
 constexpr uint16_t kStepRef2 = 0x4000u;  // step entry: the value of step byte (entry & 0x3FFF)
+#ifndef GG_EXPAND_CHASE  // (A/B builds: -DGG_EXPAND_CHASE=1, plain pointer jumping)
+#define GG_EXPAND_CHASE 8
+#endif
+constexpr int kChase = GG_EXPAND_CHASE;
 static_assert(kTBytes <= 0x4000, "14-bit step references");
 __global__ __launch_bounds__(kExpandThreads) void inflate_expand2_kernel(InflatePlace a) {
   __shared__ uint16_t v[kTBytes];
@@ -1209,14 +1213,17 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand2_kernel(Inflate
 #pragma unroll
       for (int k = 0; k < kTpt; ++k) nx[k] = tok[min(tn + k, nl)];
     }
-    for (;;) {
+    for (;;) {  // kStepRef entries followed inside the step (each to an earlier byte): up to
+                // kChase hops per entry and round, then pointer jumping (a run of one byte,
+                // dist 1, makes chains as long as the step)
       bool more = false;
       for (uint32_t i = tid; i < nb; i += kExpandThreads) {
-        const uint32_t x = v[i];
+        uint32_t x = v[i];
         if ((x & 0xC000u) == kStepRef2) {
-          const uint32_t y = v[x & 0x3FFFu];
-          v[i] = (uint16_t)y;
-          more |= (y & 0xC000u) == kStepRef2;
+#pragma unroll
+          for (int h = 0; h < kChase && (x & 0xC000u) == kStepRef2; ++h) x = v[x & 0x3FFFu];
+          v[i] = (uint16_t)x;
+          more |= (x & 0xC000u) == kStepRef2;
         }
       }
       if (!__syncthreads_or(more)) break;
