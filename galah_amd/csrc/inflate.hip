@@ -1118,6 +1118,9 @@ constexpr uint16_t kStepRef2 = 0x4000u;  // step entry: the value of step byte (
 #define GG_EXPAND_CHASE 8
 #endif
 constexpr int kChase = GG_EXPAND_CHASE;
+#ifndef GG_EXPAND_FILL32  // (A/B builds: -DGG_EXPAND_FILL32=0, 64-bit positions and branches per byte)
+#define GG_EXPAND_FILL32 1
+#endif
 static_assert(kTBytes <= 0x4000, "14-bit step references");
 __global__ __launch_bounds__(kExpandThreads) void inflate_expand2_kernel(InflatePlace a) {
   __shared__ uint16_t v[kTBytes];
@@ -1149,6 +1152,22 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand2_kernel(Inflate
       for (uint32_t k = 0; k < len; ++k) v[before + k] = (uint16_t)'\n';
       return;
     }
+#if GG_EXPAND_FILL32
+    // source bytes as 32-bit offsets from the step's first byte (r >= 0: in
+    // the step; r < lo: before the lane), the ring read unconditionally and
+    // the entry picked by selects (the 64-bit compares and branches per byte
+    // made the fill's loop mostly scalar and exec-mask work)
+    const int32_t r0 = (int32_t)before - (int32_t)dist;
+    const int32_t lo = -(int32_t)min<uint64_t>(base - o0, 0x10000u);
+    const uint32_t b32 = (uint32_t)base;
+    for (uint32_t k = 0; k < len; ++k) {
+      const int32_t r = r0 + (int32_t)k;
+      const uint32_t idx = (b32 + (uint32_t)r) & (kRing - 1);
+      const uint32_t y = ring[idx];
+      const uint32_t x = r >= 0 ? (kStepRef2 | (uint32_t)r) : r < lo ? (kSymPtr | idx) : y;
+      v[before + k] = (uint16_t)x;
+    }
+#else
     const uint64_t src = p - dist;
     for (uint32_t k = 0; k < len; ++k) {
       const uint64_t s = src + k;
@@ -1158,6 +1177,7 @@ __global__ __launch_bounds__(kExpandThreads) void inflate_expand2_kernel(Inflate
       else x = ring[(uint32_t)s & (kRing - 1)];
       v[before + k] = x;
     }
+#endif
   };
   for (uint64_t t0 = 0; t0 < n;) {
     const uint64_t ti = t0 + (uint64_t)kTpt * tid;
