@@ -494,7 +494,12 @@ struct LdsCursor {
 // too) and the right one selected, so the lanes of a wave do not split on
 // the symbol kind; the rest (long codes, end-of-block, invalid codes) take
 // decode_span's own handling.
-template <class Emit, class Ck>
+// kFlat (the first decode): ck is called on every symbol as ck(k, c, hit)
+// and records checkpoint k only when hit; k and the next checkpoint move on
+// by selects.  (With 64 lanes some lane reaches a checkpoint on nearly every
+// symbol, so the branch form ran its body, and its exec-mask work, on nearly
+// every symbol anyway.)
+template <bool kFlat = false, class Emit, class Ck>
 __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_t base, uint64_t start, uint64_t s_nom,
                                     uint64_t range_end, LaneTables<LdsStore>& t, Emit&& emit, Ck&& ck, uint32_t& n,
                                     uint64_t& stop) {
@@ -507,7 +512,16 @@ __device__ __forceinline__ uint32_t decode_span_lds(const uint32_t* lds, uint64_
   uint32_t next_stop = next_ck < rend ? next_ck : rend;
   uint32_t st = kSpanBad;
   for (;;) {
-    if (cur.pos >= next_stop) {
+    if constexpr (kFlat) {
+      if (cur.pos >= rend) {
+        st = kSpanRange;
+        break;
+      }
+      const bool hit = cur.pos >= next_ck;
+      ck(k, (uint32_t)ck_pack(cur.pos - next_ck, n, 0), hit);
+      k += hit ? 1u : 0u;
+      next_ck += hit ? kCkBits : 0u;
+    } else if (cur.pos >= next_stop) {
       if (cur.pos >= rend) {
         st = kSpanRange;
         break;
@@ -651,6 +665,9 @@ __device__ uint32_t copy_tokens(uint32_t* __restrict__ dst, const uint32_t* __re
 #define GG_STAGE_KB 10
 #endif
 constexpr uint32_t kStageWords = GG_STAGE_KB * 1024 / 4;
+#ifndef GG_CK_FLAT  // (A/B builds: -DGG_CK_FLAT=0, the first decode's checkpoints behind a branch)
+#define GG_CK_FLAT 1
+#endif
 template <bool kStaged>
 __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decode_kernel(InflateDecode a) {
   extern __shared__ uint32_t stage[];  // (kStaged: kStageWords words)
@@ -778,6 +795,12 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
           sink.on = true;  // (from the first checkpoint on the tokens are kept)
           return true;
         };
+        auto ck1f = [&](uint32_t k, uint32_t c, bool hit) {  // (the same, as decode_span_lds<true> calls it)
+          const bool rec = hit && k < ncks;
+          if (rec) CK(k) = c;
+          nck = rec ? k + 1 : nck;
+          sink.on |= hit;
+        };
         // (a lane after the first starts kWarmBits early, so that its decode
         // has most likely fallen into step with the true symbols by S and its
         // first checkpoint agrees with the lane before: fewer second decodes,
@@ -785,7 +808,11 @@ __global__ __launch_bounds__(kSpanLanes, GG_DECODE_MIN_WAVES) void inflate_decod
         // first checkpoint are dropped as before)
         const uint64_t S0 = j == 0 ? S : (S - bstart > kWarmBits ? S - kWarmBits : bstart);
         uint64_t unused_bytes = 0;
+#if GG_CK_FLAT
+        if constexpr (kStaged) sa = decode_span_lds<true>(stage, sbase, S0, S, R, tab, sink, ck1f, na, Ea);
+#else
         if constexpr (kStaged) sa = decode_span_lds(stage, sbase, S0, S, R, tab, sink, ck1, na, Ea);
+#endif
         else sa = decode_span(in, S0, S, R, tab, sink, ck1, na, unused_bytes, Ea);
         sink.flush();
       }
