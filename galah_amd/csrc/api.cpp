@@ -93,7 +93,9 @@ hipError_t host_scratch(gg_ctx* c, const char* key, size_t bytes, void** out) {
       e.first = nullptr;
       e.second = 0;
     }
-    size_t want = std::max<size_t>(bytes, 4096);
+    // (sized by scratch_hint like scratch(): a later, larger batch of the
+    // call does not regrow it)
+    size_t want = std::max<size_t>(std::max(bytes, (size_t)((double)bytes * c->scratch_hint)), 4096);
     hipError_t err = hipHostMalloc(&e.first, want, hipHostMallocDefault);
     if (err != hipSuccess) return err;
     e.second = want;

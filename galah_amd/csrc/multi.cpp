@@ -336,15 +336,32 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   auto stamp = [&](const char* what) {
     if (dbg) fprintf(stderr, "[parse] %-12s %8.3f ms\n", what, ms_since(t0));
   };
-  std::vector<uint32_t> bfile;
-  std::vector<uint64_t> bstart, bend;
-  for (uint32_t f = 0; f < nf; ++f)
-    for (uint64_t x = foff[f]; x < foff[f + 1]; x += bb) {
-      bfile.push_back(f);
-      bstart.push_back(x);
-      bend.push_back(std::min(foff[f + 1], x + bb));
-    }
-  const uint32_t nb = (uint32_t)bfile.size();
+  // The block tables and every per-block array the host scans live in one
+  // pinned buffer (pageable ones made each copy a staged, blocking one):
+  // bstart, bend, h, h2, hr, hf, boff (nb u64 each), then bfile (nb u32).
+  uint64_t n_blk = 0;
+  for (uint32_t f = 0; f < nf; ++f) n_blk += (foff[f + 1] - foff[f] + bb - 1) / bb;
+  const uint32_t nb = (uint32_t)n_blk;
+  const size_t NBH = std::max(nb, 1u);
+  uint64_t* hbuf;
+  GG_HIP(m, host_scratch_t(m, "parse_host", 7 * NBH + (NBH + 1) / 2, &hbuf));
+  uint64_t* bstart = hbuf;
+  uint64_t* bend = hbuf + NBH;
+  uint64_t* h = hbuf + 2 * NBH;
+  uint64_t* h2 = hbuf + 3 * NBH;
+  uint64_t* hr = hbuf + 4 * NBH;
+  uint64_t* hf = hbuf + 5 * NBH;
+  uint64_t* boff = hbuf + 6 * NBH;
+  uint32_t* bfile = reinterpret_cast<uint32_t*>(hbuf + 7 * NBH);
+  {
+    uint32_t b = 0;
+    for (uint32_t f = 0; f < nf; ++f)
+      for (uint64_t x = foff[f]; x < foff[f + 1]; x += bb, ++b) {
+        bfile[b] = f;
+        bstart[b] = x;
+        bend[b] = std::min(foff[f + 1], x + bb);
+      }
+  }
   runs.clear();
   ParseLaunch p{};
   p.raw = d_text;
@@ -369,11 +386,10 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   p.run_off = blk + 9 * NB;
   p.blk_first = blk + 10 * NB;
   p.file_start = d_fstart;
-  std::vector<uint64_t> h(nb), h2(nb), hr(nb), hf(nb);
   if (nb) {
-    GG_HIP(m, hipMemcpyAsync(d_bfile, bfile.data(), nb * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync((void*)p.blk_start, bstart.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync((void*)p.blk_end, bend.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync(d_bfile, bfile, nb * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync((void*)p.blk_start, bstart, nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync((void*)p.blk_end, bend, nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   }
   GG_HIP(m, hipMemcpyAsync(d_fstart, foff.data(), (nf + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   // pass 1 -> line-start prefix (last '\n' index + 1 before each block)
@@ -381,7 +397,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   uint64_t n_starts = 0;
   if (nb) {
     GG_HIP(m, timed_launch(m, GG_KERNEL_PARSE, foff[nf], st, [&] { return parse_batch_pass(1, p, st); }));
-    GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_nl, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipMemcpyAsync(h, p.blk_nl, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
     stamp("pass 1");
     uint64_t acc = 0;
@@ -390,18 +406,17 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
       h[b] = acc;
       acc = std::max(acc, x);
     }
-    GG_HIP(m, hipMemcpyAsync((void*)p.pre_nl, h.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync((void*)p.pre_nl, h, nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     // pass 2 -> bases, run starts (as if no base before), first byte a base?, last non-dropped byte
     GG_HIP(m, timed_launch(m, GG_KERNEL_PARSE, 0, st, [&] { return parse_batch_pass(2, p, st); }));
-    GG_HIP(m, hipMemcpyAsync(h.data(), p.blk_bases, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    GG_HIP(m, hipMemcpyAsync(h2.data(), p.blk_last, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    GG_HIP(m, hipMemcpyAsync(hr.data(), p.blk_runs, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
-    GG_HIP(m, hipMemcpyAsync(hf.data(), p.blk_first, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipMemcpyAsync(h, p.blk_bases, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipMemcpyAsync(h2, p.blk_last, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipMemcpyAsync(hr, p.blk_runs, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, hipMemcpyAsync(hf, p.blk_first, nb * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
     stamp("pass 2");
     for (uint32_t b = 0; b < nb; ++b) fbases[bfile[b]] += h[b];
     for (uint32_t f = 0; f < nf; ++f) gofs[f + 1] = gofs[f] + (fbases[f] + 15) / 16 * 16;  // genomes on words
-    std::vector<uint64_t> boff(nb);
     uint64_t cur = 0;
     uint32_t cf = ~0u;
     for (uint32_t b = 0; b < nb; ++b) {
@@ -412,7 +427,7 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
       boff[b] = cur;
       cur += h[b];
     }
-    GG_HIP(m, hipMemcpyAsync((void*)p.base_off, boff.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync((void*)p.base_off, boff, nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     // the last non-dropped byte before each block; a block whose first
     // non-dropped byte is a base continues the run of a block before it (in
     // its file) that ended in a base
@@ -427,8 +442,8 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
       hr[b] = n_starts;
       n_starts += runs;
     }
-    GG_HIP(m, hipMemcpyAsync((void*)p.pre_last, h2.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync((void*)p.run_off, hr.data(), nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync((void*)p.pre_last, h2, nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, hipMemcpyAsync((void*)p.run_off, hr, nb * sizeof(uint64_t), hipMemcpyHostToDevice, st));
   }
   const uint64_t total = gofs[nf];
   *n_words = total / 16;
@@ -438,11 +453,12 @@ gg_status parse_raw_batch(gg_ctx* m, const uint8_t* d_text, const std::vector<ui
   p.starts = starts;
   p.n_words = *n_words;
   p.words = *d_words;
-  std::vector<uint64_t> hs(n_starts);
+  uint64_t* hs;
+  GG_HIP(m, host_scratch_t(m, "parse_starts_host", std::max<uint64_t>(n_starts, 1), &hs));
   if (nb) {
     if (*n_words) GG_HIP(m, hipMemsetAsync(*d_words, 0, *n_words * sizeof(uint32_t), st));
     GG_HIP(m, timed_launch(m, GG_KERNEL_PARSE, 0, st, [&] { return parse_batch_pass(3, p, st); }));
-    if (n_starts) GG_HIP(m, hipMemcpyAsync(hs.data(), starts, n_starts * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    if (n_starts) GG_HIP(m, hipMemcpyAsync(hs, starts, n_starts * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     GG_HIP(m, hipStreamSynchronize(st));
     stamp("pass 3");
   }
