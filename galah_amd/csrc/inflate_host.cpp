@@ -122,6 +122,26 @@ bool inflate_debug() {
     }                                                                            \
     if (_e != hipSuccess) return hip_fail((m), _e, "scratch " key);             \
   } while (0)
+// Small per-batch host <-> device copies go through pinned host scratch, one
+// buffer per call site: pageable copies are staged and block the calling
+// thread (the parse's arrays, pinned: two-lane call 0.0475 -> 0.0456 s,
+// profiles/r06/parse_pinned/).  A site's buffer is written again only after
+// the stream has synchronised (every pass of a batch ends with a sync).
+hipError_t h2d_pinned(gg_ctx* m, const char* key, void* dst, const void* src, size_t bytes, hipStream_t st) {
+  if (!bytes) return hipSuccess;
+  uint8_t* h;
+  const hipError_t e = host_scratch_t(m, key, bytes, &h);
+  if (e != hipSuccess) return e;
+  memcpy(h, src, bytes);
+  return hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, st);
+}
+template <class T>
+hipError_t d2h_pinned(gg_ctx* m, const char* key, T** out, const T* src, size_t count, hipStream_t st) {
+  const hipError_t e = host_scratch_t(m, key, std::max<size_t>(count, 1), out);
+  if (e != hipSuccess || !count) return e;
+  return hipMemcpyAsync(*out, src, count * sizeof(T), hipMemcpyDeviceToHost, st);
+}
+
 // search granularity: the first block start of every chunk is found (48 KB
 // scans ~1/4 of the bits, 16 KB ~2/3: C2 files 0.072 -> 0.064 s per call; a
 // zlib -6 block of FASTA is ~25-27 KB, GNU gzip's ~53 KB); a segment that
@@ -212,13 +232,13 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
   GG_HIP(m, scratch_t(m, "gz_cbit0", std::max(nc, 1u), &d_cbit0));
   GG_HIP(m, scratch_t(m, "gz_start", std::max(nc, 1u), &d_start));
   if (nu) {
-    GG_HIP(m, hipMemcpyAsync(d_fword, fword.data(), nu * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync(d_fbits, fbits.data(), nu * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, h2d_pinned(m, "h_fword", d_fword, fword.data(), nu * sizeof(uint64_t), st));
+    GG_HIP(m, h2d_pinned(m, "h_fbits", d_fbits, fbits.data(), nu * sizeof(uint64_t), st));
   }
-  std::vector<uint64_t> start(nc);
+  uint64_t* start = nullptr;
   if (nc) {
-    GG_HIP(m, hipMemcpyAsync(d_cfile, chunk_file.data(), nc * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync(d_cbit0, chunk_bit0.data(), nc * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, h2d_pinned(m, "h_cfile", d_cfile, chunk_file.data(), nc * sizeof(uint32_t), st));
+    GG_HIP(m, h2d_pinned(m, "h_cbit0", d_cbit0, chunk_bit0.data(), nc * sizeof(uint64_t), st));
     InflateSearch s;
     s.in = (const uint32_t*)d_in;
     s.file_word = d_fword;
@@ -245,7 +265,7 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
               "(%.0f cycles each), %.1f candidates\n", nc, pr[2] / (double)nc, pr[0] / (double)std::max<uint64_t>(pr[2], 1),
               pr[3] / (double)nc, pr[1] / (double)std::max<uint64_t>(pr[3], 1), pr[4] / (double)nc);
     }
-    GG_HIP(m, hipMemcpyAsync(start.data(), d_start, nc * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    GG_HIP(m, d2h_pinned(m, "h_start", &start, (const uint64_t*)d_start, nc, st));
   }
   GG_HIP(m, hipStreamSynchronize(st));
   stamp("copy + search");
@@ -375,8 +395,8 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
     GG_HIP(m, scratch_t(m, "gz_res", (size_t)nl * 4, &d_res));
     std::vector<uint32_t> lf(nl);
     for (uint32_t k = 0; k < nl; ++k) lf[k] = lanes[redo[k]].unit;
-    GG_HIP(m, hipMemcpyAsync(d_arg, arg.data(), arg.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    GG_HIP(m, hipMemcpyAsync(d_lfile, lf.data(), nl * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    GG_HIP(m, h2d_pinned(m, "h_larg", d_arg, arg.data(), arg.size() * sizeof(uint64_t), st));
+    GG_HIP(m, h2d_pinned(m, "h_lfile", d_lfile, lf.data(), nl * sizeof(uint32_t), st));
     InflateDecode d;
     d.in = (const uint32_t*)d_in;
     d.file_word = d_fword;
@@ -419,11 +439,11 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
               (unsigned long long)pr[4], pr[5] / nb, pr[0] / nb, pr[1] / nb, pr[2] / nb, pr[3] / nb,
               pr[7] * us / std::max(nl, 1u), pr[6] * us);
     }
-    std::vector<uint64_t> res((size_t)nl * 4);
-    GG_HIP(m, hipMemcpyAsync(res.data(), d_res, res.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    uint64_t* res;
+    GG_HIP(m, d2h_pinned(m, "h_res", &res, (const uint64_t*)d_res, (size_t)nl * 4, st));
     GG_HIP(m, hipStreamSynchronize(st));
     stamp("decode pass");
-    const uint32_t* r32 = (const uint32_t*)(res.data() + 3 * (size_t)nl);
+    const uint32_t* r32 = (const uint32_t*)(res + 3 * (size_t)nl);
     if (timed_at < m->timed.size()) {  // (timing: the work of a decode pass is the tokens its lanes wrote)
       uint64_t toks_out = 0;
       for (uint32_t k = 0; k < nl; ++k) toks_out += res[k];
@@ -569,7 +589,7 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
   }
   for (size_t l = live.size(); l-- > 0;) ulane[live[l].unit] = (uint32_t)l;  // (every unit has a lane)
   ulane[nu] = (uint32_t)live.size();
-  GG_HIP(m, hipMemcpyAsync(d_ftext, ftext.data(), ftext.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  GG_HIP(m, h2d_pinned(m, "h_ftext", d_ftext, ftext.data(), ftext.size() * sizeof(uint64_t), st));
   std::vector<uint64_t> lv(4 * NL + (NL + 1) / 2, 0);
   for (size_t l = 0; l < live.size(); ++l) {
     lv[l] = lane_out[l];
@@ -578,7 +598,7 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
     lv[3 * NL + l] = live[l].out_len;
     ((uint32_t*)(lv.data() + 4 * NL))[l] = live[l].unit;
   }
-  GG_HIP(m, hipMemcpyAsync(d_lout, lv.data(), lv.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  GG_HIP(m, h2d_pinned(m, "h_lout", d_lout, lv.data(), lv.size() * sizeof(uint64_t), st));
   InflatePlace p;
   p.tok = d_tok;
   p.tok_off = d_lout + NL;
@@ -601,7 +621,7 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
   uint32_t *d_sfirst, *d_scrc;
   GG_HIP(m, scratch_t(m, "gz_sfirst", nu + 1, &d_sfirst));
   GG_HIP(m, scratch_t(m, "gz_scrc", std::max(nseg, 1u), &d_scrc));
-  GG_HIP(m, hipMemcpyAsync(d_sfirst, seg_first.data(), (nu + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+  GG_HIP(m, h2d_pinned(m, "h_sfirst", d_sfirst, seg_first.data(), (nu + 1) * sizeof(uint32_t), st));
   uint64_t* d_eprof = nullptr;
   if (inflate_debug()) {
     GG_HIP(m, scratch_t(m, "gz_eprof", 8, &d_eprof));
@@ -627,8 +647,8 @@ gg_status inflate_plan(gg_ctx* m, const uint8_t* h_in, uint64_t in_bytes, std::v
     if (!fl[f].gz && fl[f].data_len)
       GG_HIP(m, hipMemcpyAsync(*d_text + foff[f], d_in + fl[f].data_off, fl[f].data_len, hipMemcpyDeviceToDevice, st));
   // flags, then per unit its CRC-32 and its first byte
-  std::vector<uint32_t> chk(2 * (size_t)nu + 1);
-  GG_HIP(m, hipMemcpyAsync(chk.data(), d_flags, chk.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  uint32_t* chk;
+  GG_HIP(m, d2h_pinned(m, "h_chk", &chk, (const uint32_t*)d_flags, 2 * (size_t)nu + 1, st));
   GG_HIP(m, hipStreamSynchronize(st));
   stamp("expand + resolve + crc");
   if (chk[0])
