@@ -407,8 +407,14 @@ gg_status sketch_core(gg_ctx* c, const uint32_t* d_words, uint64_t n_words, cons
   if (runs_dev == c->device) {
     d_all_runs = const_cast<gg_run*>(runs);
   } else {
-    if (n_runs)
+    if (n_runs && runs_dev < 0) {  // (a host table through pinned scratch: a pageable copy blocks this thread)
+      gg_run* h_runs;
+      GG_HIP(c, host_scratch_t(c, "runs_h2d", n_runs, &h_runs));
+      memcpy(h_runs, runs, n_runs * sizeof(gg_run));
+      GG_HIP(c, hipMemcpyAsync(d_all_runs, h_runs, n_runs * sizeof(gg_run), hipMemcpyHostToDevice, c->copy_stream));
+    } else if (n_runs) {
       GG_HIP(c, hipMemcpyAsync(d_all_runs, runs, n_runs * sizeof(gg_run), hipMemcpyDefault, c->copy_stream));
+    }
     GG_HIP(c, hipEventRecord(c->copy_done, c->copy_stream));
     GG_HIP(c, hipStreamWaitEvent(st, c->copy_done, 0));
   }

@@ -561,8 +561,11 @@ gg_status run_lane(gg_ctx* x, GzClaims& cl, uint64_t* d_sk, uint32_t* d_len, int
     row_of.resize(ng);
     for (uint32_t q = 0; q < ng; ++q) row_of[q] = cl.row_of[g->idx[q]];
     uint32_t* d_row_of;
+    uint32_t* h_row_of;  // (pinned: a pageable copy blocks this thread; sketch_core syncs before the next batch)
     GG_HIP(x, scratch_t(x, "row_of", ng, &d_row_of));
-    GG_HIP(x, hipMemcpyAsync(d_row_of, row_of.data(), ng * sizeof(uint32_t), hipMemcpyHostToDevice, x->stream));
+    GG_HIP(x, host_scratch_t(x, "row_of_h", std::max<uint32_t>(ng, 1), &h_row_of));
+    std::copy(row_of.begin(), row_of.end(), h_row_of);
+    GG_HIP(x, hipMemcpyAsync(d_row_of, h_row_of, ng * sizeof(uint32_t), hipMemcpyHostToDevice, x->stream));
     const gg_status ks = sketch_core(x, d_words, nw, runs.data(), runs.size(), ng, d_sk, d_len, d_row_of, x->stream);
     if (ks != GG_OK) return ks;
     {
