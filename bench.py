@@ -879,7 +879,7 @@ def run_lib(a, world, rank):
         want_files = a.files if a.files is not None else (a.config == "c3")
         if world == 1 and M == 1 and want_files:
             try:
-                files, files_plain = files_leg(a, devs[0], 5)
+                files, files_plain = files_leg(a, devs[0], 9)
             except Exception as e:  # the headline stands without it
                 files = {"error": "%s: %s" % (type(e).__name__, e)}
         want_c4 = a.c4_leg if a.c4_leg is not None else (a.config == "c3")

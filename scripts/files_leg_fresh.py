@@ -11,6 +11,6 @@ sys.argv = [os.path.join(ROOT, "bench.py")]
 import bench  # noqa: E402
 
 a = bench.parse()
-files, plain = bench.files_leg(a, 0, 5)
+files, plain = bench.files_leg(a, 0, 9)
 files.pop("roofline_ingest", None)
 print(json.dumps({"files": files, "files_plain": plain}))
